@@ -1,0 +1,61 @@
+import base64
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+        return json.load(f)
+
+
+def unb64(s: str) -> np.ndarray:
+    return np.frombuffer(base64.b64decode(s), dtype=np.float64).copy()
+
+
+def unhex(s: str) -> float:
+    return float.fromhex(s)
+
+
+def solve_case(golden, name):
+    for c in golden["solves"]:
+        if c["name"] == name:
+            return c
+    raise KeyError(name)
+
+
+# Stated fp64 parity tolerance ("Stated parity tolerance"):
+#   every k with trace_ref[k]^2 >= 1e-20 * trace_ref[0]^2 must satisfy
+#   |rtrans_gpu - rtrans_ref| <= RTRANS_RTOL * rtrans_ref  (rtrans = normr^2).
+RTRANS_RTOL_1GPU = 1e-8
+RTRANS_RTOL_MULTI = 1e-7
+RTRANS_CUTOFF = 1e-20
+
+
+def check_trace(tr_test, tr_ref, rtol):
+    """Phase-aware trace comparison on rtrans = normr^2. Returns #points checked."""
+    tr_test = np.asarray(tr_test, np.float64)
+    tr_ref = np.asarray(tr_ref, np.float64)
+    r0 = tr_ref[0] ** 2
+    m = min(len(tr_test), len(tr_ref))
+    checked = 0
+    for k in range(m):
+        rr = tr_ref[k] ** 2
+        if rr < RTRANS_CUTOFF * r0:
+            break
+        rt = tr_test[k] ** 2
+        assert abs(rt - rr) <= rtol * rr, (k, rt, rr, abs(rt - rr) / rr)
+        checked += 1
+    return checked
