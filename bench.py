@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""bench.py -- HPCCG on MI355X: CG iterations/s and effective SpMV GB/s.
+
+One *step* = one full HPCCG() solve (HPCCG.cpp:312-402) with max_iter = 500
+(499 CG iterations, tolerance 0: main.cpp:187-188) on the 27-point
+nx = ny = nz = 200 problem per GPU (BASELINE.json configs[2]), matrix, b and
+x resident in HBM before the timed region (device generator).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 200] [--stencil 27]
+
+N > 1: launched by torch.distributed.run, one process per GPU; z-stacked
+slabs (local nz fixed, weak scaling), halo + dot all-reduces over RCCL inside
+libhpccg_hip.so; torch.distributed (gloo) carries only the control plane
+(unique id, barrier, max-over-ranks time).
+
+value = (CG iterations x ranks x K) / max-over-ranks wall time of the K steps
+      = 200^3-slab CG iterations per second summed over GPUs (at N = 1:
+        plain CG iterations/s).
+roofline: the SpMV kernel (84 % of the reference's time);
+  achieved = (12 nnz + 20 n) bytes per launch / average launch duration from
+  hipEvents on the solver stream over the timed steps; peak 8 TB/s.
+cpu_baseline: the reference compiled from its own sources (oracle/_ref, OpenMP)
+  -- or the oracle port if that build is absent -- on a bounded sample of the
+  same problem, rank 0, N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("OMP_NUM_THREADS", "16")
+os.environ.setdefault("OMP_PROC_BIND", "close")
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def load_pkg():
+    import importlib.util
+    name = "hpccg_sycl_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "hpccg-sycl_amd",
+                                                                    "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(nx, ny, nz, use_7pt, budget_s=15.0):
+    """Time the reference (or the oracle port) on the host cores, bounded."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle  # test infrastructure: baseline leg only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libhpccg_ref_omp.so")
+    # sample: the same matrix, first `iters` CG iterations
+    A = oracle.generate(nx, ny, nz, use_7pt=use_7pt)
+    probe = 3
+    if os.path.exists(ref_so) and not use_7pt:
+        kind = "reference"
+        M = oracle.ref_from_csr(A, omp=True)
+        run = lambda mi: oracle.ref_hpccg(M, A.b, max_iter=mi)  # noqa: E731
+    else:
+        kind = "port"
+        run = lambda mi: oracle.hpccg(A, max_iter=mi, nthreads=threads, trace=False)  # noqa: E731
+    # the reference prints residual lines on fd 1: keep bench stdout to one JSON line
+    saved = os.dup(1)
+    null = os.open(os.devnull, os.O_WRONLY)
+    os.dup2(null, 1)
+    try:
+        t = run(probe + 1)["times"][0]
+        per_it = max(t / probe, 1e-6)
+        iters = int(max(5, min(500, budget_s / per_it)))
+        res = run(iters + 1)
+    finally:
+        import ctypes
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(saved, 1)
+        os.close(null)
+        os.close(saved)
+    its = res["niters"] / res["times"][0]
+    return {"value": its, "unit": "CG iterations/s", "cores": threads, "kind": kind,
+            "sample": f"{nx}x{ny}x{nz} {'7' if use_7pt else '27'}-pt, first {res['niters']} CG "
+                      f"iterations of one HPCCG() solve ({res['times'][0]:.1f} s), "
+                      f"OpenMP {threads} threads on the GPU box host"}
+
+
+def pmc_traffic(tag):
+    """HBM bytes per SpMV launch from a committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("spmv_hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=200, help="nx = ny = nz per GPU")
+    ap.add_argument("--stencil", type=int, default=27, choices=[27, 7])
+    ap.add_argument("--max-iter", type=int, default=500)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", type=int, default=-1, help="SpMV kernel variant (-1 auto)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: hipGraph launches, no per-kernel events (roofline from stamps)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    hp = load_pkg()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    hp.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        obj = [hp.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        hp.comm_init(obj[0], world, rank)
+
+    n = args.n
+    use_7pt = args.stencil == 7
+    t0 = time.time()
+    M = hp.Matrix.generate(n, n, n, use_7pt=use_7pt)
+    info = M.info()
+    if args.variant >= 0:
+        M.set_option("spmv_variant", args.variant)
+    M.set_option("event_timing", 0 if args.graph else 1)
+    b, x0, _ = M.vectors()
+    nrow = n * n * n
+    x = torch.zeros(nrow, dtype=torch.float64, device=f"cuda:{local_rank}")
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] setup {time.time() - t0:.2f}s nnz={info['nnz']} slots={info['slots']} "
+        f"variant={info['spmv_variant']}")
+
+    def step():
+        x.zero_()
+        return hp.HPCCG(M, b, x, max_iter=args.max_iter, device=True)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    niters_total = 0
+    spmv_ms = spmv_n = upd_ms = upd_n = 0.0
+    times_acc = [0.0] * 7
+    for _ in range(args.steps):
+        _, it, nr, times = step()
+        niters_total += it
+        kt = M.kernel_times()
+        spmv_ms += kt["spmv_ms"]
+        spmv_n += kt["spmv_launches"]
+        upd_ms += kt["update_ms"]
+        upd_n += kt["update_launches"]
+        for i in range(7):
+            times_acc[i] += times[i]
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    spmv_bytes = 12.0 * info["nnz"] + 20.0 * nrow
+    if spmv_n > 0:
+        spmv_avg_s = spmv_ms / spmv_n * 1e-3
+        timing_src = "hipEvent pairs around every SpMV launch on the solver stream"
+    else:  # graph mode: device-clock stamps (SPARSEMV class time / calls)
+        spmv_avg_s = times_acc[3] / max(1, niters_total + args.steps)
+        timing_src = "s_memrealtime stamps (graph mode)"
+    achieved = spmv_bytes / spmv_avg_s / 1e9
+    it_per_s = niters_total / elapsed  # per rank: every rank runs the same iterations
+    value = it_per_s * world
+    ms_per_step = elapsed / args.steps * 1e3
+    iter_bytes = 12.0 * info["nnz"] + 116.0 * nrow  # unfused reference sequence, SURVEY 8(d)
+
+    if rank == 0:
+        out = {
+            "metric": "CG iterations/sec + effective SpMV GB/s (% HBM peak), 27-pt nx=ny=nz=200",
+            "value": round(value, 3),
+            "unit": "CG iterations/s (per-GPU %d^3 slab iterations, summed over GPUs)" % n,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (generate_matrix stencil on the device; deterministic, no RNG)",
+            "config": {
+                "workload": f"HPCCG solve, {args.stencil}-pt {n}x{n}x{n} per GPU, z-stacked, "
+                            f"max_iter={args.max_iter} (499 CG iterations), tolerance 0",
+                "nx": n, "ny": n, "nz_per_gpu": n, "stencil": args.stencil,
+                "max_iter": args.max_iter, "parallelism": f"z-slab x{world} (RCCL)",
+                "nnz_per_gpu": info["nnz"], "sell_slots_per_gpu": info["slots"],
+                "spmv_variant": info["spmv_variant"],
+            },
+            "cg_iterations_per_s_global": round(it_per_s, 3),
+            "spmv_effective_gbs": round(achieved, 1),
+            "spmv_frac_hbm_peak": round(achieved / HBM_PEAK_GBS, 4),
+            "iteration_effective_gbs": round(iter_bytes * it_per_s / 1e9, 1),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc_traffic(f"spmv_{args.stencil}pt_{n}"),
+                "kernel": "k_spmv (SELL-512 SpMV + fused p.Ap partials)",
+                "bytes_per_launch": spmv_bytes,
+                "avg_launch_us": round(spmv_avg_s * 1e6, 2),
+                "timing": timing_src,
+            },
+            "update_kernel_avg_us": round(upd_ms / upd_n * 1e3, 2) if upd_n else None,
+            "times_per_step_s": {"total": times_acc[0] / args.steps,
+                                 "ddot": times_acc[1] / args.steps,
+                                 "waxpby": times_acc[2] / args.steps,
+                                 "sparsemv": times_acc[3] / args.steps,
+                                 "allreduce": times_acc[4] / args.steps,
+                                 "halo": times_acc[5] / args.steps},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(n, n, n, use_7pt)
+            except Exception as e:  # reported, never silently replaced
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+
+    M.close()
+    if world > 1:
+        hp.comm_destroy()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,372 @@
+"""hpccg_sycl_amd -- Python mirror of the reference HPCCG interface over the
+MI355X C ABI (include/hpccg_hip.h, lib/libhpccg_hip.so).
+
+Names and argument meaning follow the reference (Dart120/HPCCG-SYCL):
+
+* ``generate_matrix(nx, ny, nz, rank=0, size=1, use_7pt=False)`` ->
+  generate_matrix.cpp:196 (host HPC_Sparse_Matrix, global columns)
+* ``Matrix.from_hpc(problem)`` / ``Matrix.from_csr(...)`` / ``Matrix.generate(...)``
+  -> the device-resident matrix HPCCG() reads (HPC_Sparse_Matrix.hpp:54-85)
+* ``HPCCG(M, b, x, max_iter, tolerance)`` -> HPCCG.cpp:312-402, returns
+  ``(ierr, niters, normr, times)`` and updates ``x`` in place
+* ``HPC_sparsemv(M, x, y)``, ``ddot(n, x, y)``, ``waxpby(n, alpha, x, beta, y, w)``
+  -> HPC_sparsemv.cpp:68, ddot.cpp:60, waxpby.cpp:69 on device buffers
+
+There is no CPU fallback: if the HIP library is missing or no GPU is present,
+calls raise (``HPCCGError``). The package directory name contains a hyphen,
+so import it by path (``load()`` below, or importlib).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libhpccg_hip.so")
+CLI_PATH = os.path.join(HERE, "bin", "test_HPCCG")
+ROOT = os.path.dirname(HERE)
+
+_lib = None
+
+
+class HPCCGError(RuntimeError):
+    pass
+
+
+def build(jobs: int = 8) -> None:
+    """Compile the gfx950 library and CLI in-tree (hipcc cross-compiles)."""
+    subprocess.run(["make", "-s", "-C", HERE, f"-j{jobs}"], check=True)
+
+
+class _HPCMatrix(C.Structure):
+    """HPC_Sparse_Matrix (HPC_Sparse_Matrix.hpp:54-85, non-MPI layout)."""
+    _fields_ = [
+        ("title", C.c_char_p), ("start_row", C.c_int), ("stop_row", C.c_int),
+        ("total_nrow", C.c_int), ("total_nnz", C.c_longlong), ("local_nrow", C.c_int),
+        ("local_ncol", C.c_int), ("local_nnz", C.c_int), ("nnz_in_row", C.POINTER(C.c_int)),
+        ("ptr_to_vals_in_row", C.POINTER(C.POINTER(C.c_double))),
+        ("ptr_to_inds_in_row", C.POINTER(C.POINTER(C.c_int))),
+        ("ptr_to_diags", C.POINTER(C.POINTER(C.c_double))),
+        ("list_of_vals", C.POINTER(C.c_double)), ("list_of_inds", C.POINTER(C.c_int)),
+    ]
+
+
+def lib() -> C.CDLL:
+    """Load libhpccg_hip.so (import torch first so one HIP runtime is shared)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HPCCGError(f"{LIB_PATH} missing: run build() (the HIP path has no CPU fallback)")
+    try:  # share torch's HIP runtime when torch is around (same sonames)
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    vp, ip, dp, lp = C.c_void_p, C.c_int, C.c_double, C.c_longlong
+    PI, PD = C.POINTER(C.c_int), C.POINTER(C.c_double)
+    sig = {
+        "hpccg_hip_abi_version": (ip, []),
+        "hpccg_hip_last_error": (C.c_char_p, []),
+        "hpccg_hip_device_count": (ip, [PI]),
+        "hpccg_hip_set_device": (ip, [ip]),
+        "hpccg_hip_comm_unique_id": (ip, [C.c_char_p]),
+        "hpccg_hip_comm_init": (ip, [C.c_char_p, ip, ip]),
+        "hpccg_hip_comm_destroy": (ip, []),
+        "hpccg_hip_comm_size": (ip, [PI, PI]),
+        "hpccg_hip_comm_allreduce_host": (ip, [PD, ip, ip]),
+        "hpccg_hip_device_name": (ip, [C.c_char_p, ip, PI]),
+        "hpccg_generate_matrix": (ip, [ip, ip, ip, ip, ip, ip, C.POINTER(C.POINTER(_HPCMatrix)),
+                                       C.POINTER(PD), C.POINTER(PD), C.POINTER(PD)]),
+        "hpccg_free_problem": (None, [C.POINTER(_HPCMatrix), PD, PD, PD]),
+        "hpccg_hip_matrix_create": (ip, [C.POINTER(_HPCMatrix), C.POINTER(vp)]),
+        "hpccg_hip_matrix_create_csr": (ip, [ip, ip, ip, vp, vp, vp, C.POINTER(vp)]),
+        "hpccg_hip_matrix_generate": (ip, [ip, ip, ip, ip, C.POINTER(vp)]),
+        "hpccg_hip_matrix_destroy": (ip, [vp]),
+        "hpccg_hip_matrix_info": (ip, [vp, C.POINTER(lp)]),
+        "hpccg_hip_matrix_vectors": (ip, [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]),
+        "hpccg_hip_solve": (ip, [vp, vp, vp, ip, dp, PI, PD, PD, ip]),
+        "hpccg_hip_solve_device": (ip, [vp, vp, vp, ip, dp, PI, PD, PD, ip]),
+        "hpccg_hip_last_trace": (ip, [vp, PD, ip]),
+        "hpccg_hip_set_option": (ip, [vp, C.c_char_p, lp]),
+        "hpccg_hip_kernel_times": (ip, [vp, PD]),
+        "hpccg_hip_sparsemv": (ip, [vp, vp, vp]),
+        "hpccg_hip_ddot": (ip, [ip, vp, vp, PD]),
+        "hpccg_hip_waxpby": (ip, [ip, dp, vp, dp, vp, vp]),
+        "hpccg_hip_HPCCG": (ip, [C.POINTER(_HPCMatrix), vp, vp, ip, dp, PI, PD, PD]),
+        "hpccg_sell_build": (lp, [ip, lp, lp, vp, vp, vp, vp, vp, vp]),
+        "hpccg_halo_plan": (ip, [ip, ip, ip, vp, vp, PI]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def exported_symbols() -> list[str]:
+    """Functions include/hpccg_hip.h declares (checked by the CPU suite)."""
+    import re
+    with open(os.path.join(ROOT, "include", "hpccg_hip.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(hpccg_\w+)\s*\(", text)))
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().hpccg_hip_last_error().decode(errors="replace")
+        raise HPCCGError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(a) -> int:
+    """Device pointer of a torch tensor (or an int)."""
+    if isinstance(a, int):
+        return a
+    return a.data_ptr()
+
+
+# ---------------------------------------------------------------------------
+# host problem (reference generate_matrix)
+# ---------------------------------------------------------------------------
+class Problem:
+    """A host HPC_Sparse_Matrix with x0, b, xexact (owned; freed on close)."""
+
+    def __init__(self, A, x, b, xe, nrow):
+        self.A, self._x, self._b, self._xe, self.nrow = A, x, b, xe, nrow
+
+    @property
+    def x(self) -> np.ndarray:
+        return np.ctypeslib.as_array(self._x, (self.nrow,)).copy()
+
+    @property
+    def b(self) -> np.ndarray:
+        return np.ctypeslib.as_array(self._b, (self.nrow,)).copy()
+
+    @property
+    def xexact(self) -> np.ndarray:
+        return np.ctypeslib.as_array(self._xe, (self.nrow,)).copy()
+
+    def to_csr(self):
+        """(row_ptr int64, cols int32, vals float64) in stored entry order."""
+        A = self.A.contents
+        n = A.local_nrow
+        lens = np.ctypeslib.as_array(A.nnz_in_row, (n,)).astype(np.int64)
+        row_ptr = np.zeros(n + 1, np.int64)
+        np.cumsum(lens, out=row_ptr[1:])
+        nnz = int(row_ptr[-1])
+        base_v = C.cast(A.list_of_vals, C.c_void_p).value
+        base_i = C.cast(A.list_of_inds, C.c_void_p).value
+        vals = np.ctypeslib.as_array(A.list_of_vals, (nnz,)).copy()
+        cols = np.ctypeslib.as_array(A.list_of_inds, (nnz,)).copy()
+        # rows are laid out back to back from list_of_* (generate_matrix.cpp:247-258)
+        first_v = C.cast(A.ptr_to_vals_in_row[0], C.c_void_p).value if n else base_v
+        first_i = C.cast(A.ptr_to_inds_in_row[0], C.c_void_p).value if n else base_i
+        assert first_v == base_v and first_i == base_i
+        return row_ptr, cols, vals
+
+    def close(self):
+        if self.A:
+            lib().hpccg_free_problem(self.A, self._x, self._b, self._xe)
+            self.A = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def generate_matrix(nx, ny, nz, rank=0, size=1, use_7pt=False) -> Problem:
+    L = lib()
+    A = C.POINTER(_HPCMatrix)()
+    x, b, xe = C.POINTER(C.c_double)(), C.POINTER(C.c_double)(), C.POINTER(C.c_double)()
+    _check(L.hpccg_generate_matrix(nx, ny, nz, rank, size, int(use_7pt), C.byref(A), C.byref(x),
+                                   C.byref(b), C.byref(xe)), "generate_matrix")
+    return Problem(A, x, b, xe, nx * ny * nz)
+
+
+# ---------------------------------------------------------------------------
+# device matrix
+# ---------------------------------------------------------------------------
+class Matrix:
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def from_hpc(cls, prob: Problem) -> "Matrix":
+        h = C.c_void_p()
+        _check(lib().hpccg_hip_matrix_create(prob.A, C.byref(h)), "matrix_create")
+        return cls(h)
+
+    @classmethod
+    def from_csr(cls, row_ptr, cols, vals, start_row=0, total_nrow=None) -> "Matrix":
+        row_ptr = np.ascontiguousarray(row_ptr, np.int64)
+        cols = np.ascontiguousarray(cols, np.int32)
+        vals = np.ascontiguousarray(vals, np.float64)
+        n = len(row_ptr) - 1
+        total = n if total_nrow is None else total_nrow
+        h = C.c_void_p()
+        _check(lib().hpccg_hip_matrix_create_csr(n, start_row, total, row_ptr.ctypes.data,
+                                                 cols.ctypes.data, vals.ctypes.data, C.byref(h)),
+               "matrix_create_csr")
+        return cls(h)
+
+    @classmethod
+    def generate(cls, nx, ny, nz, use_7pt=False) -> "Matrix":
+        h = C.c_void_p()
+        _check(lib().hpccg_hip_matrix_generate(nx, ny, nz, int(use_7pt), C.byref(h)),
+               "matrix_generate")
+        return cls(h)
+
+    def info(self) -> dict:
+        a = (C.c_longlong * 8)()
+        _check(lib().hpccg_hip_matrix_info(self.h, a), "matrix_info")
+        return {"nrow": a[0], "ncol": a[1], "nnz": a[2], "slots": a[3], "ghost_lo": a[4],
+                "ghost_hi": a[5], "spmv_variant": a[6], "uniform_width": a[7]}
+
+    def vectors(self):
+        """Device pointers (b, x0, xexact) of a device-generated matrix."""
+        b, x0, xe = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        _check(lib().hpccg_hip_matrix_vectors(self.h, C.byref(b), C.byref(x0), C.byref(xe)),
+               "matrix_vectors")
+        return b.value, x0.value, xe.value
+
+    def set_option(self, key: str, value: int) -> None:
+        _check(lib().hpccg_hip_set_option(self.h, key.encode(), int(value)), "set_option")
+
+    def kernel_times(self) -> dict:
+        """hipEvent timings of the last solve (needs set_option('event_timing', 1))."""
+        out = (C.c_double * 4)()
+        _check(lib().hpccg_hip_kernel_times(self.h, out), "kernel_times")
+        return {"spmv_ms": out[0], "spmv_launches": int(out[1]), "update_ms": out[2],
+                "update_launches": int(out[3])}
+
+    def last_trace(self, cap: int = 100000) -> np.ndarray:
+        out = np.zeros(cap, np.float64)
+        n = lib().hpccg_hip_last_trace(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), cap)
+        return out[:max(n, 0)]
+
+    def close(self):
+        if self.h:
+            lib().hpccg_hip_matrix_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def HPCCG(M: Matrix, b, x, max_iter: int = 500, tolerance: float = 0.0, print_residuals=False,
+          device=False):
+    """HPCCG.cpp:312-402. b, x: numpy (host) or, with device=True, device
+    pointers/tensors. x is updated in place. Returns (ierr, niters, normr, times)."""
+    it = C.c_int(0)
+    nr = C.c_double(0.0)
+    times = np.zeros(7, np.float64)
+    tp = times.ctypes.data_as(C.POINTER(C.c_double))
+    L = lib()
+    if device:
+        rc = L.hpccg_hip_solve_device(M.h, _ptr(b), _ptr(x), max_iter, tolerance, C.byref(it),
+                                      C.byref(nr), tp, int(print_residuals))
+    else:
+        assert x.dtype == np.float64 and x.flags.c_contiguous
+        bb = np.ascontiguousarray(b, np.float64)
+        rc = L.hpccg_hip_solve(M.h, bb.ctypes.data, x.ctypes.data, max_iter, tolerance,
+                               C.byref(it), C.byref(nr), tp, int(print_residuals))
+    _check(rc, "HPCCG")
+    return rc, it.value, nr.value, times
+
+
+def HPC_sparsemv(M: Matrix, x, y) -> int:
+    _check(lib().hpccg_hip_sparsemv(M.h, _ptr(x), _ptr(y)), "HPC_sparsemv")
+    return 0
+
+
+def ddot(n: int, x, y) -> float:
+    r = C.c_double(0.0)
+    _check(lib().hpccg_hip_ddot(n, _ptr(x), _ptr(y), C.byref(r)), "ddot")
+    return r.value
+
+
+def waxpby(n: int, alpha: float, x, beta: float, y, w) -> int:
+    _check(lib().hpccg_hip_waxpby(n, alpha, _ptr(x), beta, _ptr(y), _ptr(w)), "waxpby")
+    return 0
+
+
+def device_count() -> int:
+    c = C.c_int(0)
+    lib().hpccg_hip_device_count(C.byref(c))
+    return c.value
+
+
+def set_device(d: int) -> None:
+    _check(lib().hpccg_hip_set_device(d), "set_device")
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    _check(lib().hpccg_hip_comm_unique_id(buf), "comm_unique_id")
+    return buf.raw
+
+
+def comm_init(uid: bytes, nranks: int, rank: int) -> None:
+    _check(lib().hpccg_hip_comm_init(uid, nranks, rank), "comm_init")
+
+
+def comm_destroy() -> None:
+    lib().hpccg_hip_comm_destroy()
+
+
+def device_name() -> tuple[str, int]:
+    buf = C.create_string_buffer(256)
+    cus = C.c_int(0)
+    _check(lib().hpccg_hip_device_name(buf, 256, C.byref(cus)), "device_name")
+    return buf.value.decode(), cus.value
+
+
+# ---------------------------------------------------------------------------
+# host-only helpers (no GPU)
+# ---------------------------------------------------------------------------
+SLICE_ROWS = 512
+
+
+def sell_build(row_ptr, cols, vals, col_base=0, ncol_ext=None):
+    """SELL-512 image the device uses: (slice_base, sell_cols, sell_vals)."""
+    row_ptr = np.ascontiguousarray(row_ptr, np.int64)
+    cols = np.ascontiguousarray(cols, np.int32)
+    vals = np.ascontiguousarray(vals, np.float64)
+    n = len(row_ptr) - 1
+    ncol_ext = n if ncol_ext is None else ncol_ext
+    ns = (n + SLICE_ROWS - 1) // SLICE_ROWS
+    sb = np.zeros(ns + 1, np.uint32)
+    L = lib()
+    slots = L.hpccg_sell_build(n, col_base, ncol_ext, row_ptr.ctypes.data, cols.ctypes.data,
+                               vals.ctypes.data, sb.ctypes.data, None, None)
+    sc = np.zeros(max(int(slots), 1), np.int32)
+    sv = np.zeros(max(int(slots), 1), np.float64)
+    r = L.hpccg_sell_build(n, col_base, ncol_ext, row_ptr.ctypes.data, cols.ctypes.data,
+                           vals.ctypes.data, sb.ctypes.data, sc.ctypes.data, sv.ctypes.data)
+    if r < 0:
+        raise HPCCGError("sell_build: column outside the halo plan")
+    return sb, sc[:slots], sv[:slots]
+
+
+def halo_plan(row_ptr, cols, start_row, total_nrow):
+    row_ptr = np.ascontiguousarray(row_ptr, np.int64)
+    cols = np.ascontiguousarray(cols, np.int32)
+    out = (C.c_int * 4)()
+    _check(lib().hpccg_halo_plan(len(row_ptr) - 1, start_row, total_nrow, row_ptr.ctypes.data,
+                                 cols.ctypes.data, out), "halo_plan")
+    return {"ghost_lo": out[0], "ghost_hi": out[1], "min_col": out[2], "max_col": out[3]}
+
+
+def load():
+    """Return this module (for callers that import the package by path)."""
+    import sys
+    return sys.modules[__name__]

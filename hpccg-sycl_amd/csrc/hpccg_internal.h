@@ -1,0 +1,85 @@
+// hpccg_internal.h -- shared between the kernel TU (hpccg_kernels.hip) and the
+// host orchestration TU (hpccg_solver.cpp). Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace hpccg {
+
+// SELL-C layout: C rows per slice, slot-major inside a slice. C is fixed so
+// that one workgroup owns exactly one slice in every CG kernel, which keeps
+// the per-slice dot partials of every kernel aligned (deterministic sums).
+constexpr int kSliceRows = 512;
+constexpr int kNumXcd = 8;        // MI355X: 8 XCDs, blocks dealt round-robin
+constexpr int kFinalizeThreads = 1024;
+
+// Indices into the device scalar block.
+enum Scalar : int { kRR = 0, kPAP = 1 };
+
+// Stamp slots (SURVEY 8(a) TICK/TOCK classes, HPCCG.cpp:71-72).
+enum StampSlot : int {
+    kStampPUpdate = 0,  // waxpby p = r + beta p       -> WAXPBY
+    kStampHalo = 1,     // halo exchange starts         -> exchange (t5)
+    kStampSpmv = 2,     // SpMV (+ fused p.Ap partials) -> SPARSEMV
+    kStampFinPAP = 3,   // final p.Ap reduction         -> DDOT
+    kStampArPAP = 4,    // all-reduce of p.Ap           -> DDOT + all-reduce (t4)
+    kStampUpdate = 5,   // x += a p, r -= a Ap (+ r.r)  -> WAXPBY
+    kStampFinRR = 6,    // final r.r reduction          -> DDOT
+    kStampArRR = 7,     // all-reduce of r.r            -> DDOT + all-reduce (t4)
+    kStampPrologue = 8, // p = x, r = b - Ap            -> WAXPBY
+    kStampEnd = 9,
+    kNumStampSlots = 10
+};
+
+// Everything a CG kernel needs, passed by value (graph-capture friendly: all
+// per-iteration state lives in device memory, never in kernel arguments).
+struct CgArgs {
+    int n;                 // local rows
+    int nslices;           // ceil(n / kSliceRows)
+    int grid;              // nslices rounded up to a multiple of kNumXcd
+    int max_iter;
+    double tol;
+    int nranks;
+    int ghost_lo;          // halo rows below (in p only)
+    const double* b;
+    double* x;
+    double* r;
+    double* p;             // local rows of p; p - ghost_lo .. p + n + ghost_hi valid
+    double* Ap;
+    double* partial;       // [nslices] per-slice partial dot products
+    double* g;             // [2] dot results after the all-reduce
+    double* loc;           // [2] local dot results
+    double* hist;          // [max_iter + 1]: hist[j] = r_j . r_j (global)
+    int* kst;              // [0] next iteration k, [1] end stamped, [2] stamp count
+    unsigned long long* stamps;  // pairs (s_memrealtime, slot)
+    int stamp_cap;         // capacity in pairs
+    // SELL-512 matrix
+    const unsigned int* slice_base;  // [nslices + 1], units of kSliceRows slots
+    const int* cols;       // local column (ghost-inclusive base), -1 = padding
+    const double* vals;
+};
+
+// ---- launches (hpccg_kernels.hip) -----------------------------------------
+// CG iteration pieces; all take the same CgArgs.
+void launch_cg_prologue_copy(const CgArgs& a, hipStream_t s);   // p = x + 0*x
+void launch_cg_p_update(const CgArgs& a, hipStream_t s);        // p = r + beta p
+void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s);
+void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s);
+void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
+void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);
+void launch_cg_end(const CgArgs& a, hipStream_t s);
+
+// Kernel-level ops on arbitrary device pointers.
+void launch_waxpby(int n, double alpha, const double* x, double beta, const double* y, double* w,
+                   hipStream_t s);
+void launch_ddot(int n, const double* x, const double* y, double* partial, int nparts,
+                 double* out, hipStream_t s);
+int ddot_nparts(int n);
+void launch_sparsemv(const CgArgs& a, const double* xext, double* y, int variant, hipStream_t s);
+
+// Device generator: writes the SELL-512 image, b, xexact.
+void launch_generate(int nx, int ny, int nz, int rank, int size, int use_7pt, long long col_base,
+                     const unsigned int* slice_base, int* cols, double* vals, double* b,
+                     double* xexact, int nrow, hipStream_t s);
+
+}  // namespace hpccg

@@ -1,0 +1,622 @@
+// hpccg_kernels.hip -- hand-written CDNA4 (gfx950) kernels for the HPCCG hot
+// path. Memory-bound throughout (fp64, ~0.16 flop/byte): no MFMA; the design
+// goals are coalesced 16 B/lane streams, one pass per fused step, XCD-local
+// slice ownership, and bitwise-reproducible reductions.
+//
+// Numerics contract (tests/test_gpu_parity.py): compiled with
+// -ffp-contract=off, SpMV and waxpby are BITWISE equal to the reference
+// (HPC_sparsemv.cpp:76-87, waxpby.cpp:73-90: same per-row entry order, no
+// FMA); dot products use a fixed-shape two-stage tree (per-slice partials,
+// then one 1024-thread block in fixed order), so they are reproducible run to
+// run and differ from the reference's sequential sum only by rounding.
+#include "hpccg_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace hpccg {
+
+namespace {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ unsigned long long now_ticks()
+{
+    return __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
+}
+
+// Block b of a grid dealt round-robin over the 8 XCDs -> logical slice, so
+// that every XCD walks one contiguous 1/8 of the rows (x re-reads of the
+// stencil's neighbouring planes then hit that XCD's L2).
+__device__ __forceinline__ int xcd_slice(int grid)
+{
+    const int b = blockIdx.x;
+    const int per = grid / kNumXcd;
+    return (b % kNumXcd) * per + (b / kNumXcd);
+}
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+// Deterministic block reduction (fixed shape): waves by shfl_xor, then the
+// wave sums in wave order by thread 0. Result valid in thread 0.
+template <int kThreads>
+__device__ __forceinline__ double block_sum(double v)
+{
+    constexpr int kWaves = kThreads / kWave;
+    __shared__ double wsum[kWaves];
+    v = wave_sum(v);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+    if (lane == 0) wsum[w] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < kWaves; i++) s += wsum[i];
+    }
+    return s;
+}
+
+__device__ __forceinline__ void stamp(const CgArgs& a, int slot)
+{
+    const int idx = atomicAdd(&a.kst[2], 1);
+    if (idx < a.stamp_cap) {
+        a.stamps[2 * idx] = now_ticks();
+        a.stamps[2 * idx + 1] = (unsigned long long)slot;
+    }
+}
+
+// First kernel that finds the solve finished records the end time once.
+__device__ __forceinline__ void mark_end(const CgArgs& a)
+{
+    if (atomicCAS(&a.kst[1], 0, 1) == 0) stamp(a, kStampEnd);
+}
+
+// HPCCG.cpp:358 loop condition for iteration k: k < max_iter && normr > tol,
+// where normr is the value computed in iteration k-1, i.e. sqrt(r_{k-2}.r_{k-2})
+// (sqrt(r_0.r_0) for k = 1). hist[j] = r_j.r_j is filled by the p-update
+// kernel of iteration j+1; that kernel itself reads r_{k-1}.r_{k-1} from g.
+__device__ __forceinline__ bool cg_run(const CgArgs& a, int k, bool in_p_update)
+{
+    if (k >= a.max_iter) return false;
+    double chk;
+    if (k == 1)
+        chk = in_p_update ? a.g[kRR] : a.hist[0];
+    else
+        chk = a.hist[k - 2];
+    return sqrt(chk) > a.tol;
+}
+
+// ---------------------------------------------------------------------------
+// Row-blocked vector access: each thread owns kRpt consecutive rows of the
+// block's 512-row slice; kRpt = 2 gives 16 B per lane per stream.
+// ---------------------------------------------------------------------------
+template <int kRpt>
+struct Rows {
+    double v[kRpt];
+};
+
+template <int kRpt>
+__device__ __forceinline__ Rows<kRpt> ld(const double* __restrict__ p)
+{
+    Rows<kRpt> r;
+    if constexpr (kRpt == 1) {
+        r.v[0] = p[0];
+    } else {
+#pragma unroll
+        for (int i = 0; i < kRpt; i += 2) {
+            const double2 t = *reinterpret_cast<const double2*>(p + i);
+            r.v[i] = t.x;
+            r.v[i + 1] = t.y;
+        }
+    }
+    return r;
+}
+
+template <int kRpt>
+__device__ __forceinline__ void st(double* __restrict__ p, const Rows<kRpt>& r)
+{
+    if constexpr (kRpt == 1) {
+        p[0] = r.v[0];
+    } else {
+#pragma unroll
+        for (int i = 0; i < kRpt; i += 2) *reinterpret_cast<double2*>(p + i) = make_double2(r.v[i], r.v[i + 1]);
+    }
+}
+
+template <int kRpt>
+__device__ __forceinline__ void ld_cols(const int* __restrict__ p, int (&c)[kRpt])
+{
+    if constexpr (kRpt == 1) {
+        c[0] = p[0];
+    } else if constexpr (kRpt == 2) {
+        const int2 t = *reinterpret_cast<const int2*>(p);
+        c[0] = t.x;
+        c[1] = t.y;
+    } else {
+#pragma unroll
+        for (int i = 0; i < kRpt; i += 4) {
+            const int4 t = *reinterpret_cast<const int4*>(p + i);
+            c[i] = t.x;
+            c[i + 1] = t.y;
+            c[i + 2] = t.z;
+            c[i + 3] = t.w;
+        }
+    }
+}
+
+// Vectors are allocated padded to a multiple of 512 rows, so full-width loads
+// are always in bounds; rows >= n are masked on store and in the dots.
+
+// ---------------------------------------------------------------------------
+// Prologue: p = x + 0.0*x   (HPCCG.cpp:347, waxpby(nrow, 1.0, x, 0.0, x, p))
+// ---------------------------------------------------------------------------
+template <int kRpt>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_prologue_copy(CgArgs a)
+{
+    const int s = xcd_slice(a.grid);
+    if (blockIdx.x == 0 && threadIdx.x == 0) stamp(a, kStampPrologue);
+    if (s >= a.nslices) return;
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    Rows<kRpt> xv = ld<kRpt>(a.x + row), o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = xv.v[i] + 0.0 * xv.v[i];
+    if (row + kRpt <= a.n) {
+        st<kRpt>(a.p + row, o);
+    } else {
+        for (int i = 0; i < kRpt; i++)
+            if (row + i < a.n) a.p[row + i] = o.v[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// p = r + beta*p  (HPCCG.cpp:362 for k == 1: p = r + 0*r; :366-369 otherwise)
+// ---------------------------------------------------------------------------
+template <int kRpt>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_p_update(CgArgs a)
+{
+    const int k = a.kst[0];
+    const bool run = cg_run(a, k, true);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (k == 1 || run) a.hist[k - 1] = a.g[kRR];
+        if (run)
+            stamp(a, kStampPUpdate);
+        else
+            mark_end(a);
+    }
+    if (!run) return;
+    const int s = xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    const double beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+    const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+    const Rows<kRpt> yv = (k == 1) ? rv : ld<kRpt>(a.p + row);
+    Rows<kRpt> o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = rv.v[i] + beta * yv.v[i];
+    if (row + kRpt <= a.n) {
+        st<kRpt>(a.p + row, o);
+    } else {
+        for (int i = 0; i < kRpt; i++)
+            if (row + i < a.n) a.p[row + i] = o.v[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// SpMV over SELL-512 + fused per-slice partial of p.Ap
+// (HPC_sparsemv.cpp:68-89 then ddot.cpp:60-73 on (p, Ap)).
+//
+// Thread t of slice s owns rows s*512 + t*kRpt + [0, kRpt). Slot j of the
+// slice is a contiguous 512-entry run: lane loads are 16 B (vals) / 8 B (cols)
+// and a wave reads 1 KiB + 512 B per slot. x is gathered through L1/L2/MALL;
+// for the stencil the 64 lanes of a wave hit consecutive x.
+// kW > 0: slice width known at compile time (27 / 7), fully unrolled.
+// ---------------------------------------------------------------------------
+template <int kRpt, int kW>
+__device__ __forceinline__ void spmv_rows(const CgArgs& a, const double* __restrict__ xext, int s,
+                                          double (&sum)[kRpt])
+{
+    // kW > 0: every slice has exactly kW slots (host padded the image to a
+    // uniform width), so slice s starts at s*kW and the loop fully unrolls.
+    const size_t b0 = (kW > 0) ? (size_t)s * kW : (size_t)a.slice_base[s];
+    const int w = (kW > 0) ? kW : (int)(a.slice_base[s + 1] - a.slice_base[s]);
+    const size_t base = b0 * kSliceRows + (size_t)threadIdx.x * kRpt;
+    const double* __restrict__ vp = a.vals + base;
+    const int* __restrict__ cp = a.cols + base;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+    if constexpr (kW > 0) {
+#pragma unroll
+        for (int j = 0; j < kW; j++) {
+            int c[kRpt];
+            ld_cols<kRpt>(cp + (size_t)j * kSliceRows, c);
+            const Rows<kRpt> v = ld<kRpt>(vp + (size_t)j * kSliceRows);
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) {
+                const double xv = (c[i] >= 0) ? xext[c[i]] : 0.0;
+                sum[i] = sum[i] + v.v[i] * xv;
+            }
+        }
+    } else {
+#pragma unroll 3
+        for (int j = 0; j < w; j++) {
+            int c[kRpt];
+            ld_cols<kRpt>(cp + (size_t)j * kSliceRows, c);
+            const Rows<kRpt> v = ld<kRpt>(vp + (size_t)j * kSliceRows);
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) {
+                const double xv = (c[i] >= 0) ? xext[c[i]] : 0.0;
+                sum[i] = sum[i] + v.v[i] * xv;
+            }
+        }
+    }
+}
+
+// Padding slots add v*x = 0*0 = +0: a sum that starts at +0.0 is never -0 under
+// round-to-nearest, so +0 leaves every row sum bit-identical to skipping it.
+
+template <int kRpt, int kW, bool kDot>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv(CgArgs a, bool prologue)
+{
+    if (!prologue) {
+        const int k = a.kst[0];
+        const bool run = cg_run(a, k, false);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (run)
+                stamp(a, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    const double* __restrict__ xext = a.p - a.ghost_lo;
+    double sum[kRpt];
+    spmv_rows<kRpt, kW>(a, xext, s, sum);
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    Rows<kRpt> o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+    double d = 0.0;
+    if (row + kRpt <= a.n) {
+        st<kRpt>(a.Ap + row, o);
+        if constexpr (kDot) {
+            const Rows<kRpt> pv = ld<kRpt>(a.p + row);
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) d += pv.v[i] * o.v[i];
+        }
+    } else {
+        for (int i = 0; i < kRpt; i++)
+            if (row + i < a.n) {
+                a.Ap[row + i] = o.v[i];
+                if constexpr (kDot) d += a.p[row + i] * o.v[i];
+            }
+    }
+    if constexpr (kDot) {
+        const double bs = block_sum<kSliceRows / kRpt>(d);
+        if (threadIdx.x == 0) a.partial[s] = bs;
+    }
+}
+
+// Plain SpMV on arbitrary x (kernel-level C ABI): same body, no dot.
+template <int kRpt>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_plain(CgArgs a, const double* xext,
+                                                                  double* y)
+{
+    const int s = xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    double sum[kRpt];
+    spmv_rows<kRpt, 0>(a, xext, s, sum);
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) y[row + i] = sum[i];
+}
+
+// ---------------------------------------------------------------------------
+// Final reduction of the per-slice partials, one block, fixed order.
+// which = kPAP: p.Ap (HPCCG.cpp:381); which = kRR: r.r (HPCCG.cpp:353, 367).
+// The r.r finalize closes iteration k: it advances kst[0] to k+1.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int which, bool prologue)
+{
+    const int k = a.kst[0];
+    const bool run = prologue || cg_run(a, k, false);
+    if (threadIdx.x == 0) {
+        if (run)
+            stamp(a, which == kRR ? kStampFinRR : kStampFinPAP);
+        else
+            mark_end(a);
+    }
+    if (!run) return;
+    double v = 0.0;
+    for (int i = threadIdx.x; i < a.nslices; i += kFinalizeThreads) v += a.partial[i];
+    const double s = block_sum<kFinalizeThreads>(v);
+    if (threadIdx.x == 0) {
+        a.loc[which] = s;
+        if (a.nranks == 1) a.g[which] = s;
+        if (which == kRR) a.kst[0] = prologue ? 1 : k + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused update + r.r partial.
+// prologue: r = b + (-1)*Ap                (HPCCG.cpp:352)
+// loop:     x = x + alpha*p; r = r + (-alpha)*Ap   (HPCCG.cpp:382-384),
+//           alpha = rtrans / (p.Ap); then the r.r partial that the next
+//           iteration's ddot(r, r) (HPCCG.cpp:367) would compute.
+// ---------------------------------------------------------------------------
+template <int kRpt, bool kPrologue>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
+{
+    if constexpr (!kPrologue) {
+        const int k = a.kst[0];
+        const bool run = cg_run(a, k, false);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (run)
+                stamp(a, kStampUpdate);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    const Rows<kRpt> apv = ld<kRpt>(a.Ap + row);
+    Rows<kRpt> rn;
+    if constexpr (kPrologue) {
+        const Rows<kRpt> bv = ld<kRpt>(a.b + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) rn.v[i] = bv.v[i] + (-1.0) * apv.v[i];
+    } else {
+        const double alpha = a.g[kRR] / a.g[kPAP];
+        const Rows<kRpt> xv = ld<kRpt>(a.x + row);
+        const Rows<kRpt> pv = ld<kRpt>(a.p + row);
+        const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+        Rows<kRpt> xn;
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            xn.v[i] = xv.v[i] + alpha * pv.v[i];
+            rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
+        }
+        if (row + kRpt <= a.n) {
+            st<kRpt>(a.x + row, xn);
+        } else {
+            for (int i = 0; i < kRpt; i++)
+                if (row + i < a.n) a.x[row + i] = xn.v[i];
+        }
+    }
+    double d = 0.0;
+    if (row + kRpt <= a.n) {
+        st<kRpt>(a.r + row, rn);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) d += rn.v[i] * rn.v[i];
+    } else {
+        for (int i = 0; i < kRpt; i++)
+            if (row + i < a.n) {
+                a.r[row + i] = rn.v[i];
+                d += rn.v[i] * rn.v[i];
+            }
+    }
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    if (threadIdx.x == 0) a.partial[s] = bs;
+}
+
+// Timestamp-only kernel around RCCL calls (multi-rank): one lane, one store.
+__global__ void k_stamp(CgArgs a, int slot, bool prologue)
+{
+    if (!prologue) {
+        // The r.r all-reduce follows the finalize that already advanced k.
+        const int k = a.kst[0] - (slot == kStampArRR ? 1 : 0);
+        if (!cg_run(a, k, false)) {
+            mark_end(a);
+            return;
+        }
+    }
+    stamp(a, slot);
+}
+
+__global__ void k_end(CgArgs a) { mark_end(a); }
+
+// ---------------------------------------------------------------------------
+// Kernel-level ops on arbitrary device pointers.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_waxpby(int n, double alpha, const double* x, double beta,
+                                                const double* y, double* w)
+{
+    // waxpby.cpp:73-90 branches (alpha == 1 / beta == 1 only drop an exact
+    // multiply by one, so every branch rounds like the general expression).
+    const int stride = gridDim.x * blockDim.x;
+    if (alpha == 1.0) {
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) w[i] = x[i] + beta * y[i];
+    } else if (beta == 1.0) {
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) w[i] = alpha * x[i] + y[i];
+    } else {
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+            w[i] = alpha * x[i] + beta * y[i];
+    }
+}
+
+constexpr int kDotChunk = 4096;  // rows per partial: fixed shape, deterministic
+
+__global__ __launch_bounds__(256) void k_dot_partial(int n, const double* x, const double* y,
+                                                     double* partial)
+{
+    const int base = blockIdx.x * kDotChunk;
+    const int end = min(n, base + kDotChunk);
+    double d = 0.0;
+    for (int i = base + threadIdx.x; i < end; i += 256) d += x[i] * y[i];
+    const double s = block_sum<256>(d);
+    if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kFinalizeThreads) void k_dot_final(const double* partial, int nparts,
+                                                                double* out)
+{
+    double v = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += kFinalizeThreads) v += partial[i];
+    const double s = block_sum<kFinalizeThreads>(v);
+    if (threadIdx.x == 0) *out = s;
+}
+
+// ---------------------------------------------------------------------------
+// Device generator: generate_matrix.cpp:251-289 written straight into the
+// SELL-512 image. One thread per row; entries in (sz, sy, sx) order; slots
+// past the row length padded with col = -1, val = 0. Local columns are
+// global - col_base (col_base = start_row - ghost_lo).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_generate(int nx, int ny, int nz, int rank, int size,
+                                                  int use_7pt, long long col_base,
+                                                  const unsigned int* slice_base, int* cols,
+                                                  double* vals, double* b, double* xexact, int nrow)
+{
+    const int lrow = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lrow >= nrow) return;
+    const long long nxy = (long long)nx * ny;
+    const long long total_nrow = (long long)nrow * size;
+    const long long start_row = (long long)nrow * rank;
+    const int iz = (int)(lrow / nxy);
+    const int iy = (int)((lrow - (long long)iz * nxy) / nx);
+    const int ix = (int)(lrow - (long long)iz * nxy - (long long)iy * nx);
+    const long long currow = start_row + lrow;
+    const int s = lrow / kSliceRows;
+    const int lane = lrow - s * kSliceRows;
+    const unsigned int b0 = slice_base[s];
+    const int w = (int)(slice_base[s + 1] - b0);
+    const size_t base = (size_t)b0 * kSliceRows + lane;
+    int j = 0;
+    for (int sz = -1; sz <= 1; sz++)
+        for (int sy = -1; sy <= 1; sy++)
+            for (int sx = -1; sx <= 1; sx++) {
+                const long long curcol = currow + sz * nxy + (long long)sy * nx + sx;
+                if (ix + sx >= 0 && ix + sx < nx && iy + sy >= 0 && iy + sy < ny && curcol >= 0 &&
+                    curcol < total_nrow && (!use_7pt || sz * sz + sy * sy + sx * sx <= 1)) {
+                    vals[base + (size_t)j * kSliceRows] = (curcol == currow) ? 27.0 : -1.0;
+                    cols[base + (size_t)j * kSliceRows] = (int)(curcol - col_base);
+                    j++;
+                }
+            }
+    b[lrow] = 27.0 - ((double)(j - 1));
+    xexact[lrow] = 1.0;
+    for (; j < w; j++) {
+        vals[base + (size_t)j * kSliceRows] = 0.0;
+        cols[base + (size_t)j * kSliceRows] = -1;
+    }
+}
+
+// Rows of the last slice past nrow: all slots padding.
+__global__ void k_generate_tail(int nrow, int nslices, const unsigned int* slice_base, int* cols,
+                                double* vals)
+{
+    const int s = nslices - 1;
+    const int lane = threadIdx.x;
+    if (s * kSliceRows + lane < nrow) return;
+    const unsigned int b0 = slice_base[s];
+    const int w = (int)(slice_base[s + 1] - b0);
+    for (int j = 0; j < w; j++) {
+        vals[(size_t)b0 * kSliceRows + (size_t)j * kSliceRows + lane] = 0.0;
+        cols[(size_t)b0 * kSliceRows + (size_t)j * kSliceRows + lane] = -1;
+    }
+}
+
+constexpr int kRpt = 2;
+constexpr int kBlock = kSliceRows / kRpt;
+
+}  // namespace
+
+// ---- launch wrappers ------------------------------------------------------
+void launch_cg_prologue_copy(const CgArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_prologue_copy<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
+}
+
+void launch_cg_p_update(const CgArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_p_update<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
+}
+
+// variant: 0 = runtime slice width (any matrix), 27 / 7 = uniform-width fast
+// path chosen by the host when every slice has that width.
+void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
+{
+    switch (variant) {
+    case 27:
+        hipLaunchKernelGGL((k_spmv<kRpt, 27, true>), dim3(a.grid), dim3(kBlock), 0, s, a, prologue);
+        break;
+    case 7:
+        hipLaunchKernelGGL((k_spmv<kRpt, 7, true>), dim3(a.grid), dim3(kBlock), 0, s, a, prologue);
+        break;
+    case 1:  // one row per thread, runtime width
+        hipLaunchKernelGGL((k_spmv<1, 0, true>), dim3(a.grid), dim3(kSliceRows), 0, s, a, prologue);
+        break;
+    default:
+        hipLaunchKernelGGL((k_spmv<kRpt, 0, true>), dim3(a.grid), dim3(kBlock), 0, s, a, prologue);
+        break;
+    }
+}
+
+void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kFinalizeThreads), 0, s, a, which, prologue);
+}
+
+void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)
+{
+    if (prologue)
+        hipLaunchKernelGGL((k_update<kRpt, true>), dim3(a.grid), dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_update<kRpt, false>), dim3(a.grid), dim3(kBlock), 0, s, a);
+}
+
+void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, s, a, slot, prologue);
+}
+
+void launch_cg_end(const CgArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_end, dim3(1), dim3(64), 0, s, a);
+}
+
+void launch_waxpby(int n, double alpha, const double* x, double beta, const double* y, double* w,
+                   hipStream_t s)
+{
+    if (n <= 0) return;
+    int grid = (n + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(k_waxpby, dim3(grid), dim3(256), 0, s, n, alpha, x, beta, y, w);
+}
+
+int ddot_nparts(int n) { return n <= 0 ? 1 : (n + kDotChunk - 1) / kDotChunk; }
+
+void launch_ddot(int n, const double* x, const double* y, double* partial, int nparts, double* out,
+                 hipStream_t s)
+{
+    if (n > 0) hipLaunchKernelGGL(k_dot_partial, dim3(nparts), dim3(256), 0, s, n, x, y, partial);
+    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(kFinalizeThreads), 0, s, partial,
+                       n > 0 ? nparts : 0, out);
+}
+
+void launch_sparsemv(const CgArgs& a, const double* xext, double* y, int variant, hipStream_t s)
+{
+    (void)variant;
+    hipLaunchKernelGGL(k_spmv_plain<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a, xext, y);
+}
+
+void launch_generate(int nx, int ny, int nz, int rank, int size, int use_7pt, long long col_base,
+                     const unsigned int* slice_base, int* cols, double* vals, double* b,
+                     double* xexact, int nrow, hipStream_t s)
+{
+    const int nslices = (nrow + kSliceRows - 1) / kSliceRows;
+    hipLaunchKernelGGL(k_generate, dim3((nrow + 255) / 256), dim3(256), 0, s, nx, ny, nz, rank, size,
+                       use_7pt, col_base, slice_base, cols, vals, b, xexact, nrow);
+    hipLaunchKernelGGL(k_generate_tail, dim3(1), dim3(kSliceRows), 0, s, nrow, nslices, slice_base,
+                       cols, vals);
+}
+
+}  // namespace hpccg

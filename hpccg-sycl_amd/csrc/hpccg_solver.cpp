@@ -1,0 +1,1054 @@
+// hpccg_solver.cpp -- host side of the MI355X HPCCG path: HPC_Sparse_Matrix ->
+// SELL-512 conversion, device residency, the device-resident CG driver
+// (HPCCG.cpp:312-402), the z-slab halo exchange and scalar all-reduces over
+// RCCL (exchange_externals.cpp:51-131, ddot.cpp:75-85), and the C ABI.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/HPC_Sparse_Matrix.hpp"
+#include "../../include/hpccg_hip.h"
+#include "hpccg_internal.h"
+
+using namespace hpccg;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return set_err(e_ == hipErrorOutOfMemory ? HPCCG_HIP_ENOMEM : HPCCG_HIP_EHIP,          \
+                           "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__);   \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                             \
+    do {                                                                                           \
+        ncclResult_t r_ = (expr);                                                                  \
+        if (r_ != ncclSuccess)                                                                     \
+            return set_err(HPCCG_HIP_ERCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_),      \
+                           __FILE__, __LINE__);                                                    \
+    } while (0)
+
+#define TRY(expr)                                                                                  \
+    do {                                                                                           \
+        int rc_ = (expr);                                                                          \
+        if (rc_ != 0) return rc_;                                                                  \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// communicator (one rank per GPU per process)
+// ---------------------------------------------------------------------------
+struct Comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 1;
+    int rank = 0;
+};
+Comm g_comm;
+
+// ---------------------------------------------------------------------------
+// SELL-512 build from any row accessor. Entry order per row is preserved.
+// ---------------------------------------------------------------------------
+template <class RowLen, class RowAt>
+long long sell_build_impl(int nrow, long long col_base, long long ncol_ext, RowLen row_len,
+                          RowAt row_at, unsigned int* slice_base, int* sell_cols, double* sell_vals,
+                          int uniform_width, int* err)
+{
+    const int nslices = (nrow + kSliceRows - 1) / kSliceRows;
+    // widths
+    long long total = 0;
+    int wmax = 0;
+    std::vector<int> w(nslices, 0);
+    for (int s = 0; s < nslices; s++) {
+        int m = 0;
+        for (int i = s * kSliceRows; i < std::min(nrow, (s + 1) * kSliceRows); i++)
+            m = std::max(m, row_len(i));
+        w[s] = m;
+        wmax = std::max(wmax, m);
+    }
+    if (uniform_width) std::fill(w.begin(), w.end(), wmax);
+    for (int s = 0; s < nslices; s++) {
+        if (slice_base) slice_base[s] = (unsigned int)total;
+        total += w[s];
+    }
+    if (slice_base) slice_base[nslices] = (unsigned int)total;
+    if (!sell_cols || !sell_vals) return total * kSliceRows;
+    // fill, parallel over slices
+    std::atomic<int> bad{0};
+    const int nth = std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
+    auto work = [&](int t) {
+        for (int s = t; s < nslices; s += nth) {
+            const size_t b0 = (size_t)slice_base[s] * kSliceRows;
+            for (int lane = 0; lane < kSliceRows; lane++) {
+                const int i = s * kSliceRows + lane;
+                const int len = i < nrow ? row_len(i) : 0;
+                for (int j = 0; j < w[s]; j++) {
+                    const size_t e = b0 + (size_t)j * kSliceRows + lane;
+                    if (j < len) {
+                        double v;
+                        long long c;
+                        row_at(i, j, &c, &v);
+                        const long long lc = c - col_base;
+                        if (lc < 0 || lc >= ncol_ext) bad.store(1);
+                        sell_cols[e] = (int)lc;
+                        sell_vals[e] = v;
+                    } else {
+                        sell_cols[e] = -1;
+                        sell_vals[e] = 0.0;
+                    }
+                }
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    if (err) *err = bad.load();
+    return total * kSliceRows;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// device matrix + CG workspace
+// ---------------------------------------------------------------------------
+struct hpccg_hip_matrix {
+    int device = 0;
+    int nrow = 0, start_row = 0, total_nrow = 0;
+    int ghost_lo = 0, ghost_hi = 0;
+    // what neighbours need from us (filled by the collective plan exchange)
+    int send_lo = 0;  // rows to send to rank-1 (its ghost_hi)
+    int send_hi = 0;  // rows to send to rank+1 (its ghost_lo)
+    long long nnz = 0, nslots = 0;
+    int nslices = 0, grid = 0, width = 0, uniform = 0;
+    int spmv_variant = 0;
+    int use_graph = 1;
+    unsigned int* d_slice_base = nullptr;
+    int* d_cols = nullptr;
+    double* d_vals = nullptr;
+    // workspace (padded to a multiple of kSliceRows rows)
+    size_t npad = 0;
+    double* d_pbuf = nullptr;  // ghost_lo_pad + npad + ghost_hi
+    double* d_p = nullptr;
+    double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
+    double* d_partial = nullptr;
+    double* d_scal = nullptr;  // g[2], loc[2], scratch[4]
+    int* d_kst = nullptr;
+    double* d_hist = nullptr;
+    unsigned long long* d_stamps = nullptr;
+    int hist_cap = 0, stamp_cap = 0;
+    double* d_ddot_partial = nullptr;
+    int ddot_cap = 0;
+    // generated-problem vectors
+    double *d_gen_b = nullptr, *d_gen_x0 = nullptr, *d_gen_xexact = nullptr;
+    hipStream_t stream = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    int graph_chunk = 0;
+    CgArgs graph_args{};
+    int graph_variant = -1;
+    // hipEvent timing (event_timing option)
+    int event_timing = 0;
+    std::vector<hipEvent_t> ev;   // 4 per iteration slot: spmv start/end, update start/end
+    double ktimes[4] = {0, 0, 0, 0};
+    // last solve
+    std::vector<double> trace;
+    int last_niters = 0;
+};
+
+namespace {
+
+int free_matrix(hpccg_hip_matrix* M)
+{
+    if (!M) return 0;
+    (void)hipSetDevice(M->device);
+    if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
+    void* ptrs[] = {M->d_slice_base, M->d_cols,    M->d_vals,  M->d_pbuf,         M->d_r,
+                    M->d_Ap,         M->d_x,       M->d_b,     M->d_partial,      M->d_scal,
+                    M->d_kst,        M->d_hist,    M->d_stamps, M->d_ddot_partial, M->d_gen_b,
+                    M->d_gen_x0,     M->d_gen_xexact};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
+    if (M->stream) (void)hipStreamDestroy(M->stream);
+    delete M;
+    return 0;
+}
+
+// Plan exchange: every rank learns what its neighbours need (make_local_matrix
+// .cpp:286-587 does this with MPI handshakes; for z-slabs it is one
+// all-gather of {nrow, ghost_lo, ghost_hi}).
+int exchange_plan(hpccg_hip_matrix* M)
+{
+    M->send_lo = M->send_hi = 0;
+    if (g_comm.nranks == 1) {
+        if (M->ghost_lo || M->ghost_hi)
+            return set_err(HPCCG_HIP_EPLAN, "columns outside the local rows on a single rank");
+        return 0;
+    }
+    int* d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof(int) * 4 * (g_comm.nranks + 1)));
+    int mine[4] = {M->nrow, M->ghost_lo, M->ghost_hi, M->start_row};
+    HIP_TRY(hipMemcpy(d, mine, sizeof mine, hipMemcpyHostToDevice));
+    NCCL_TRY(ncclAllGather(d, d + 4, 4, ncclInt32, g_comm.comm, M->stream));
+    std::vector<int> all(4 * g_comm.nranks);
+    HIP_TRY(hipMemcpyAsync(all.data(), d + 4, sizeof(int) * 4 * g_comm.nranks, hipMemcpyDeviceToHost,
+                           M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    (void)hipFree(d);
+    const int r = g_comm.rank, P = g_comm.nranks;
+    // ghosts must come from the adjacent ranks only, contiguously
+    if (M->ghost_lo > 0 && (r == 0 || M->ghost_lo > all[4 * (r - 1)]))
+        return set_err(HPCCG_HIP_EPLAN, "rank %d: ghost_lo %d not owned by rank %d", r, M->ghost_lo, r - 1);
+    if (M->ghost_hi > 0 && (r == P - 1 || M->ghost_hi > all[4 * (r + 1)]))
+        return set_err(HPCCG_HIP_EPLAN, "rank %d: ghost_hi %d not owned by rank %d", r, M->ghost_hi, r + 1);
+    if (r > 0 && all[4 * (r - 1) + 3] + all[4 * (r - 1)] != M->start_row)
+        return set_err(HPCCG_HIP_EPLAN, "rank %d: row ranges are not contiguous", r);
+    M->send_lo = (r > 0) ? all[4 * (r - 1) + 2] : 0;      // rank-1's ghost_hi
+    M->send_hi = (r < P - 1) ? all[4 * (r + 1) + 1] : 0;  // rank+1's ghost_lo
+    if (M->send_lo > M->nrow || M->send_hi > M->nrow)
+        return set_err(HPCCG_HIP_EPLAN, "rank %d: neighbour needs more rows than owned", r);
+    return 0;
+}
+
+int alloc_workspace(hpccg_hip_matrix* M)
+{
+    M->npad = (size_t)M->nslices * kSliceRows;
+    if (M->npad == 0) M->npad = kSliceRows;
+    // p = [ghost_lo | n | ghost_hi]; local rows start 512-row aligned
+    const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
+    HIP_TRY(hipMalloc(&M->d_pbuf, sizeof(double) * (glo_pad + M->npad + M->ghost_hi + 2)));
+    HIP_TRY(hipMemset(M->d_pbuf, 0, sizeof(double) * (glo_pad + M->npad + M->ghost_hi + 2)));
+    M->d_p = M->d_pbuf + glo_pad;
+    double** vecs[] = {&M->d_r, &M->d_Ap, &M->d_x, &M->d_b};
+    for (double** v : vecs) {
+        HIP_TRY(hipMalloc(v, sizeof(double) * M->npad));
+        HIP_TRY(hipMemset(*v, 0, sizeof(double) * M->npad));
+    }
+    HIP_TRY(hipMalloc(&M->d_partial, sizeof(double) * std::max(1, M->nslices)));
+    HIP_TRY(hipMalloc(&M->d_scal, sizeof(double) * 8));
+    HIP_TRY(hipMemset(M->d_scal, 0, sizeof(double) * 8));
+    HIP_TRY(hipMalloc(&M->d_kst, sizeof(int) * 4));
+    return 0;
+}
+
+int ensure_hist(hpccg_hip_matrix* M, int max_iter)
+{
+    const int need = std::max(2, max_iter + 1);
+    if (need > M->hist_cap) {
+        if (M->d_hist) (void)hipFree(M->d_hist);
+        HIP_TRY(hipMalloc(&M->d_hist, sizeof(double) * need));
+        M->hist_cap = need;
+    }
+    const int scap = 16 + (max_iter + 2) * kNumStampSlots;
+    if (scap > M->stamp_cap) {
+        if (M->d_stamps) (void)hipFree(M->d_stamps);
+        HIP_TRY(hipMalloc(&M->d_stamps, sizeof(unsigned long long) * 2 * scap));
+        M->stamp_cap = scap;
+    }
+    return 0;
+}
+
+CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
+{
+    CgArgs a;
+    std::memset(&a, 0, sizeof a);  // graph cache compares bytes
+    a.n = M->nrow;
+    a.nslices = M->nslices;
+    a.grid = M->grid;
+    a.max_iter = max_iter;
+    a.tol = tol;
+    a.nranks = g_comm.nranks;
+    a.ghost_lo = M->ghost_lo;
+    a.b = b;
+    a.x = x;
+    a.r = M->d_r;
+    a.p = M->d_p;
+    a.Ap = M->d_Ap;
+    a.partial = M->d_partial;
+    a.g = M->d_scal;
+    a.loc = M->d_scal + 2;
+    a.hist = M->d_hist;
+    a.kst = M->d_kst;
+    a.stamps = M->d_stamps;
+    a.stamp_cap = M->stamp_cap;
+    a.slice_base = M->d_slice_base;
+    a.cols = M->d_cols;
+    a.vals = M->d_vals;
+    return a;
+}
+
+// Halo exchange of p (exchange_externals.cpp:51-131): the z-slab ghosts are
+// contiguous, so no pack: rank r sends its first send_lo rows down and its
+// last send_hi rows up, and receives straight into the ghost regions.
+int enqueue_halo(hpccg_hip_matrix* M, double* p)
+{
+    if (g_comm.nranks == 1) return 0;
+    const int r = g_comm.rank;
+    NCCL_TRY(ncclGroupStart());
+    if (r > 0) {
+        if (M->ghost_lo) NCCL_TRY(ncclRecv(p - M->ghost_lo, M->ghost_lo, ncclFloat64, r - 1, g_comm.comm, M->stream));
+        if (M->send_lo) NCCL_TRY(ncclSend(p, M->send_lo, ncclFloat64, r - 1, g_comm.comm, M->stream));
+    }
+    if (r < g_comm.nranks - 1) {
+        if (M->ghost_hi) NCCL_TRY(ncclRecv(p + M->nrow, M->ghost_hi, ncclFloat64, r + 1, g_comm.comm, M->stream));
+        if (M->send_hi)
+            NCCL_TRY(ncclSend(p + M->nrow - M->send_hi, M->send_hi, ncclFloat64, r + 1, g_comm.comm, M->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return 0;
+}
+
+int enqueue_allreduce(hpccg_hip_matrix* M, const CgArgs& a, int which)
+{
+    if (g_comm.nranks == 1) return 0;
+    NCCL_TRY(ncclAllReduce(a.loc + which, a.g + which, 1, ncclFloat64, ncclSum, g_comm.comm, M->stream));
+    return 0;
+}
+
+int ensure_events(hpccg_hip_matrix* M, int slots)
+{
+    while ((int)M->ev.size() < 4 * slots) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        M->ev.push_back(e);
+    }
+    return 0;
+}
+
+// One CG iteration k (HPCCG.cpp:358-386), fully device resident. slot >= 0:
+// bracket the SpMV and the fused update with that slot's hipEvents.
+int enqueue_iteration(hpccg_hip_matrix* M, const CgArgs& a, int slot = -1)
+{
+    hipStream_t s = M->stream;
+    launch_cg_p_update(a, s);
+    if (g_comm.nranks > 1) {
+        launch_cg_stamp(a, kStampHalo, false, s);
+        TRY(enqueue_halo(M, a.p));
+    }
+    if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], s));
+    launch_cg_spmv(a, M->spmv_variant, false, s);
+    if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], s));
+    launch_cg_finalize(a, kPAP, false, s);
+    if (g_comm.nranks > 1) {
+        launch_cg_stamp(a, kStampArPAP, false, s);
+        TRY(enqueue_allreduce(M, a, kPAP));
+    }
+    if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], s));
+    launch_cg_update(a, false, s);
+    if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 3], s));
+    launch_cg_finalize(a, kRR, false, s);
+    if (g_comm.nranks > 1) {
+        launch_cg_stamp(a, kStampArRR, false, s);
+        TRY(enqueue_allreduce(M, a, kRR));
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int enqueue_prologue(hpccg_hip_matrix* M, const CgArgs& a, bool events)
+{
+    hipStream_t s = M->stream;
+    launch_cg_prologue_copy(a, s);  // p = x
+    if (g_comm.nranks > 1) {
+        launch_cg_stamp(a, kStampHalo, true, s);
+        TRY(enqueue_halo(M, a.p));
+    }
+    if (events) HIP_TRY(hipEventRecord(M->ev[0], s));
+    launch_cg_spmv(a, M->spmv_variant, true, s);  // Ap = A p
+    if (events) HIP_TRY(hipEventRecord(M->ev[1], s));
+    if (events) HIP_TRY(hipEventRecord(M->ev[2], s));
+    launch_cg_update(a, true, s);                  // r = b - Ap (+ r.r partials)
+    if (events) HIP_TRY(hipEventRecord(M->ev[3], s));
+    launch_cg_finalize(a, kRR, true, s);           // rtrans, k = 1
+    if (g_comm.nranks > 1) {
+        launch_cg_stamp(a, kStampArRR, true, s);
+        TRY(enqueue_allreduce(M, a, kRR));
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+constexpr int kGraphChunk = 8;  // CG iterations per captured graph
+
+int build_graph(hpccg_hip_matrix* M, const CgArgs& a)
+{
+    if (M->graph_exec) {
+        (void)hipGraphExecDestroy(M->graph_exec);
+        M->graph_exec = nullptr;
+    }
+    hipGraph_t g = nullptr;
+    HIP_TRY(hipStreamBeginCapture(M->stream, hipStreamCaptureModeThreadLocal));
+    int rc = 0;
+    for (int i = 0; i < kGraphChunk && rc == 0; i++) rc = enqueue_iteration(M, a);
+    hipError_t e = hipStreamEndCapture(M->stream, &g);
+    if (rc) return rc;
+    if (e != hipSuccess) return set_err(HPCCG_HIP_EHIP, "graph capture failed: %s", hipGetErrorString(e));
+    e = hipGraphInstantiate(&M->graph_exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) return set_err(HPCCG_HIP_EHIP, "graph instantiate failed: %s", hipGetErrorString(e));
+    M->graph_chunk = kGraphChunk;
+    return 0;
+}
+
+// Turns the device stamp sequence into the reference's timer classes.
+void stamps_to_times(const std::vector<unsigned long long>& st, int count, double* times)
+{
+    double t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
+    for (int i = 0; i + 1 < count; i++) {
+        const int slot = (int)st[2 * i + 1];
+        if (slot == kStampEnd) break;
+        const double d = (double)(st[2 * (i + 1)] - st[2 * i]) * 1e-8;  // 100 MHz
+        switch (slot) {
+        case kStampPUpdate:
+        case kStampUpdate:
+        case kStampPrologue: t2 += d; break;
+        case kStampSpmv: t3 += d; break;
+        case kStampFinPAP:
+        case kStampFinRR: t1 += d; break;
+        case kStampArPAP:
+        case kStampArRR:
+            t1 += d;
+            t4 += d;
+            break;
+        case kStampHalo: t5 += d; break;
+        default: break;
+        }
+    }
+    times[1] = t1;
+    times[2] = t2;
+    times[3] = t3;
+    times[4] = t4;
+    times[5] = t5;
+}
+
+int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_iter, double tol,
+               int* niters_out, double* normr_out, double* times, int print)
+{
+    HIP_TRY(hipSetDevice(M->device));
+    TRY(ensure_hist(M, max_iter));
+    const auto t_begin = std::chrono::steady_clock::now();
+    CgArgs a = make_args(M, b_dev, x_dev, max_iter, tol);
+    const int iters = std::max(0, max_iter - 1);
+    const bool events = M->event_timing != 0;
+    if (events) TRY(ensure_events(M, iters + 1));
+    HIP_TRY(hipMemsetAsync(M->d_kst, 0, sizeof(int) * 4, M->stream));
+    TRY(enqueue_prologue(M, a, events));
+    const bool graph = !events && M->use_graph && g_comm.nranks == 1 && iters >= kGraphChunk;
+    int done = 0;
+    if (graph) {
+        // kernel arguments are baked into the graph: rebuild only when they change
+        if (!M->graph_exec || std::memcmp(&M->graph_args, &a, sizeof a) != 0 ||
+            M->graph_variant != M->spmv_variant) {
+            TRY(build_graph(M, a));
+            M->graph_args = a;
+            M->graph_variant = M->spmv_variant;
+        }
+        for (; done + kGraphChunk <= iters; done += kGraphChunk)
+            HIP_TRY(hipGraphLaunch(M->graph_exec, M->stream));
+    }
+    for (; done < iters; done++) TRY(enqueue_iteration(M, a, events ? done + 1 : -1));
+    launch_cg_end(a, M->stream);
+    HIP_TRY(hipGetLastError());
+    // results
+    int kst[4];
+    HIP_TRY(hipMemcpyAsync(kst, M->d_kst, sizeof kst, hipMemcpyDeviceToHost, M->stream));
+    double scal[8];
+    HIP_TRY(hipMemcpyAsync(scal, M->d_scal, sizeof scal, hipMemcpyDeviceToHost, M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    const auto t_end = std::chrono::steady_clock::now();
+    const int niters = std::max(0, kst[0] - 1);
+    std::vector<double> hist(std::max(1, niters));
+    if (niters > 0)
+        HIP_TRY(hipMemcpy(hist.data(), M->d_hist, sizeof(double) * niters, hipMemcpyDeviceToHost));
+    const int nst = std::min(kst[2], M->stamp_cap);
+    std::vector<unsigned long long> st(2 * std::max(1, nst));
+    if (nst > 0)
+        HIP_TRY(hipMemcpy(st.data(), M->d_stamps, sizeof(unsigned long long) * 2 * nst,
+                          hipMemcpyDeviceToHost));
+    // normr after iteration k is sqrt(r_{k-1}.r_{k-1}) (HPCCG.cpp:371)
+    M->trace.assign(niters + 1, 0.0);
+    M->trace[0] = std::sqrt(niters > 0 ? hist[0] : scal[kRR]);
+    for (int k = 1; k <= niters; k++) M->trace[k] = std::sqrt(hist[k - 1]);
+    M->last_niters = niters;
+    const double normr = M->trace[niters];
+    if (events) {
+        double sp = 0, up = 0;
+        for (int i = 0; i <= niters; i++) {
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, M->ev[4 * i], M->ev[4 * i + 1]));
+            sp += ms;
+            HIP_TRY(hipEventElapsedTime(&ms, M->ev[4 * i + 2], M->ev[4 * i + 3]));
+            up += ms;
+        }
+        M->ktimes[0] = sp;
+        M->ktimes[1] = niters + 1;
+        M->ktimes[2] = up;
+        M->ktimes[3] = niters + 1;
+    }
+    if (print && g_comm.rank == 0) {
+        int pf = max_iter / 10;
+        if (pf > 50) pf = 50;
+        if (pf < 1) pf = 1;
+        std::cout << "Initial Residual = " << M->trace[0] << std::endl;
+        for (int k = 1; k <= niters; k++)
+            if (k % pf == 0 || k + 1 == max_iter)
+                std::cout << "Iteration = " << k << "   Residual = " << M->trace[k] << std::endl;
+    }
+    if (times) {
+        stamps_to_times(st, nst, times);
+        times[0] = std::chrono::duration<double>(t_end - t_begin).count();
+    }
+    *niters_out = niters;
+    *normr_out = normr;
+    return 0;
+}
+
+template <class RowLen, class RowAt>
+int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_nrow, RowLen row_len,
+                     RowAt row_at)
+{
+    if (!out) return set_err(HPCCG_HIP_EINVAL, "out is NULL");
+    if (nrow < 0) return set_err(HPCCG_HIP_EINVAL, "nrow < 0");
+    auto* M = new hpccg_hip_matrix();
+    HIP_TRY(hipGetDevice(&M->device));
+    M->nrow = nrow;
+    M->start_row = start_row;
+    M->total_nrow = total_nrow;
+    // halo plan from the column range
+    long long mn = start_row, mx = (long long)start_row + nrow - 1, nnz = 0;
+    for (int i = 0; i < nrow; i++) {
+        const int len = row_len(i);
+        nnz += len;
+        for (int j = 0; j < len; j++) {
+            long long c;
+            double v;
+            row_at(i, j, &c, &v);
+            mn = std::min(mn, c);
+            mx = std::max(mx, c);
+        }
+    }
+    M->nnz = nnz;
+    M->ghost_lo = (int)std::max(0LL, (long long)start_row - mn);
+    M->ghost_hi = (int)std::max(0LL, mx - ((long long)start_row + nrow - 1));
+    HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamNonBlocking));
+    int rc = exchange_plan(M);
+    if (rc) {
+        free_matrix(M);
+        return rc;
+    }
+    M->nslices = (nrow + kSliceRows - 1) / kSliceRows;
+    M->grid = std::max(kNumXcd, (M->nslices + kNumXcd - 1) / kNumXcd * kNumXcd);
+    const long long col_base = (long long)start_row - M->ghost_lo;
+    const long long ncol_ext = (long long)M->ghost_lo + nrow + M->ghost_hi;
+    // uniform width when padding to the max costs < 4 % (stencils)
+    std::vector<unsigned int> sb(M->nslices + 1);
+    const long long slots_var =
+        sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, sb.data(), nullptr, nullptr, 0, nullptr);
+    const long long slots_uni =
+        sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, sb.data(), nullptr, nullptr, 1, nullptr);
+    M->uniform = (slots_uni <= slots_var + slots_var / 25) ? 1 : 0;
+    M->nslots = sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, sb.data(), nullptr, nullptr,
+                                M->uniform, nullptr);
+    M->width = M->nslices ? (int)(M->nslots / kSliceRows / M->nslices) : 0;
+    std::vector<int> hc((size_t)std::max(1LL, M->nslots));
+    std::vector<double> hv((size_t)std::max(1LL, M->nslots));
+    int bad = 0;
+    sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, sb.data(), hc.data(), hv.data(), M->uniform,
+                    &bad);
+    if (bad) {
+        free_matrix(M);
+        return set_err(HPCCG_HIP_EPLAN, "column index outside the halo plan");
+    }
+    M->spmv_variant = (M->uniform && (M->width == 27 || M->width == 7)) ? M->width : 0;
+    rc = [&]() -> int {
+        HIP_TRY(hipMalloc(&M->d_slice_base, sizeof(unsigned int) * sb.size()));
+        HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&M->d_cols, sizeof(int) * hc.size()));
+        HIP_TRY(hipMemcpy(M->d_cols, hc.data(), sizeof(int) * hc.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&M->d_vals, sizeof(double) * hv.size()));
+        HIP_TRY(hipMemcpy(M->d_vals, hv.data(), sizeof(double) * hv.size(), hipMemcpyHostToDevice));
+        return alloc_workspace(M);
+    }();
+    if (rc) {
+        free_matrix(M);
+        return rc;
+    }
+    *out = M;
+    return 0;
+}
+
+// scratch for kernel-level ddot without a matrix
+struct Scratch {
+    double* partial = nullptr;
+    int cap = 0;
+    double* out = nullptr;
+    hipStream_t s = nullptr;
+    int device = -1;
+};
+thread_local Scratch g_scratch;
+
+int scratch_for(int nparts)
+{
+    int dev;
+    HIP_TRY(hipGetDevice(&dev));
+    if (g_scratch.device != dev) {
+        g_scratch = Scratch();
+        g_scratch.device = dev;
+        HIP_TRY(hipStreamCreateWithFlags(&g_scratch.s, hipStreamNonBlocking));
+        HIP_TRY(hipMalloc(&g_scratch.out, sizeof(double) * 2));
+    }
+    if (nparts > g_scratch.cap) {
+        if (g_scratch.partial) (void)hipFree(g_scratch.partial);
+        HIP_TRY(hipMalloc(&g_scratch.partial, sizeof(double) * (nparts + 8)));
+        g_scratch.cap = nparts;
+    }
+    return 0;
+}
+
+std::mutex g_dropin_mu;
+std::map<const void*, hpccg_hip_matrix*> g_dropin_cache;
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int hpccg_hip_abi_version(void) { return 1; }
+
+const char* hpccg_hip_last_error(void) { return g_err.c_str(); }
+
+int hpccg_hip_device_count(int* count)
+{
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    *count = c;
+    return c > 0 ? 0 : set_err(HPCCG_HIP_ENODEV, "no HIP device");
+}
+
+int hpccg_hip_set_device(int device)
+{
+    HIP_TRY(hipSetDevice(device));
+    return 0;
+}
+
+int hpccg_hip_comm_unique_id(unsigned char id_out[128])
+{
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    std::memcpy(id_out, &id, 128);
+    return 0;
+}
+
+int hpccg_hip_comm_init(const unsigned char id[128], int nranks, int rank)
+{
+    if (nranks < 1 || rank < 0 || rank >= nranks) return set_err(HPCCG_HIP_EINVAL, "bad nranks/rank");
+    if (g_comm.comm) {
+        ncclCommDestroy(g_comm.comm);
+        g_comm = Comm();
+    }
+    if (nranks == 1) return 0;
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    NCCL_TRY(ncclCommInitRank(&g_comm.comm, nranks, uid, rank));
+    g_comm.nranks = nranks;
+    g_comm.rank = rank;
+    return 0;
+}
+
+int hpccg_hip_comm_destroy(void)
+{
+    if (g_comm.comm) ncclCommDestroy(g_comm.comm);
+    g_comm = Comm();
+    return 0;
+}
+
+int hpccg_hip_comm_size(int* nranks, int* rank)
+{
+    if (nranks) *nranks = g_comm.nranks;
+    if (rank) *rank = g_comm.rank;
+    return 0;
+}
+
+int hpccg_hip_comm_allreduce_host(double* vals, int n, int op)
+{
+    if (!vals || n < 0 || op < 0 || op > 2) return set_err(HPCCG_HIP_EINVAL, "bad argument");
+    if (g_comm.nranks == 1 || n == 0) return 0;
+    double* d = nullptr;
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_TRY(hipMalloc(&d, sizeof(double) * n));
+    HIP_TRY(hipMemcpy(d, vals, sizeof(double) * n, hipMemcpyHostToDevice));
+    const ncclRedOp_t ops[3] = {ncclSum, ncclMin, ncclMax};
+    NCCL_TRY(ncclAllReduce(d, d, n, ncclFloat64, ops[op], g_comm.comm, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemcpy(vals, d, sizeof(double) * n, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    (void)hipStreamDestroy(s);
+    return 0;
+}
+
+int hpccg_hip_device_name(char* buf, int cap, int* cus)
+{
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, dev));
+    if (buf && cap > 0) {
+        std::snprintf(buf, cap, "%s (%s)", prop.name, prop.gcnArchName);
+    }
+    if (cus) *cus = prop.multiProcessorCount;
+    return 0;
+}
+
+int hpccg_hip_matrix_create(const HPC_Sparse_Matrix* A, hpccg_hip_matrix** out)
+{
+    if (!A) return set_err(HPCCG_HIP_EINVAL, "A is NULL");
+    const int n = A->local_nrow;
+    return create_from_rows(
+        out, n, A->start_row, A->total_nrow, [A](int i) { return A->nnz_in_row[i]; },
+        [A](int i, int j, long long* c, double* v) {
+            *c = A->ptr_to_inds_in_row[i][j];
+            *v = A->ptr_to_vals_in_row[i][j];
+        });
+}
+
+int hpccg_hip_matrix_create_csr(int nrow, int start_row, int total_nrow, const long long* row_ptr,
+                                const int* cols, const double* vals, hpccg_hip_matrix** out)
+{
+    if (nrow > 0 && (!row_ptr || !cols || !vals)) return set_err(HPCCG_HIP_EINVAL, "NULL CSR array");
+    return create_from_rows(
+        out, nrow, start_row, total_nrow, [row_ptr](int i) { return (int)(row_ptr[i + 1] - row_ptr[i]); },
+        [row_ptr, cols, vals](int i, int j, long long* c, double* v) {
+            *c = cols[row_ptr[i] + j];
+            *v = vals[row_ptr[i] + j];
+        });
+}
+
+int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_matrix** out)
+{
+    if (nx < 1 || ny < 1 || nz < 1) return set_err(HPCCG_HIP_EINVAL, "nx, ny, nz must be >= 1");
+    const long long n64 = (long long)nx * ny * nz;
+    if (n64 * g_comm.nranks >= (1LL << 31)) return set_err(HPCCG_HIP_EINVAL, "global rows exceed int32");
+    const int n = (int)n64, rank = g_comm.rank, size = g_comm.nranks;
+    auto* M = new hpccg_hip_matrix();
+    HIP_TRY(hipGetDevice(&M->device));
+    M->nrow = n;
+    M->start_row = n * rank;
+    M->total_nrow = n * size;
+    const int nxy = nx * ny;
+    M->ghost_lo = rank > 0 ? std::min(nxy, n) : 0;
+    M->ghost_hi = rank < size - 1 ? std::min(nxy, n) : 0;
+    // rows per z-plane beyond one plane would need rank+-2 (nz >= 1 keeps it at +-1)
+    HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamNonBlocking));
+    int rc = exchange_plan(M);
+    if (rc) {
+        free_matrix(M);
+        return rc;
+    }
+    M->nslices = (n + kSliceRows - 1) / kSliceRows;
+    M->grid = std::max(kNumXcd, (M->nslices + kNumXcd - 1) / kNumXcd * kNumXcd);
+    // row lengths analytically (generate_matrix.cpp:259-281 acceptance test)
+    auto axis = [](int i, int nn) { return 1 + (i > 0) + (i < nn - 1); };
+    const long long total = (long long)n * size;
+    const long long start = (long long)n * rank;
+    auto row_len = [&](int lrow) -> int {
+        const int iz = lrow / nxy, iy = (lrow % nxy) / nx, ix = lrow % nx;
+        const long long grow = start + lrow;
+        const int zl = grow - nxy >= 0, zh = grow + nxy < total;
+        if (use_7pt) return 1 + (ix > 0) + (ix < nx - 1) + (iy > 0) + (iy < ny - 1) + zl + zh;
+        (void)iz;
+        return axis(ix, nx) * axis(iy, ny) * (1 + zl + zh);
+    };
+    std::vector<int> w(M->nslices, 0);
+    long long nnz = 0;
+    for (int i = 0; i < n; i++) {
+        const int l = row_len(i);
+        nnz += l;
+        w[i / kSliceRows] = std::max(w[i / kSliceRows], l);
+    }
+    M->nnz = nnz;
+    int wmax = 0;
+    long long var = 0;
+    for (int s = 0; s < M->nslices; s++) {
+        wmax = std::max(wmax, w[s]);
+        var += w[s];
+    }
+    M->uniform = ((long long)wmax * M->nslices <= var + var / 25) ? 1 : 0;
+    std::vector<unsigned int> sb(M->nslices + 1);
+    long long acc = 0;
+    for (int s = 0; s < M->nslices; s++) {
+        sb[s] = (unsigned int)acc;
+        acc += M->uniform ? wmax : w[s];
+    }
+    sb[M->nslices] = (unsigned int)acc;
+    M->nslots = acc * kSliceRows;
+    M->width = M->uniform ? wmax : 0;
+    M->spmv_variant = (M->uniform && (wmax == 27 || wmax == 7)) ? wmax : 0;
+    rc = [&]() -> int {
+        HIP_TRY(hipMalloc(&M->d_slice_base, sizeof(unsigned int) * sb.size()));
+        HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&M->d_cols, sizeof(int) * std::max(1LL, M->nslots)));
+        HIP_TRY(hipMalloc(&M->d_vals, sizeof(double) * std::max(1LL, M->nslots)));
+        TRY(alloc_workspace(M));
+        HIP_TRY(hipMalloc(&M->d_gen_b, sizeof(double) * M->npad));
+        HIP_TRY(hipMalloc(&M->d_gen_x0, sizeof(double) * M->npad));
+        HIP_TRY(hipMalloc(&M->d_gen_xexact, sizeof(double) * M->npad));
+        HIP_TRY(hipMemset(M->d_gen_b, 0, sizeof(double) * M->npad));
+        HIP_TRY(hipMemset(M->d_gen_x0, 0, sizeof(double) * M->npad));
+        HIP_TRY(hipMemset(M->d_gen_xexact, 0, sizeof(double) * M->npad));
+        launch_generate(nx, ny, nz, rank, size, use_7pt, start - M->ghost_lo, M->d_slice_base, M->d_cols,
+                        M->d_vals, M->d_gen_b, M->d_gen_xexact, n, M->stream);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(M->stream));
+        return 0;
+    }();
+    if (rc) {
+        free_matrix(M);
+        return rc;
+    }
+    *out = M;
+    return 0;
+}
+
+int hpccg_hip_matrix_destroy(hpccg_hip_matrix* M) { return free_matrix(M); }
+
+int hpccg_hip_matrix_info(const hpccg_hip_matrix* M, long long info[8])
+{
+    if (!M) return set_err(HPCCG_HIP_EINVAL, "M is NULL");
+    info[0] = M->nrow;
+    info[1] = (long long)M->ghost_lo + M->nrow + M->ghost_hi;
+    info[2] = M->nnz;
+    info[3] = M->nslots;
+    info[4] = M->ghost_lo;
+    info[5] = M->ghost_hi;
+    info[6] = M->spmv_variant;
+    info[7] = M->uniform ? M->width : 0;
+    return 0;
+}
+
+int hpccg_hip_matrix_vectors(hpccg_hip_matrix* M, double** b, double** x0, double** xexact)
+{
+    if (!M || !M->d_gen_b) return set_err(HPCCG_HIP_EINVAL, "not a device-generated matrix");
+    if (b) *b = M->d_gen_b;
+    if (x0) *x0 = M->d_gen_x0;
+    if (xexact) *xexact = M->d_gen_xexact;
+    return 0;
+}
+
+int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
+{
+    if (!M || !key) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    if (!std::strcmp(key, "use_graph")) {
+        M->use_graph = (int)value;
+    } else if (!std::strcmp(key, "event_timing")) {
+        M->event_timing = (int)value;
+    } else if (!std::strcmp(key, "spmv_variant")) {
+        if (value == 27 || value == 7) {
+            if (!(M->uniform && M->width == value))
+                return set_err(HPCCG_HIP_EINVAL, "variant %lld needs a uniform width-%lld image", value, value);
+        } else if (value != 0 && value != 1) {
+            return set_err(HPCCG_HIP_EINVAL, "unknown spmv variant %lld", value);
+        }
+        M->spmv_variant = (int)value;
+        if (M->graph_exec) {
+            (void)hipGraphExecDestroy(M->graph_exec);
+            M->graph_exec = nullptr;
+        }
+    } else {
+        return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
+    }
+    return 0;
+}
+
+int hpccg_hip_solve_device(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_iter,
+                           double tolerance, int* niters, double* normr, double* times, int print)
+{
+    if (!M || !b_dev || !x_dev || !niters || !normr) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    // The vectorised kernels need 512-row padded buffers: x is staged through
+    // the workspace (x_dev may be any length-n buffer); b likewise unless it
+    // is the generated b, which is already padded.
+    HIP_TRY(hipSetDevice(M->device));
+    double* x = M->d_x;
+    HIP_TRY(hipMemcpyAsync(x, x_dev, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
+    const double* b = b_dev;
+    if (b_dev != M->d_gen_b && b_dev != M->d_b) {
+        HIP_TRY(hipMemcpyAsync(M->d_b, b_dev, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
+        b = M->d_b;
+    }
+    TRY(solve_impl(M, b, x, max_iter, tolerance, niters, normr, times, print));
+    HIP_TRY(hipMemcpyAsync(x_dev, x, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    return 0;
+}
+
+int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tolerance,
+                    int* niters, double* normr, double* times, int print)
+{
+    if (!M || !b || !x || !niters || !normr) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(M->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipMemcpyAsync(M->d_b, b, sizeof(double) * M->nrow, hipMemcpyHostToDevice, M->stream));
+    HIP_TRY(hipMemcpyAsync(M->d_x, x, sizeof(double) * M->nrow, hipMemcpyHostToDevice, M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    const double setup = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    TRY(solve_impl(M, M->d_b, M->d_x, max_iter, tolerance, niters, normr, times, print));
+    HIP_TRY(hipMemcpy(x, M->d_x, sizeof(double) * M->nrow, hipMemcpyDeviceToHost));
+    if (times) times[6] = setup;
+    return 0;
+}
+
+int hpccg_hip_kernel_times(const hpccg_hip_matrix* M, double out[4])
+{
+    if (!M || !out) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    for (int i = 0; i < 4; i++) out[i] = M->ktimes[i];
+    return 0;
+}
+
+int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap)
+{
+    if (!M || !out) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    const int n = std::min<int>(cap, (int)M->trace.size());
+    for (int i = 0; i < n; i++) out[i] = M->trace[i];
+    return n;
+}
+
+int hpccg_hip_sparsemv(hpccg_hip_matrix* M, const double* x_dev, double* y_dev)
+{
+    if (!M || !x_dev || !y_dev) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(M->device));
+    // stage x into p (the halo-carrying buffer), exchange, multiply
+    HIP_TRY(hipMemcpyAsync(M->d_p, x_dev, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
+    TRY(enqueue_halo(M, M->d_p));
+    CgArgs a = make_args(M, nullptr, nullptr, 0, 0.0);
+    launch_sparsemv(a, M->d_p - M->ghost_lo, y_dev, 0, M->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    return 0;
+}
+
+int hpccg_hip_ddot(int n, const double* x_dev, const double* y_dev, double* result)
+{
+    if (n < 0 || !result || (n > 0 && (!x_dev || !y_dev))) return set_err(HPCCG_HIP_EINVAL, "bad argument");
+    const int nparts = ddot_nparts(n);
+    TRY(scratch_for(nparts));
+    launch_ddot(n, x_dev, y_dev, g_scratch.partial, nparts, g_scratch.out, g_scratch.s);
+    HIP_TRY(hipGetLastError());
+    if (g_comm.nranks > 1)
+        NCCL_TRY(ncclAllReduce(g_scratch.out, g_scratch.out + 1, 1, ncclFloat64, ncclSum, g_comm.comm,
+                               g_scratch.s));
+    HIP_TRY(hipMemcpyAsync(result, g_scratch.out + (g_comm.nranks > 1 ? 1 : 0), sizeof(double),
+                           hipMemcpyDeviceToHost, g_scratch.s));
+    HIP_TRY(hipStreamSynchronize(g_scratch.s));
+    return 0;
+}
+
+int hpccg_hip_waxpby(int n, double alpha, const double* x_dev, double beta, const double* y_dev,
+                     double* w_dev)
+{
+    if (n < 0 || (n > 0 && (!x_dev || !y_dev || !w_dev))) return set_err(HPCCG_HIP_EINVAL, "bad argument");
+    TRY(scratch_for(1));
+    launch_waxpby(n, alpha, x_dev, beta, y_dev, w_dev, g_scratch.s);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(g_scratch.s));
+    return 0;
+}
+
+int hpccg_hip_HPCCG(HPC_Sparse_Matrix* A, double* b, double* x, int max_iter, double tolerance,
+                    int* niters, double* normr, double* times)
+{
+    hpccg_hip_matrix* M = nullptr;
+    double setup = 0.0;
+    {
+        std::lock_guard<std::mutex> lk(g_dropin_mu);
+        auto it = g_dropin_cache.find(A);
+        if (it != g_dropin_cache.end()) {
+            M = it->second;
+        } else {
+            const auto t0 = std::chrono::steady_clock::now();
+            TRY(hpccg_hip_matrix_create(A, &M));
+            setup = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            g_dropin_cache[A] = M;
+        }
+    }
+    TRY(hpccg_hip_solve(M, b, x, max_iter, tolerance, niters, normr, times, 1));
+    if (times) times[6] += setup;
+    return 0;
+}
+
+long long hpccg_sell_build(int nrow, long long col_base, long long ncol_ext, const long long* row_ptr,
+                           const int* cols, const double* vals, unsigned int* slice_base, int* sell_cols,
+                           double* sell_vals)
+{
+    auto row_len = [row_ptr](int i) { return (int)(row_ptr[i + 1] - row_ptr[i]); };
+    auto row_at = [row_ptr, cols, vals](int i, int j, long long* c, double* v) {
+        *c = cols[row_ptr[i] + j];
+        *v = vals ? vals[row_ptr[i] + j] : 0.0;
+    };
+    std::vector<unsigned int> tmp;
+    if (!slice_base) {
+        tmp.resize((nrow + kSliceRows - 1) / kSliceRows + 1);
+        slice_base = tmp.data();
+    }
+    const long long var = sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, slice_base, nullptr,
+                                          nullptr, 0, nullptr);
+    const long long uni = sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, slice_base, nullptr,
+                                          nullptr, 1, nullptr);
+    const int uniform = (uni <= var + var / 25) ? 1 : 0;
+    int bad = 0;
+    const long long r = sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, slice_base, sell_cols,
+                                        sell_vals, uniform, &bad);
+    return bad ? HPCCG_HIP_EPLAN : r;
+}
+
+int hpccg_halo_plan(int nrow, int start_row, int total_nrow, const long long* row_ptr, const int* cols,
+                    int plan_out[4])
+{
+    long long mn = start_row, mx = (long long)start_row + nrow - 1;
+    for (long long e = 0; e < (nrow > 0 ? row_ptr[nrow] : 0); e++) {
+        mn = std::min<long long>(mn, cols[e]);
+        mx = std::max<long long>(mx, cols[e]);
+    }
+    if (mn < 0 || mx >= total_nrow) return set_err(HPCCG_HIP_EPLAN, "column outside [0, total_nrow)");
+    plan_out[0] = (int)(start_row - mn);
+    plan_out[1] = (int)(mx - ((long long)start_row + nrow - 1));
+    plan_out[2] = (int)mn;
+    plan_out[3] = (int)mx;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,253 @@
+// test_HPCCG.cpp -- the reference command line, MI355X edition.
+//
+//   test_HPCCG nx ny nz          (Mode 1, main.cpp:146-159)
+//   test_HPCCG HPC_data_file     (Mode 2, deprecated in the reference; not built here)
+//
+// Same stdout as the reference (main.cpp:136-305): residual lines, "Elapsed
+// time: X s", then the YAML report (also written to ./hpccg-1.0_<stamp>.yaml).
+// GPU-specific figures are appended under an extra "GPU Summary" key; no
+// reference key is changed.
+//
+// Multi-GPU (the reference's `mpirun -np P test_HPCCG nx ny nz`): start one
+// process per GPU with WORLD_SIZE / RANK / LOCAL_RANK set (torchrun, or
+// hpccg-sycl_amd/bin/hpccg_launch) and HPCCG_ID_FILE naming a shared path for
+// the RCCL unique id. nz is per rank; the global grid is nx x ny x (P*nz).
+//
+// Environment knobs (the reference only had compile-time switches):
+//   HPCCG_MAX_ITER   (default 500, main.cpp:187)
+//   HPCCG_7PT=1      use_7pt_stencil (generate_matrix.cpp:219)
+//   HPCCG_DEVICE_GENERATE=1  build the matrix on the GPU instead of the host
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/HPC_Sparse_Matrix.hpp"
+#include "../../include/hpccg_hip.h"
+#include "yaml_report.hpp"
+
+namespace {
+
+int env_int(const char* name, int dflt)
+{
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+void die(const char* what)
+{
+    std::cerr << what << ": " << hpccg_hip_last_error() << std::endl;
+    std::exit(2);
+}
+
+// Rank 0 writes the RCCL unique id to HPCCG_ID_FILE; the others wait for it.
+void init_comm(int nranks, int rank)
+{
+    unsigned char id[128];
+    const char* path = std::getenv("HPCCG_ID_FILE");
+    if (!path) {
+        std::cerr << "HPCCG_ID_FILE must name a shared file for multi-rank runs" << std::endl;
+        std::exit(2);
+    }
+    if (rank == 0) {
+        if (hpccg_hip_comm_unique_id(id)) die("ncclGetUniqueId");
+        const std::string tmp = std::string(path) + ".tmp";
+        std::ofstream(tmp, std::ios::binary).write(reinterpret_cast<const char*>(id), 128);
+        std::rename(tmp.c_str(), path);
+    } else {
+        for (int tries = 0;; tries++) {
+            std::ifstream f(path, std::ios::binary);
+            if (f && f.read(reinterpret_cast<char*>(id), 128) && f.gcount() == 128) break;
+            if (tries > 6000) {
+                std::cerr << "timed out waiting for " << path << std::endl;
+                std::exit(2);
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        }
+    }
+    if (hpccg_hip_comm_init(id, nranks, rank)) die("ncclCommInitRank");
+}
+
+}  // namespace
+
+int main(int argc, char* argv[])
+{
+    const int size = env_int("WORLD_SIZE", 1);
+    const int rank = env_int("RANK", 0);
+    const int local_rank = env_int("LOCAL_RANK", rank);
+
+    if (argc != 2 && argc != 4) {
+        if (rank == 0)
+            std::cerr << "Usage:" << std::endl
+                      << "Mode 1: " << argv[0] << " nx ny nz" << std::endl
+                      << "     where nx, ny and nz are the local sub-block dimensions, or" << std::endl
+                      << "Mode 2: " << argv[0] << " HPC_data_file " << std::endl
+                      << "     where HPC_data_file is a globally accessible file containing matrix data."
+                      << std::endl;
+        std::exit(1);
+    }
+    if (argc == 2) {
+        std::cerr << "Mode 2 (HPC_data_file) is not available in this build; use: " << argv[0]
+                  << " nx ny nz" << std::endl;
+        std::exit(1);
+    }
+    const int nx = std::atoi(argv[1]), ny = std::atoi(argv[2]), nz = std::atoi(argv[3]);
+    const int max_iter = env_int("HPCCG_MAX_ITER", 500);
+    const int use_7pt = env_int("HPCCG_7PT", 0);
+    const bool dev_gen = env_int("HPCCG_DEVICE_GENERATE", 0) != 0;
+    const double tolerance = 0.0;  // main.cpp:188
+
+    int ndev = 0;
+    if (hpccg_hip_device_count(&ndev)) die("no HIP device");
+    if (hpccg_hip_set_device(local_rank % ndev)) die("hipSetDevice");
+    if (size > 1) init_comm(size, rank);
+
+    double times[7] = {0, 0, 0, 0, 0, 0, 0};
+    HPC_Sparse_Matrix* A = nullptr;
+    double *x = nullptr, *b = nullptr, *xexact = nullptr;
+    hpccg_hip_matrix* M = nullptr;
+    const auto ts = std::chrono::steady_clock::now();
+    if (dev_gen) {
+        if (hpccg_hip_matrix_generate(nx, ny, nz, use_7pt, &M)) die("device generate");
+    } else {
+        if (hpccg_generate_matrix(nx, ny, nz, rank, size, use_7pt, &A, &x, &b, &xexact))
+            die("generate_matrix");
+        if (hpccg_hip_matrix_create(A, &M)) die("matrix upload");
+    }
+    times[6] = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
+
+    int niters = 0;
+    double normr = 0.0;
+    const long long n = (long long)nx * ny * nz;
+    std::vector<double> xv;
+    int ierr;
+    const auto start = std::chrono::high_resolution_clock::now();
+    if (dev_gen) {
+        double *db, *dx0, *dxe;
+        hpccg_hip_matrix_vectors(M, &db, &dx0, &dxe);
+        double* dx = nullptr;
+        if (hipMalloc(&dx, sizeof(double) * n) != hipSuccess || hipMemset(dx, 0, sizeof(double) * n) != hipSuccess)
+            die("hipMalloc");
+        ierr = hpccg_hip_solve_device(M, db, dx, max_iter, tolerance, &niters, &normr, times, 1);
+        xv.resize(n);
+        if (hipMemcpy(xv.data(), dx, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess) die("hipMemcpy");
+        (void)hipFree(dx);
+    } else {
+        double t6 = times[6];
+        ierr = hpccg_hip_solve(M, b, x, max_iter, tolerance, &niters, &normr, times, 1);
+        times[6] = t6;
+    }
+    const auto end = std::chrono::high_resolution_clock::now();
+    std::chrono::duration<double> elapsed = end - start;
+    if (rank == 0) std::cout << "Elapsed time: " << elapsed.count() << " s\n";
+    if (ierr) std::cerr << "Error in call to CG: " << ierr << ".\n" << hpccg_hip_last_error() << std::endl;
+
+    // residual vs xexact (compute_residual.cpp:59-81), max over ranks
+    double resid = 0.0;
+    {
+        const double* xs = dev_gen ? xv.data() : x;
+        for (long long i = 0; i < n; i++) resid = std::max(resid, std::fabs(xs[i] - 1.0));
+        if (std::isnan(resid)) resid = NAN;
+    }
+    double t4 = times[4], t4min = t4, t4max = t4, t4avg = t4;
+    if (size > 1) {
+        hpccg_hip_comm_allreduce_host(&t4min, 1, 1);
+        hpccg_hip_comm_allreduce_host(&t4max, 1, 2);
+        hpccg_hip_comm_allreduce_host(&t4avg, 1, 0);
+        t4avg /= size;
+        hpccg_hip_comm_allreduce_host(&resid, 1, 2);
+    }
+
+    if (rank == 0) {
+        long long info[8];
+        hpccg_hip_matrix_info(M, info);
+        const double fniters = niters;
+        const double fnrow = (double)n * size;
+        const double fnnz = 27.0 * fnrow;  // total_nnz as the reference stores it (main.cpp:222)
+        const double fnops_ddot = fniters * 4 * fnrow;
+        const double fnops_waxpby = fniters * 6 * fnrow;
+        const double fnops_sparsemv = fniters * 2 * fnnz;
+        const double fnops = fnops_ddot + fnops_waxpby + fnops_sparsemv;
+
+        hpccg::Report doc("hpccg", "1.0");
+        doc.add("Parallelism", "");
+        if (size > 1)
+            doc.get("Parallelism")->add("Number of MPI ranks", size);
+        else
+            doc.get("Parallelism")->add("MPI not enabled", "");
+        doc.get("Parallelism")->add("OpenMP not enabled", "");
+        doc.get("Parallelism")->add("SYCL not enabled", "");
+        doc.add("Dimensions", "");
+        doc.get("Dimensions")->add("nx", nx);
+        doc.get("Dimensions")->add("ny", ny);
+        doc.get("Dimensions")->add("nz", nz);
+        doc.add("Number of iterations", niters);
+        doc.add("Final residual", normr);
+        doc.add("#********** Performance Summary (times in sec) ***********", "");
+        doc.add("Time Summary", "");
+        doc.get("Time Summary")->add("Total   ", times[0]);
+        doc.get("Time Summary")->add("DDOT    ", times[1]);
+        doc.get("Time Summary")->add("WAXPBY  ", times[2]);
+        doc.get("Time Summary")->add("SPARSEMV", times[3]);
+        doc.add("FLOPS Summary", "");
+        doc.get("FLOPS Summary")->add("Total   ", fnops);
+        doc.get("FLOPS Summary")->add("DDOT    ", fnops_ddot);
+        doc.get("FLOPS Summary")->add("WAXPBY  ", fnops_waxpby);
+        doc.get("FLOPS Summary")->add("SPARSEMV", fnops_sparsemv);
+        doc.add("MFLOPS Summary", "");
+        doc.get("MFLOPS Summary")->add("Total   ", fnops / times[0] / 1.0E6);
+        doc.get("MFLOPS Summary")->add("DDOT    ", fnops_ddot / times[1] / 1.0E6);
+        doc.get("MFLOPS Summary")->add("WAXPBY  ", fnops_waxpby / times[2] / 1.0E6);
+        doc.get("MFLOPS Summary")->add("SPARSEMV", fnops_sparsemv / (times[3]) / 1.0E6);
+        if (size > 1) {
+            doc.add("DDOT Timing Variations", "");
+            doc.get("DDOT Timing Variations")->add("Min DDOT MPI_Allreduce time", t4min);
+            doc.get("DDOT Timing Variations")->add("Max DDOT MPI_Allreduce time", t4max);
+            doc.get("DDOT Timing Variations")->add("Avg DDOT MPI_Allreduce time", t4avg);
+            const double tot = times[3] + times[5] + times[6];
+            doc.add("SPARSEMV OVERHEADS", "");
+            auto* o = doc.get("SPARSEMV OVERHEADS");
+            o->add("SPARSEMV MFLOPS W OVERHEAD", fnops_sparsemv / tot / 1.0E6);
+            o->add("SPARSEMV PARALLEL OVERHEAD Time", times[5] + times[6]);
+            o->add("SPARSEMV PARALLEL OVERHEAD Pct", (times[5] + times[6]) / tot * 100.0);
+            o->add("SPARSEMV PARALLEL OVERHEAD Setup Time", times[6]);
+            o->add("SPARSEMV PARALLEL OVERHEAD Setup Pct", times[6] / tot * 100.0);
+            o->add("SPARSEMV PARALLEL OVERHEAD Bdry Exch Time", times[5]);
+            o->add("SPARSEMV PARALLEL OVERHEAD Bdry Exch Pct", times[5] / tot * 100.0);
+        }
+        // appended (not in the reference): MI355X figures
+        char dname[256] = {0};
+        int cus = 0;
+        hpccg_hip_device_name(dname, sizeof dname, &cus);
+        const double spmv_bytes = 12.0 * (double)info[2] + 20.0 * (double)info[0];
+        const double spmv_calls = niters + 1.0;
+        const double gbs = times[3] > 0 ? spmv_bytes * spmv_calls / times[3] / 1e9 : 0.0;
+        doc.add("GPU Summary", "");
+        auto* gs = doc.get("GPU Summary");
+        gs->add("Device", std::string(dname));
+        gs->add("Compute units", cus);
+        gs->add("GPU ranks", size);
+        gs->add("Stored nonzeros per rank", (long long)info[2]);
+        gs->add("SELL-512 slots per rank", (long long)info[3]);
+        gs->add("CG iterations per second", times[0] > 0 ? fniters / times[0] : 0.0);
+        gs->add("SPARSEMV effective GB/s per rank", gbs);
+        gs->add("SPARSEMV fraction of 8 TB/s HBM peak", gbs / 8000.0);
+        gs->add("Setup time (generate + upload)", times[6]);
+        gs->add("Difference between computed and exact", resid);
+        std::cout << doc.render(true);
+    }
+
+    hpccg_hip_matrix_destroy(M);
+    if (A) hpccg_free_problem(A, x, b, xexact);
+    if (size > 1) hpccg_hip_comm_destroy();
+    return 0;
+}

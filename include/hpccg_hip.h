@@ -1,0 +1,146 @@
+/*
+ * hpccg_hip.h -- C ABI of the MI355X-native HPCCG hot path (libhpccg_hip.so).
+ *
+ * Plain pointers and sizes only. Every entry point replaces one interface of
+ * the reference (Dart120/HPCCG-SYCL, file:line cited per function). Return
+ * value: 0 on success, a negative HPCCG_HIP_E* code on failure (the message
+ * is available from hpccg_hip_last_error()). The reference itself has no
+ * error path (HPCCG.cpp:401 always returns 0; fatal conditions abort).
+ *
+ * Layout on the device (per GPU / rank):
+ *   matrix   SELL-512: slices of 512 consecutive rows, slot-major inside a
+ *            slice (vals[slice][slot][512] fp64, cols[...] int32, padding
+ *            col = -1); slice width = max row length in the slice; entry
+ *            order per row is the caller's order (so rounding matches).
+ *   vectors  fp64, length padded to a multiple of 512; p carries the halo:
+ *            [ghost_lo | local rows | ghost_hi].
+ */
+#ifndef HPCCG_HIP_H
+#define HPCCG_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct HPC_Sparse_Matrix_STRUCT;
+typedef struct hpccg_hip_matrix hpccg_hip_matrix; /* opaque, device resident */
+
+#define HPCCG_HIP_OK 0
+#define HPCCG_HIP_EINVAL (-1)  /* bad argument / shape */
+#define HPCCG_HIP_EHIP (-2)    /* HIP runtime error */
+#define HPCCG_HIP_ERCCL (-3)   /* RCCL error */
+#define HPCCG_HIP_ENOMEM (-4)  /* device allocation failed */
+#define HPCCG_HIP_EPLAN (-5)   /* matrix couples ranks other than r-1, r+1 */
+#define HPCCG_HIP_ENODEV (-6)  /* no HIP device */
+
+/* ---- library ---------------------------------------------------------- */
+int hpccg_hip_abi_version(void);            /* == 1 */
+const char* hpccg_hip_last_error(void);     /* thread-local message */
+int hpccg_hip_device_count(int* count);
+int hpccg_hip_set_device(int device);       /* one GPU per rank/process */
+
+/* ---- communicator: replaces MPI_COMM_WORLD in ddot.cpp:75-85,
+ *      exchange_externals.cpp:51-131 and make_local_matrix.cpp:185-201.
+ *      RCCL over xGMI; one rank per GPU. Without a communicator the
+ *      library runs single-GPU (nranks = 1). ---------------------------- */
+int hpccg_hip_comm_unique_id(unsigned char id_out[128]);
+int hpccg_hip_comm_init(const unsigned char id[128], int nranks, int rank);
+int hpccg_hip_comm_destroy(void);
+int hpccg_hip_comm_size(int* nranks, int* rank);
+/* Host-value all-reduce over the communicator (main.cpp:206-208,
+ * compute_residual.cpp:73): op 0 = sum, 1 = min, 2 = max. In place. */
+int hpccg_hip_comm_allreduce_host(double* vals, int n, int op);
+/* Device name and compute-unit count of the current device. */
+int hpccg_hip_device_name(char* buf, int cap, int* compute_units);
+
+/* ---- host-side input (the reference's generate_matrix.cpp:196-307) ------
+ * Builds the reference HPC_Sparse_Matrix for rank `rank` of `size`
+ * z-stacked slabs (global column indices), plus x0 = 0, b, xexact = 1.
+ * use_7pt selects the 7-point stencil (generate_matrix.cpp:219). Arrays are
+ * allocated with new[]; free with hpccg_free_problem. */
+int hpccg_generate_matrix(int nx, int ny, int nz, int rank, int size, int use_7pt,
+                          struct HPC_Sparse_Matrix_STRUCT** A, double** x, double** b,
+                          double** xexact);
+void hpccg_free_problem(struct HPC_Sparse_Matrix_STRUCT* A, double* x, double* b,
+                        double* xexact);
+
+/* ---- device matrix -------------------------------------------------------
+ * hpccg_hip_matrix_create: converts the caller's HPC_Sparse_Matrix
+ * (HPC_Sparse_Matrix.hpp:54-85; read-only, caller keeps ownership) to
+ * SELL-512 and uploads it. Global column indices in [start_row - G_lo,
+ * stop_row + G_hi] are localised against rank+-1 (the z-slab plan that
+ * make_local_matrix.cpp:58-610 derives with MPI); anything else returns
+ * HPCCG_HIP_EPLAN. Collective over the communicator when nranks > 1. */
+int hpccg_hip_matrix_create(const struct HPC_Sparse_Matrix_STRUCT* A, hpccg_hip_matrix** out);
+/* Same from plain CSR (row_ptr[nrow+1] int64, cols int32 global, vals fp64). */
+int hpccg_hip_matrix_create_csr(int nrow, int start_row, int total_nrow, const long long* row_ptr,
+                                const int* cols, const double* vals, hpccg_hip_matrix** out);
+/* Generate the stencil matrix directly on the GPU in SELL-512 layout
+ * (same entries, same order as generate_matrix.cpp:251-289), with b and
+ * xexact on the device. Rank/size from the communicator. */
+int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_matrix** out);
+int hpccg_hip_matrix_destroy(hpccg_hip_matrix* M);
+/* nrow, ncol (incl. ghosts), stored nnz, SELL slots (incl. padding). */
+int hpccg_hip_matrix_info(const hpccg_hip_matrix* M, long long info_out[8]);
+/* Device pointers owned by M: b, x0 (zeros) and xexact of a generated matrix. */
+int hpccg_hip_matrix_vectors(hpccg_hip_matrix* M, double** b_dev, double** x0_dev,
+                             double** xexact_dev);
+
+/* ---- solver: replaces HPCCG() HPCCG.cpp:312-402 ----------------------------
+ * Host-pointer form (b, x host; x in/out). times[0..6]:
+ * [0] solve total, [1] DDOT (incl. all-reduce), [2] WAXPBY, [3] SPARSEMV,
+ * [4] all-reduce, [5] halo exchange, [6] setup (H2D of b, x).
+ * Residual lines (HPCCG.cpp:356,372-373) are printed by rank 0 when
+ * print != 0. */
+int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_iter,
+                    double tolerance, int* niters, double* normr, double* times, int print);
+/* Device-pointer form: b_dev, x_dev already in HBM (x_dev in/out); nothing
+ * crosses PCIe inside. The bench's timed step. */
+int hpccg_hip_solve_device(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_iter,
+                           double tolerance, int* niters, double* normr, double* times,
+                           int print);
+/* normr computed in each iteration of the last solve: out[0] = initial
+ * residual, out[k] = iteration k (k <= niters). Returns entries written. */
+int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
+/* Solver knobs: "use_graph" (capture CG iterations in a hipGraph; default
+ * on for nranks == 1), "spmv_variant" (0 = auto), "event_timing" (1 = bracket
+ * every SpMV and fused-update launch with hipEvents on the solver stream;
+ * eager launches). */
+int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value);
+/* hipEvent kernel timings of the last solve with event_timing on:
+ * out[0] SpMV total ms, out[1] SpMV launches, out[2] fused-update total ms,
+ * out[3] update launches (launches that did work, i.e. <= niters + 1). */
+int hpccg_hip_kernel_times(const hpccg_hip_matrix* M, double out[4]);
+
+/* ---- kernel level, device pointers, synchronous ----------------------------
+ * hpccg_hip_sparsemv: HPC_sparsemv.cpp:68-89. x_dev has the local rows (the
+ * halo is exchanged from it on multi-rank runs), y_dev local rows. */
+int hpccg_hip_sparsemv(hpccg_hip_matrix* M, const double* x_dev, double* y_dev);
+/* ddot.cpp:60-88: deterministic two-stage reduction; all-reduced over the
+ * communicator when nranks > 1. Result to host. */
+int hpccg_hip_ddot(int n, const double* x_dev, const double* y_dev, double* result);
+/* waxpby.cpp:69-93: w = alpha*x + beta*y (w may alias x or y). */
+int hpccg_hip_waxpby(int n, double alpha, const double* x_dev, double beta, const double* y_dev,
+                     double* w_dev);
+
+/* ---- drop-in driver: HPCCG.hpp:61-63 with C linkage. Prepares (and caches
+ * by A) the device matrix, then runs hpccg_hip_solve. --------------------- */
+int hpccg_hip_HPCCG(struct HPC_Sparse_Matrix_STRUCT* A, double* b, double* x, int max_iter,
+                    double tolerance, int* niters, double* normr, double* times);
+
+/* ---- host-only helpers (no GPU needed; used by the CPU test suite) -------
+ * Converts CSR rows [0, nrow) with global columns into the SELL-512 image the
+ * device uses. First call with vals/cols = NULL to size: returns the number
+ * of SELL slots; slice_base has nslices+1 entries (units of 512 slots). */
+long long hpccg_sell_build(int nrow, long long col_base, long long ncol_ext, const long long* row_ptr,
+                           const int* cols, const double* vals, unsigned int* slice_base,
+                           int* sell_cols, double* sell_vals);
+/* z-slab halo plan for a CSR slab: ghost_lo/ghost_hi from the column range
+ * (see hpccg_hip_matrix_create). Returns 0 or HPCCG_HIP_EPLAN. */
+int hpccg_halo_plan(int nrow, int start_row, int total_nrow, const long long* row_ptr,
+                    const int* cols, int plan_out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

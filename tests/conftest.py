@@ -59,3 +59,33 @@ def check_trace(tr_test, tr_ref, rtol):
         assert abs(rt - rr) <= rtol * rr, (k, rt, rr, abs(rt - rr) / rr)
         checked += 1
     return checked
+
+
+def load_pkg():
+    """Import hpccg-sycl_amd/ (hyphenated dir) as module hpccg_sycl_amd."""
+    import importlib.util
+    name = "hpccg_sycl_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    spec = importlib.util.spec_from_file_location(
+        name, os.path.join(ROOT, "hpccg-sycl_amd", "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.fixture(scope="session")
+def hp():
+    return load_pkg()
+
+
+@pytest.fixture(scope="session")
+def gpu(hp):
+    """GPU tests: the HIP library must load and see a device -- no fallback."""
+    import torch
+    assert torch.cuda.is_available(), "gpu test without a visible HIP device"
+    hp.lib()
+    assert hp.device_count() >= 1
+    hp.set_device(0)
+    return torch.device("cuda:0")
