@@ -65,7 +65,7 @@ def lib() -> C.CDLL:
         import torch  # noqa: F401
     except Exception:
         pass
-    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    L = C.CDLL(LIB_PATH)  # RTLD_LOCAL: never interpose HPCCG() into other libraries
     vp, ip, dp, lp = C.c_void_p, C.c_int, C.c_double, C.c_longlong
     PI, PD = C.POINTER(C.c_int), C.POINTER(C.c_double)
     sig = {
@@ -93,6 +93,7 @@ def lib() -> C.CDLL:
         "hpccg_hip_last_trace": (ip, [vp, PD, ip]),
         "hpccg_hip_set_option": (ip, [vp, C.c_char_p, lp]),
         "hpccg_hip_kernel_times": (ip, [vp, PD]),
+        "hpccg_hip_diag_spmv": (ip, [vp, ip, ip, PD]),
         "hpccg_hip_sparsemv": (ip, [vp, vp, vp]),
         "hpccg_hip_ddot": (ip, [ip, vp, vp, PD]),
         "hpccg_hip_waxpby": (ip, [ip, dp, vp, dp, vp, vp]),
@@ -244,6 +245,12 @@ class Matrix:
         _check(lib().hpccg_hip_kernel_times(self.h, out), "kernel_times")
         return {"spmv_ms": out[0], "spmv_launches": int(out[1]), "update_ms": out[2],
                 "update_launches": int(out[3])}
+
+    def diag_spmv(self, variant: int, reps: int = 20) -> float:
+        """Average us per launch of SpMV variant (diagnostic sweep)."""
+        us = C.c_double(0.0)
+        _check(lib().hpccg_hip_diag_spmv(self.h, variant, reps, C.byref(us)), "diag_spmv")
+        return us.value
 
     def last_trace(self, cap: int = 100000) -> np.ndarray:
         out = np.zeros(cap, np.float64)

@@ -64,6 +64,7 @@ struct CgArgs {
 void launch_cg_prologue_copy(const CgArgs& a, hipStream_t s);   // p = x + 0*x
 void launch_cg_p_update(const CgArgs& a, hipStream_t s);        // p = r + beta p
 void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s);
+bool spmv_variant_ok(int variant);
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s);
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);

@@ -129,6 +129,58 @@ __device__ __forceinline__ void st(double* __restrict__ p, const Rows<kRpt>& r)
 }
 
 template <int kRpt>
+__device__ __forceinline__ void ld_cols(const int* __restrict__ p, int (&c)[kRpt]);
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef int i2v __attribute__((ext_vector_type(2)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+// Matrix streams: optionally non-temporal (read once per SpMV; keeps L2 for x).
+template <int kRpt, bool kNT>
+__device__ __forceinline__ Rows<kRpt> ld_m(const double* __restrict__ p)
+{
+    if constexpr (!kNT) {
+        return ld<kRpt>(p);
+    } else {
+        Rows<kRpt> r;
+        if constexpr (kRpt == 1) {
+            r.v[0] = __builtin_nontemporal_load(p);
+        } else {
+#pragma unroll
+            for (int i = 0; i < kRpt; i += 2) {
+                const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p + i));
+                r.v[i] = t.x;
+                r.v[i + 1] = t.y;
+            }
+        }
+        return r;
+    }
+}
+
+template <int kRpt, bool kNT>
+__device__ __forceinline__ void ld_cols_m(const int* __restrict__ p, int (&c)[kRpt])
+{
+    if constexpr (!kNT) {
+        ld_cols<kRpt>(p, c);
+    } else if constexpr (kRpt == 1) {
+        c[0] = __builtin_nontemporal_load(p);
+    } else if constexpr (kRpt == 2) {
+        const i2v t = __builtin_nontemporal_load(reinterpret_cast<const i2v*>(p));
+        c[0] = t.x;
+        c[1] = t.y;
+    } else {
+#pragma unroll
+        for (int i = 0; i < kRpt; i += 4) {
+            const i4v t = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(p + i));
+            c[i] = t.x;
+            c[i + 1] = t.y;
+            c[i + 2] = t.z;
+            c[i + 3] = t.w;
+        }
+    }
+}
+
+template <int kRpt>
 __device__ __forceinline__ void ld_cols(const int* __restrict__ p, int (&c)[kRpt])
 {
     if constexpr (kRpt == 1) {
@@ -216,7 +268,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_p_update(CgArgs a)
 // for the stencil the 64 lanes of a wave hit consecutive x.
 // kW > 0: slice width known at compile time (27 / 7), fully unrolled.
 // ---------------------------------------------------------------------------
-template <int kRpt, int kW>
+template <int kRpt, int kW, bool kNT = false>
 __device__ __forceinline__ void spmv_rows(const CgArgs& a, const double* __restrict__ xext, int s,
                                           double (&sum)[kRpt])
 {
@@ -233,8 +285,8 @@ __device__ __forceinline__ void spmv_rows(const CgArgs& a, const double* __restr
 #pragma unroll
         for (int j = 0; j < kW; j++) {
             int c[kRpt];
-            ld_cols<kRpt>(cp + (size_t)j * kSliceRows, c);
-            const Rows<kRpt> v = ld<kRpt>(vp + (size_t)j * kSliceRows);
+            ld_cols_m<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
+            const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
 #pragma unroll
             for (int i = 0; i < kRpt; i++) {
                 const double xv = (c[i] >= 0) ? xext[c[i]] : 0.0;
@@ -245,8 +297,8 @@ __device__ __forceinline__ void spmv_rows(const CgArgs& a, const double* __restr
 #pragma unroll 3
         for (int j = 0; j < w; j++) {
             int c[kRpt];
-            ld_cols<kRpt>(cp + (size_t)j * kSliceRows, c);
-            const Rows<kRpt> v = ld<kRpt>(vp + (size_t)j * kSliceRows);
+            ld_cols_m<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
+            const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
 #pragma unroll
             for (int i = 0; i < kRpt; i++) {
                 const double xv = (c[i] >= 0) ? xext[c[i]] : 0.0;
@@ -259,8 +311,8 @@ __device__ __forceinline__ void spmv_rows(const CgArgs& a, const double* __restr
 // Padding slots add v*x = 0*0 = +0: a sum that starts at +0.0 is never -0 under
 // round-to-nearest, so +0 leaves every row sum bit-identical to skipping it.
 
-template <int kRpt, int kW, bool kDot>
-__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv(CgArgs a, bool prologue)
+template <int kRpt, int kW, bool kDot, int kMinW = 1, bool kNT = false>
+__global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, bool prologue)
 {
     if (!prologue) {
         const int k = a.kst[0];
@@ -277,7 +329,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv(CgArgs a, bool prolo
     if (s >= a.nslices) return;
     const double* __restrict__ xext = a.p - a.ghost_lo;
     double sum[kRpt];
-    spmv_rows<kRpt, kW>(a, xext, s, sum);
+    spmv_rows<kRpt, kW, kNT>(a, xext, s, sum);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     Rows<kRpt> o;
 #pragma unroll
@@ -315,6 +367,32 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_plain(CgArgs a, cons
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     for (int i = 0; i < kRpt; i++)
         if (row + i < a.n) y[row + i] = sum[i];
+}
+
+// Diagnostic only (never in the CG path): streams the SELL image like the
+// SpMV but without the x gather -- the matrix-streaming ceiling.
+template <int kW>
+__global__ __launch_bounds__(256) void k_stream_diag(CgArgs a)
+{
+    const int s = xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    const size_t base = (size_t)s * kW * kSliceRows + (size_t)threadIdx.x * 2;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < kW; j++) {
+        int c[2];
+        ld_cols<2>(a.cols + base + (size_t)j * kSliceRows, c);
+        const Rows<2> v = ld<2>(a.vals + base + (size_t)j * kSliceRows);
+        s0 = s0 + v.v[0] * (double)c[0];
+        s1 = s1 + v.v[1] * (double)c[1];
+    }
+    const int row = s * kSliceRows + threadIdx.x * 2;
+    if (row + 2 <= a.n) {
+        Rows<2> o;
+        o.v[0] = s0;
+        o.v[1] = s1;
+        st<2>(a.Ap + row, o);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -540,25 +618,57 @@ void launch_cg_p_update(const CgArgs& a, hipStream_t s)
     hipLaunchKernelGGL(k_p_update<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
 }
 
-// variant: 0 = runtime slice width (any matrix), 27 / 7 = uniform-width fast
-// path chosen by the host when every slice has that width.
+// SpMV variants. All compute every row bitwise identically; the p.Ap
+// partial's summation tree depends only on rows-per-thread (kRpt), so
+// variants with equal kRpt give bitwise-equal CG traces.
+//   0 runtime width, 2 rows/thread      1 runtime width, 1 row/thread
+//   2 runtime width, 4 rows/thread
+//   27 / 7  uniform width, fully unrolled, 2 rows/thread
+//   100*w + 27: same with __launch_bounds__ min waves/SIMD w (w = 1..4)
+//   +1000: non-temporal loads of vals/cols
+//   9999: diagnostic matrix stream without the gather (not an SpMV)
+#define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
+    hipLaunchKernelGGL((k_spmv<RPT, W, true, MINW, NT>), dim3(a.grid), dim3(kSliceRows / RPT), 0, s, \
+                       a, prologue)
+bool spmv_variant_ok(int v)
+{
+    switch (v) {
+    case 0: case 1: case 2: case 27: case 7: case 127: case 227: case 327: case 427: case 527:
+    case 627: case 1000: case 1027: case 1007: case 1127: case 1227: case 1327: case 1427:
+    case 1527: case 1627: case 9999:
+        return true;
+    default:
+        return false;
+    }
+}
+
 void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
 {
     switch (variant) {
-    case 27:
-        hipLaunchKernelGGL((k_spmv<kRpt, 27, true>), dim3(a.grid), dim3(kBlock), 0, s, a, prologue);
-        break;
-    case 7:
-        hipLaunchKernelGGL((k_spmv<kRpt, 7, true>), dim3(a.grid), dim3(kBlock), 0, s, a, prologue);
-        break;
-    case 1:  // one row per thread, runtime width
-        hipLaunchKernelGGL((k_spmv<1, 0, true>), dim3(a.grid), dim3(kSliceRows), 0, s, a, prologue);
-        break;
-    default:
-        hipLaunchKernelGGL((k_spmv<kRpt, 0, true>), dim3(a.grid), dim3(kBlock), 0, s, a, prologue);
-        break;
+    case 1: HPCCG_SPMV(1, 0, 1, false); break;
+    case 2: HPCCG_SPMV(4, 0, 1, false); break;
+    case 27: HPCCG_SPMV(2, 27, 1, false); break;
+    case 127: HPCCG_SPMV(2, 27, 1, false); break;
+    case 227: HPCCG_SPMV(2, 27, 2, false); break;
+    case 327: HPCCG_SPMV(2, 27, 3, false); break;
+    case 427: HPCCG_SPMV(2, 27, 4, false); break;
+    case 527: HPCCG_SPMV(2, 27, 5, false); break;
+    case 627: HPCCG_SPMV(2, 27, 6, false); break;
+    case 7: HPCCG_SPMV(2, 7, 1, false); break;
+    case 1000: HPCCG_SPMV(2, 0, 1, true); break;
+    case 1027: HPCCG_SPMV(2, 27, 1, true); break;
+    case 1127: HPCCG_SPMV(2, 27, 1, true); break;
+    case 1227: HPCCG_SPMV(2, 27, 2, true); break;
+    case 1327: HPCCG_SPMV(2, 27, 3, true); break;
+    case 1427: HPCCG_SPMV(2, 27, 4, true); break;
+    case 1527: HPCCG_SPMV(2, 27, 5, true); break;
+    case 1627: HPCCG_SPMV(2, 27, 6, true); break;
+    case 1007: HPCCG_SPMV(2, 7, 1, true); break;
+    case 9999: hipLaunchKernelGGL(k_stream_diag<27>, dim3(a.grid), dim3(256), 0, s, a); break;
+    default: HPCCG_SPMV(2, 0, 1, false); break;
     }
 }
+#undef HPCCG_SPMV
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
 {

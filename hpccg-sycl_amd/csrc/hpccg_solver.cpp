@@ -878,17 +878,13 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "event_timing")) {
         M->event_timing = (int)value;
     } else if (!std::strcmp(key, "spmv_variant")) {
-        if (value == 27 || value == 7) {
-            if (!(M->uniform && M->width == value))
-                return set_err(HPCCG_HIP_EINVAL, "variant %lld needs a uniform width-%lld image", value, value);
-        } else if (value != 0 && value != 1) {
+        const int v = (int)value;
+        const int w = v % 100;  // 27 / 7 for the fixed-width variants
+        if (!spmv_variant_ok(v) || v == 9999)
             return set_err(HPCCG_HIP_EINVAL, "unknown spmv variant %lld", value);
-        }
-        M->spmv_variant = (int)value;
-        if (M->graph_exec) {
-            (void)hipGraphExecDestroy(M->graph_exec);
-            M->graph_exec = nullptr;
-        }
+        if ((w == 27 || w == 7) && !(M->uniform && M->width == w))
+            return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform width-%d SELL image", v, w);
+        M->spmv_variant = v;
     } else {
         return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
     }
@@ -929,6 +925,33 @@ int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_ite
     TRY(solve_impl(M, M->d_b, M->d_x, max_iter, tolerance, niters, normr, times, print));
     HIP_TRY(hipMemcpy(x, M->d_x, sizeof(double) * M->nrow, hipMemcpyDeviceToHost));
     if (times) times[6] = setup;
+    return 0;
+}
+
+int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_us)
+{
+    if (!M || !avg_us || reps < 1) return set_err(HPCCG_HIP_EINVAL, "bad argument");
+    const int w = variant % 100;
+    if (!spmv_variant_ok(variant)) return set_err(HPCCG_HIP_EINVAL, "unknown variant %d", variant);
+    if ((w == 27 || w == 7 || variant == 9999) && !(M->uniform && M->width == (variant == 9999 ? 27 : w)))
+        return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform SELL image of that width", variant);
+    HIP_TRY(hipSetDevice(M->device));
+    TRY(ensure_hist(M, 2));
+    CgArgs a = make_args(M, M->d_b, M->d_x, 2, 0.0);
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    launch_cg_spmv(a, variant, true, M->stream);  // warm
+    HIP_TRY(hipEventRecord(e0, M->stream));
+    for (int i = 0; i < reps; i++) launch_cg_spmv(a, variant, true, M->stream);
+    HIP_TRY(hipEventRecord(e1, M->stream));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *avg_us = 1e3 * ms / reps;
     return 0;
 }
 

@@ -111,6 +111,9 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value);
  * out[0] SpMV total ms, out[1] SpMV launches, out[2] fused-update total ms,
  * out[3] update launches (launches that did work, i.e. <= niters + 1). */
 int hpccg_hip_kernel_times(const hpccg_hip_matrix* M, double out[4]);
+/* Diagnostic: average duration (hipEvents, solver stream) of `reps`
+ * back-to-back launches of SpMV variant `variant` on the resident p. */
+int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_us);
 
 /* ---- kernel level, device pointers, synchronous ----------------------------
  * hpccg_hip_sparsemv: HPC_sparsemv.cpp:68-89. x_dev has the local rows (the

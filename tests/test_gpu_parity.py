@@ -52,9 +52,11 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
     assert np.array_equal(host(y), prob.b)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 27])
+@pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 527, 627, 1000, 1027, 1327, 1427])
 def test_sparsemv_variants_agree(hp, gpu, variant):
-    """Every SpMV kernel variant gives the identical CG trace (same sums)."""
+    """Every SpMV variant computes every row bitwise identically; variants with
+    the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
+    tree, so their CG traces are bitwise equal; 1 and 2 stay in tolerance."""
     prob = hp.generate_matrix(24, 20, 18)
     M = hp.Matrix.from_hpc(prob)
     M.set_option("spmv_variant", variant)
@@ -64,9 +66,13 @@ def test_sparsemv_variants_agree(hp, gpu, variant):
     M.set_option("spmv_variant", 0)
     x0 = prob.x
     _, it0, nr0, _ = hp.HPCCG(M, prob.b, x0, max_iter=60)
-    assert it == it0 and nr == nr0
-    assert np.array_equal(tr, M.last_trace())
-    assert np.array_equal(x, x0)
+    assert it == it0
+    if variant in (1, 2):
+        assert check_trace(tr, M.last_trace(), RTRANS_RTOL_1GPU) > 10
+    else:
+        assert nr == nr0
+        assert np.array_equal(tr, M.last_trace())
+        assert np.array_equal(x, x0)
 
 
 def test_waxpby_bitwise_vs_reference(hp, gpu, golden):

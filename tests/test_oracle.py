@@ -153,3 +153,18 @@ def test_oracle_vs_live_reference_extra_sizes():
         assert np.array_equal(rp, A.row_ptr) and np.array_equal(cols, A.cols)
         assert np.array_equal(vals, A.vals) and np.array_equal(b, A.b)
         M.close()
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="reference build only in the dev container")
+def test_reference_build_not_interposed_by_our_library(hp, golden):
+    """Our libhpccg_hip.so exports the drop-in HPCCG() symbol; the reference
+    build (linked -Bsymbolic, ours loaded RTLD_LOCAL) must still run its own
+    CPU HPCCG -- with no GPU here, an interposed call would fail."""
+    hp.lib()
+    c = solve_case(golden, "27pt_10x10x10")
+    M, x0, b, xe = oracle.ref_generate(10, 10, 10)
+    import subprocess, sys
+    res = oracle.ref_hpccg(M, b, max_iter=150)
+    M.close()
+    assert res["niters"] == c["runs"]["150"]["niters"]
+    assert res["normr"] == unhex(c["runs"]["150"]["normr"])
