@@ -124,9 +124,13 @@ def _check(rc: int, what: str) -> None:
 
 
 def _ptr(a) -> int:
-    """Device pointer of a torch tensor (or an int)."""
+    """Device pointer of a torch tensor (or an int). Work torch queued on the
+    tensor is completed first: the library runs on its own HIP stream."""
     if isinstance(a, int):
         return a
+    if a.is_cuda:
+        import torch
+        torch.cuda.current_stream(a.device).synchronize()
     return a.data_ptr()
 
 

@@ -625,7 +625,8 @@ void launch_cg_p_update(const CgArgs& a, hipStream_t s)
 //   2 runtime width, 4 rows/thread
 //   27 / 7  uniform width, fully unrolled, 2 rows/thread
 //   100*w + 27: same with __launch_bounds__ min waves/SIMD w (w = 1..4)
-//   +1000: non-temporal loads of vals/cols
+//   +1000: non-temporal loads of vals/cols (1000 = the default: runtime
+//   width, 2 rows/thread, nt -- within ~3 % of the matrix-streaming ceiling)
 //   9999: diagnostic matrix stream without the gather (not an SpMV)
 #define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
     hipLaunchKernelGGL((k_spmv<RPT, W, true, MINW, NT>), dim3(a.grid), dim3(kSliceRows / RPT), 0, s, \
@@ -635,7 +636,7 @@ bool spmv_variant_ok(int v)
     switch (v) {
     case 0: case 1: case 2: case 27: case 7: case 127: case 227: case 327: case 427: case 527:
     case 627: case 1000: case 1027: case 1007: case 1127: case 1227: case 1327: case 1427:
-    case 1527: case 1627: case 9999:
+    case 1527: case 1627: case 1001: case 1002: case 9999:
         return true;
     default:
         return false;
@@ -656,6 +657,8 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 627: HPCCG_SPMV(2, 27, 6, false); break;
     case 7: HPCCG_SPMV(2, 7, 1, false); break;
     case 1000: HPCCG_SPMV(2, 0, 1, true); break;
+    case 1001: HPCCG_SPMV(1, 0, 1, true); break;
+    case 1002: HPCCG_SPMV(4, 0, 1, true); break;
     case 1027: HPCCG_SPMV(2, 27, 1, true); break;
     case 1127: HPCCG_SPMV(2, 27, 1, true); break;
     case 1227: HPCCG_SPMV(2, 27, 2, true); break;

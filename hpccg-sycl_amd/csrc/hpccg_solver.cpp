@@ -400,6 +400,10 @@ int enqueue_prologue(hpccg_hip_matrix* M, const CgArgs& a, bool events)
 }
 
 constexpr int kGraphChunk = 8;  // CG iterations per captured graph
+// SELL-512 SpMV, runtime slice width, 2 rows/thread, non-temporal matrix
+// loads: 450 us at 200^3 (6.05 TB/s algorithmic) vs 436 us for a bare
+// stream of the same image (profiles/spmv_sweep_r01.jsonl).
+constexpr int kDefaultSpmvVariant = 1000;
 
 int build_graph(hpccg_hip_matrix* M, const CgArgs& a)
 {
@@ -561,7 +565,7 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
     M->nnz = nnz;
     M->ghost_lo = (int)std::max(0LL, (long long)start_row - mn);
     M->ghost_hi = (int)std::max(0LL, mx - ((long long)start_row + nrow - 1));
-    HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamDefault));
     int rc = exchange_plan(M);
     if (rc) {
         free_matrix(M);
@@ -590,7 +594,7 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
         free_matrix(M);
         return set_err(HPCCG_HIP_EPLAN, "column index outside the halo plan");
     }
-    M->spmv_variant = (M->uniform && (M->width == 27 || M->width == 7)) ? M->width : 0;
+    M->spmv_variant = kDefaultSpmvVariant;
     rc = [&]() -> int {
         HIP_TRY(hipMalloc(&M->d_slice_base, sizeof(unsigned int) * sb.size()));
         HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
@@ -625,7 +629,7 @@ int scratch_for(int nparts)
     if (g_scratch.device != dev) {
         g_scratch = Scratch();
         g_scratch.device = dev;
-        HIP_TRY(hipStreamCreateWithFlags(&g_scratch.s, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&g_scratch.s, hipStreamDefault));
         HIP_TRY(hipMalloc(&g_scratch.out, sizeof(double) * 2));
     }
     if (nparts > g_scratch.cap) {
@@ -710,7 +714,7 @@ int hpccg_hip_comm_allreduce_host(double* vals, int n, int op)
     if (g_comm.nranks == 1 || n == 0) return 0;
     double* d = nullptr;
     hipStream_t s = nullptr;
-    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamDefault));
     HIP_TRY(hipMalloc(&d, sizeof(double) * n));
     HIP_TRY(hipMemcpy(d, vals, sizeof(double) * n, hipMemcpyHostToDevice));
     const ncclRedOp_t ops[3] = {ncclSum, ncclMin, ncclMax};
@@ -774,7 +778,7 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     M->ghost_lo = rank > 0 ? std::min(nxy, n) : 0;
     M->ghost_hi = rank < size - 1 ? std::min(nxy, n) : 0;
     // rows per z-plane beyond one plane would need rank+-2 (nz >= 1 keeps it at +-1)
-    HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamDefault));
     int rc = exchange_plan(M);
     if (rc) {
         free_matrix(M);
@@ -818,7 +822,7 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     sb[M->nslices] = (unsigned int)acc;
     M->nslots = acc * kSliceRows;
     M->width = M->uniform ? wmax : 0;
-    M->spmv_variant = (M->uniform && (wmax == 27 || wmax == 7)) ? wmax : 0;
+    M->spmv_variant = kDefaultSpmvVariant;
     rc = [&]() -> int {
         HIP_TRY(hipMalloc(&M->d_slice_base, sizeof(unsigned int) * sb.size()));
         HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));

@@ -44,6 +44,50 @@ RTRANS_RTOL_MULTI = 1e-7
 RTRANS_CUTOFF = 1e-20
 
 
+CONVERGED_REL = 1e-15
+
+
+def first_converged(tr):
+    """First k with normr_k / normr_0 <= 1e-15 (the start of rounding noise)."""
+    tr = np.asarray(tr, np.float64)
+    hit = np.nonzero(tr <= CONVERGED_REL * tr[0])[0]
+    return int(hit[0]) if len(hit) else None
+
+
+def check_final(niters, normr, tr_test, ref_niters, ref_normr, ref_trace, max_iter):
+    """Termination parity (stated tolerance).
+
+    Before convergence the trajectory is checked by check_trace. After
+    normr/normr0 <= 1e-15 the recurrence is rounding noise, and the reference
+    itself is not reproducible there: its own OpenMP build (serial order vs
+    2..8 threads, 21 runs each, measured with oracle/ in this repo) exits on
+    rtrans underflow at niters 259..276 where serial gives 274 (10^3),
+    268..279 vs 272 (13x7x5), 491..499 vs 499 (20^3), 319..499 vs 325
+    (8x8x16), with final-residual ratios up to 10^1.14. So:
+      * equal niters when both runs go the full max_iter-1 iterations;
+      * otherwise (an underflow exit on either side) both runs must end in
+        the noise regime;
+      * both final residuals <= 1e-15 * normr0 (0 = underflow) whenever the
+        reference's is;
+      * the first converged iteration agrees within +-2.
+    """
+    full = max_iter - 1
+    r0 = tr_test[0]
+    if ref_niters == full and niters == full:
+        pass
+    else:
+        assert normr <= CONVERGED_REL * r0, (niters, normr)
+        assert ref_normr <= CONVERGED_REL * r0, (ref_niters, ref_normr)
+    if ref_normr <= CONVERGED_REL * r0:
+        assert normr <= CONVERGED_REL * r0, (normr, r0)
+    else:
+        assert niters == ref_niters
+        assert abs(normr - ref_normr) <= 1e-4 * ref_normr, (normr, ref_normr)
+    kt, kr = first_converged(tr_test), first_converged(ref_trace)
+    if kr is not None and kt is not None:
+        assert abs(kt - kr) <= 2, (kt, kr)
+
+
 def check_trace(tr_test, tr_ref, rtol):
     """Phase-aware trace comparison on rtrans = normr^2. Returns #points checked."""
     tr_test = np.asarray(tr_test, np.float64)

@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--n", type=int, nargs="+", default=[200, 100])
     ap.add_argument("--stencil", type=int, default=27)
     ap.add_argument("--variants", type=int, nargs="+",
-                    default=[0, 1, 2, 27, 327, 427, 527, 627, 1000, 1027, 1327, 1427, 1527, 9999])
+                    default=[0, 1, 2, 27, 1000, 1001, 1002, 1027, 9999])
     ap.add_argument("--reps", type=int, default=20)
     args = ap.parse_args()
     import torch  # noqa: F401
