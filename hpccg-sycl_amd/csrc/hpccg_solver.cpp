@@ -733,7 +733,7 @@ int hpccg_hip_device_name(char* buf, int cap, int* cus)
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, dev));
     if (buf && cap > 0) {
-        std::snprintf(buf, cap, "%s (%s)", prop.name, prop.gcnArchName);
+        std::snprintf(buf, cap, "%s (%s)", prop.name[0] ? prop.name : "AMD Instinct GPU", prop.gcnArchName);
     }
     if (cus) *cus = prop.multiProcessorCount;
     return 0;

@@ -1,0 +1,22 @@
+#!/bin/bash
+# rocprofv3 evidence for the round: kernel-trace stats of the bench command,
+# then FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md HBM
+# section) over the SpMV and the known-bytes streaming kernel used to
+# calibrate them. Stops at the first crash/timeout; no retries.
+set -u
+export TMPDIR=/tmp
+OUT=gpurun_out/prof
+mkdir -p $OUT
+step() {
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2> "$OUT/$name.err"
+    local rc=$?
+    echo "$name rc=$rc"
+    case $rc in 124|134|137|139) echo "fatal in $name, stopping"; exit $rc;; esac
+    return 0
+}
+N=${N:-200}
+step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --steps 2 --warmup 1 --no-cpu-baseline
+step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python tools/spmv_sweep.py --n $N --variants 1000 9999 --reps 3
+step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python tools/spmv_sweep.py --n $N --variants 1000 9999 --reps 3
+find $OUT -name "*.csv" | head -20
