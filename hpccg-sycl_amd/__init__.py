@@ -100,6 +100,7 @@ def lib() -> C.CDLL:
         "hpccg_hip_HPCCG": (ip, [C.POINTER(_HPCMatrix), vp, vp, ip, dp, PI, PD, PD]),
         "hpccg_sell_build": (lp, [ip, lp, lp, vp, vp, vp, vp, vp, vp]),
         "hpccg_halo_plan": (ip, [ip, ip, ip, vp, vp, PI]),
+        "hpccg_slab_plan": (ip, [ip, ip, PI, PI]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -375,6 +376,14 @@ def halo_plan(row_ptr, cols, start_row, total_nrow):
     _check(lib().hpccg_halo_plan(len(row_ptr) - 1, start_row, total_nrow, row_ptr.ctypes.data,
                                  cols.ctypes.data, out), "halo_plan")
     return {"ghost_lo": out[0], "ghost_hi": out[1], "min_col": out[2], "max_col": out[3]}
+
+
+def slab_plan(nranks: int, rank: int, info) -> tuple[int, int]:
+    """(rows sent to rank-1, rows sent to rank+1) from all ranks' 4-int info."""
+    arr = (C.c_int * (4 * nranks))(*[int(v) for v in np.asarray(info).ravel()])
+    out = (C.c_int * 2)()
+    _check(lib().hpccg_slab_plan(nranks, rank, arr, out), "slab_plan")
+    return out[0], out[1]
 
 
 def load():

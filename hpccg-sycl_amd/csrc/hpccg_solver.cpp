@@ -226,18 +226,10 @@ int exchange_plan(hpccg_hip_matrix* M)
                            M->stream));
     HIP_TRY(hipStreamSynchronize(M->stream));
     (void)hipFree(d);
-    const int r = g_comm.rank, P = g_comm.nranks;
-    // ghosts must come from the adjacent ranks only, contiguously
-    if (M->ghost_lo > 0 && (r == 0 || M->ghost_lo > all[4 * (r - 1)]))
-        return set_err(HPCCG_HIP_EPLAN, "rank %d: ghost_lo %d not owned by rank %d", r, M->ghost_lo, r - 1);
-    if (M->ghost_hi > 0 && (r == P - 1 || M->ghost_hi > all[4 * (r + 1)]))
-        return set_err(HPCCG_HIP_EPLAN, "rank %d: ghost_hi %d not owned by rank %d", r, M->ghost_hi, r + 1);
-    if (r > 0 && all[4 * (r - 1) + 3] + all[4 * (r - 1)] != M->start_row)
-        return set_err(HPCCG_HIP_EPLAN, "rank %d: row ranges are not contiguous", r);
-    M->send_lo = (r > 0) ? all[4 * (r - 1) + 2] : 0;      // rank-1's ghost_hi
-    M->send_hi = (r < P - 1) ? all[4 * (r + 1) + 1] : 0;  // rank+1's ghost_lo
-    if (M->send_lo > M->nrow || M->send_hi > M->nrow)
-        return set_err(HPCCG_HIP_EPLAN, "rank %d: neighbour needs more rows than owned", r);
+    int sends[2];
+    TRY(hpccg_slab_plan(g_comm.nranks, g_comm.rank, all.data(), sends));
+    M->send_lo = sends[0];
+    M->send_hi = sends[1];
     return 0;
 }
 
@@ -1060,6 +1052,27 @@ long long hpccg_sell_build(int nrow, long long col_base, long long ncol_ext, con
     const long long r = sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, slice_base, sell_cols,
                                         sell_vals, uniform, &bad);
     return bad ? HPCCG_HIP_EPLAN : r;
+}
+
+int hpccg_slab_plan(int nranks, int rank, const int* info, int sends[2])
+{
+    if (nranks < 1 || rank < 0 || rank >= nranks || !info || !sends)
+        return set_err(HPCCG_HIP_EINVAL, "bad argument");
+    const int r = rank, P = nranks;
+    const int* me = info + 4 * r;
+    const int nrow = me[0], ghost_lo = me[1], ghost_hi = me[2], start_row = me[3];
+    // ghosts must come from the adjacent ranks only, contiguously
+    if (ghost_lo > 0 && (r == 0 || ghost_lo > info[4 * (r - 1)]))
+        return set_err(HPCCG_HIP_EPLAN, "rank %d: ghost_lo %d not owned by rank %d", r, ghost_lo, r - 1);
+    if (ghost_hi > 0 && (r == P - 1 || ghost_hi > info[4 * (r + 1)]))
+        return set_err(HPCCG_HIP_EPLAN, "rank %d: ghost_hi %d not owned by rank %d", r, ghost_hi, r + 1);
+    if (r > 0 && info[4 * (r - 1) + 3] + info[4 * (r - 1)] != start_row)
+        return set_err(HPCCG_HIP_EPLAN, "rank %d: row ranges are not contiguous", r);
+    sends[0] = (r > 0) ? info[4 * (r - 1) + 2] : 0;      // rank-1's ghost_hi: our first rows
+    sends[1] = (r < P - 1) ? info[4 * (r + 1) + 1] : 0;  // rank+1's ghost_lo: our last rows
+    if (sends[0] > nrow || sends[1] > nrow)
+        return set_err(HPCCG_HIP_EPLAN, "rank %d: neighbour needs more rows than owned", r);
+    return 0;
 }
 
 int hpccg_halo_plan(int nrow, int start_row, int total_nrow, const long long* row_ptr, const int* cols,

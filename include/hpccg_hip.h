@@ -142,6 +142,11 @@ long long hpccg_sell_build(int nrow, long long col_base, long long ncol_ext, con
  * (see hpccg_hip_matrix_create). Returns 0 or HPCCG_HIP_EPLAN. */
 int hpccg_halo_plan(int nrow, int start_row, int total_nrow, const long long* row_ptr,
                     const int* cols, int plan_out[4]);
+/* What rank `rank` sends (make_local_matrix.cpp:286-587 handshake, z-slabs):
+ * info has 4 ints per rank {nrow, ghost_lo, ghost_hi, start_row} (the
+ * all-gather the library does at matrix creation); sends[0] = rows to
+ * rank-1 (its first rows), sends[1] = rows to rank+1 (its last rows). */
+int hpccg_slab_plan(int nranks, int rank, const int* info, int sends[2]);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Turn a tools/gpu_profile.sh run into committed evidence under profiles/.
+
+* kernel stats of the bench command (rocprofv3 --kernel-trace --stats)
+* HBM traffic per SpMV launch from two separate --pmc passes (FETCH_SIZE,
+  WRITE_SIZE; KiB units). gfx950 correction (MI355X_MICROARCH.md, HBM):
+  FETCH_SIZE reports 1/2 of a wide coalesced stream; the factor is
+  calibrated here on k_stream_diag, which reads exactly
+  12 * sell_slots bytes (vals fp64 + cols int32, 16 B / 8 B per lane, the
+  SpMV's own matrix access pattern) and writes 8 * nrow.
+
+usage: tools/pmc_summary.py <prof_dir> <tag> <nx> [<bench_json_log>]
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path):
+    agg = defaultdict(list)
+    for row in csv.DictReader(open(path)):
+        agg[(row["Kernel_Name"], row["Counter_Name"])].append(float(row["Counter_Value"]))
+    return agg
+
+
+def pick(agg, needle, counter):
+    for (k, c), v in agg.items():
+        if needle in k and c == counter:
+            return sum(v) / len(v), k
+    raise KeyError(needle)
+
+
+def main():
+    prof, tag, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    bench_log = sys.argv[4] if len(sys.argv) > 4 else None
+    outdir = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(outdir, exist_ok=True)
+    stats = glob.glob(os.path.join(prof, "stats", "*", "*_kernel_stats.csv"))[0]
+    shutil.copy(stats, os.path.join(outdir, "kernel_stats.csv"))
+    dom = glob.glob(os.path.join(prof, "stats", "*", "*_domain_stats.csv"))
+    if dom:
+        shutil.copy(dom[0], os.path.join(outdir, "domain_stats.csv"))
+    fetch = counters(glob.glob(os.path.join(prof, "fetch", "*", "*_counter_collection.csv"))[0])
+    write = counters(glob.glob(os.path.join(prof, "write", "*", "*_counter_collection.csv"))[0])
+    for src, name in [("fetch", "pmc_fetch_size.csv"), ("write", "pmc_write_size.csv")]:
+        shutil.copy(glob.glob(os.path.join(prof, src, "*", "*_counter_collection.csv"))[0],
+                    os.path.join(outdir, name))
+
+    nrow = n ** 3
+    # SELL-512 uniform width 27 image of the 27-pt problem
+    slots = ((nrow + 511) // 512) * 512 * 27
+    nnz = (3 * n - 2) ** 3
+    stream_read = 12.0 * slots
+    f_stream, _ = pick(fetch, "k_stream_diag", "FETCH_SIZE")
+    w_stream, _ = pick(write, "k_stream_diag", "WRITE_SIZE")
+    fetch_factor = stream_read / (f_stream * 1024.0)
+    f_spmv, kname = pick(fetch, "k_spmv<", "FETCH_SIZE")
+    w_spmv, _ = pick(write, "k_spmv<", "WRITE_SIZE")
+    spmv_read = f_spmv * 1024.0 * fetch_factor
+    spmv_write = w_spmv * 1024.0
+    algo = 12.0 * nnz + 20.0 * nrow
+
+    avg_ns = None
+    for row in csv.DictReader(open(stats)):
+        if "k_spmv<" in row["Name"]:
+            avg_ns = float(row["AverageNs"])
+    out = {
+        "tag": tag,
+        "problem": f"27-pt {n}^3, SELL-512 width 27 ({slots} slots, nnz {nnz})",
+        "kernel": kname,
+        "fetch_size_kib_raw": f_spmv,
+        "write_size_kib_raw": w_spmv,
+        "fetch_calibration": {"kernel": "k_stream_diag<27>", "known_read_bytes": stream_read,
+                              "fetch_size_kib": f_stream, "factor": round(fetch_factor, 4),
+                              "write_size_kib": w_stream, "known_write_bytes": 8.0 * nrow},
+        "spmv_hbm_read_bytes_per_launch": spmv_read,
+        "spmv_hbm_write_bytes_per_launch": spmv_write,
+        "spmv_hbm_bytes_per_launch": spmv_read + spmv_write,
+        "spmv_algorithmic_bytes_per_launch": algo,
+        "traffic_over_algorithmic": (spmv_read + spmv_write) / algo,
+        "rocprof_avg_spmv_ns": avg_ns,
+        "rocprof_spmv_GBs": algo / avg_ns if avg_ns else None,
+    }
+    if bench_log and os.path.exists(bench_log):
+        lines = [l for l in open(bench_log) if l.startswith("{")]
+        if lines:
+            b = json.loads(lines[-1])
+            out["bench_avg_launch_us"] = b["roofline"]["avg_launch_us"]
+            out["bench_value"] = b["value"]
+            shutil.copy(bench_log, os.path.join(outdir, "bench_under_rocprof.json"))
+    with open(os.path.join(ROOT, "profiles", f"pmc_spmv_27pt_{n}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    with open(os.path.join(outdir, "summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
