@@ -1,0 +1,106 @@
+"""The CLI seam on the GPU: our test_HPCCG and the reference's own main.cpp
+linked against libhpccg_hip.so (oracle/_ref/test_HPCCG_dropin) must print what
+the reference CLI prints (tests/golden/ref_cli_*.txt): same lines, same YAML
+keys, identical deterministic values (dimensions, iterations, FLOPS), the
+initial residual bit-identical at %g, residual lines at the same iterations."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+DROPIN = os.path.join(ROOT, "oracle", "_ref", "test_HPCCG_dropin")
+
+
+def keys(text):
+    """YAML key paths (indent-aware), timing values dropped."""
+    out = []
+    for line in text.splitlines():
+        m = re.match(r"^( *)([^:]+): ?(.*)$", line)
+        if m and not line.startswith(("Initial Residual", "Iteration", "Elapsed")):
+            out.append((len(m.group(1)), m.group(2)))
+    return out
+
+
+def values(text):
+    d = {}
+    path = []
+    for line in text.splitlines():
+        m = re.match(r"^( *)([^:]+): ?(.*)$", line)
+        if not m or line.startswith(("Initial Residual", "Iteration", "Elapsed")):
+            continue
+        lvl = len(m.group(1)) // 2
+        path = path[:lvl] + [m.group(2)]
+        d["/".join(path)] = m.group(3)
+    return d
+
+
+def run_cli(exe, dims, tmp_path, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run([exe, *map(str, dims)], cwd=tmp_path, capture_output=True, text=True,
+                       env=e, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stdout
+
+
+def residual_lines(text):
+    return [l for l in text.splitlines() if l.startswith(("Initial Residual", "Iteration ="))]
+
+
+def compare_to_reference(out, ref, extra_ok=("GPU Summary",)):
+    # residual lines: same iterations printed, initial residual identical
+    lo, lr = residual_lines(out), residual_lines(ref)
+    assert [l.split("Residual")[0] for l in lo] == [l.split("Residual")[0] for l in lr]
+    assert lo[0] == lr[0]
+    assert any(l.startswith("Elapsed time: ") and l.endswith(" s") for l in out.splitlines())
+    ko = [k for k in keys(out)]
+    kr = keys(ref)
+    # our extra block is appended at the end
+    if ko != kr:
+        cut = next(i for i, k in enumerate(ko) if k[1] in extra_ok)
+        assert ko[:cut] == kr
+    vo, vr = values(out), values(ref)
+    for k in ["Dimensions/nx", "Dimensions/ny", "Dimensions/nz", "Number of iterations",
+              "FLOPS Summary/Total   ", "FLOPS Summary/DDOT    ", "FLOPS Summary/WAXPBY  ",
+              "FLOPS Summary/SPARSEMV", "Mini-Application Name", "Mini-Application Version"]:
+        assert vo[k] == vr[k], k
+    fo, fr = float(vo["Final residual"]), float(vr["Final residual"])
+    r0 = float(lo[0].split("=")[1])
+    assert fo <= 1e-15 * r0 and fr <= 1e-15 * r0
+
+
+@pytest.mark.parametrize("dims", [(20, 20, 20), (10, 10, 10)])
+def test_our_cli_matches_reference_output(gpu, tmp_path, dims):
+    out = run_cli(os.path.join(ROOT, "hpccg-sycl_amd", "bin", "test_HPCCG"), dims, tmp_path)
+    ref = open(os.path.join(ROOT, "tests", "golden", "ref_cli_%dx%dx%d.txt" % dims)).read()
+    compare_to_reference(out, ref)
+    assert any(f.startswith("hpccg-1.0_") and f.endswith(".yaml") for f in os.listdir(tmp_path))
+    v = values(out)
+    assert float(v["GPU Summary/Difference between computed and exact"]) <= 1e-12
+
+
+def test_our_cli_device_generator_and_max_iter_env(gpu, tmp_path):
+    out = run_cli(os.path.join(ROOT, "hpccg-sycl_amd", "bin", "test_HPCCG"), (10, 10, 10), tmp_path,
+                  env={"HPCCG_DEVICE_GENERATE": "1", "HPCCG_MAX_ITER": "150"})
+    ref = open(os.path.join(ROOT, "tests", "golden", "out_10x10x10_150.txt")).read()
+    lo = residual_lines(out)
+    assert lo[0] == "Initial Residual = 258.24"
+    assert lo[1] == "Iteration = 15   Residual = 2.15402e-06"  # out.txt:2, pre-convergence
+    assert [l.split("Residual")[0] for l in lo] == [l.split("Residual")[0]
+                                                      for l in residual_lines(ref)]
+    assert values(out)["Number of iterations"] == "149"
+
+
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="oracle/_ref/test_HPCCG_dropin not built")
+def test_reference_main_linked_to_our_library(gpu, tmp_path):
+    """the reference's own main.cpp, generate_matrix.cpp and
+    YAML code, with HPCCG() resolved from libhpccg_hip.so, on the GPU."""
+    out = run_cli(DROPIN, (20, 20, 20), tmp_path)
+    ref = open(os.path.join(ROOT, "tests", "golden", "ref_cli_20x20x20.txt")).read()
+    compare_to_reference(out, ref)
+    assert keys(out) == keys(ref)  # the reference's own report code: exact key set
