@@ -94,13 +94,16 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=15.0):
                       f"OpenMP {threads} threads on the GPU box host"}
 
 
-def pmc_traffic(tag):
-    """HBM bytes per SpMV launch from a committed rocprofv3 PMC summary."""
+def pmc_traffic(tag, fused_p):
+    """HBM bytes per SpMV launch from the committed rocprofv3 PMC summary of
+    the same kernel configuration (profiles/pmc_<tag>.json), else None."""
     path = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
+    if bool(d.get("fuse_p", False)) != bool(fused_p):
+        return None
     return d.get("spmv_hbm_bytes_per_launch")
 
 
@@ -185,7 +188,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    spmv_bytes = 12.0 * info["nnz"] + 20.0 * nrow
+    # Algorithmic bytes of the reference operations the SpMV kernel performs
+    # (fused kernels are credited with the unfused bytes):
+    # HPC_sparsemv 12 nnz + 20 n, ddot(p, Ap) 16 n, and with fuse_p the
+    # waxpby p = r + beta p, 24 n.
+    fused_p = M.get_option("fuse_p")
+    spmv_bytes = 12.0 * info["nnz"] + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fused_p else 0.0)
     if spmv_n > 0:
         spmv_avg_s = spmv_ms / spmv_n * 1e-3
         timing_src = "hipEvent pairs around every SpMV launch on the solver stream"
@@ -230,8 +238,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(f"spmv_{args.stencil}pt_{n}"),
-                "kernel": "k_spmv (SELL-512 SpMV + fused p.Ap partials)",
+                "traffic": pmc_traffic(f"spmv_{args.stencil}pt_{n}", fused_p),
+                "kernel": "k_spmv (SELL-512 SpMV + p.Ap%s)" % (" + p = r + beta p" if fused_p else ""),
+                "bytes_formula": "12 nnz + 20 n (SpMV) + 16 n (ddot p.Ap)" + (" + 24 n (waxpby p)" if fused_p else ""),
                 "bytes_per_launch": spmv_bytes,
                 "avg_launch_us": round(spmv_avg_s * 1e6, 2),
                 "timing": timing_src,

@@ -92,6 +92,7 @@ def lib() -> C.CDLL:
         "hpccg_hip_solve_device": (ip, [vp, vp, vp, ip, dp, PI, PD, PD, ip]),
         "hpccg_hip_last_trace": (ip, [vp, PD, ip]),
         "hpccg_hip_set_option": (ip, [vp, C.c_char_p, lp]),
+        "hpccg_hip_get_option": (ip, [vp, C.c_char_p, C.POINTER(lp)]),
         "hpccg_hip_kernel_times": (ip, [vp, PD]),
         "hpccg_hip_diag_spmv": (ip, [vp, ip, ip, PD]),
         "hpccg_hip_sparsemv": (ip, [vp, vp, vp]),
@@ -243,6 +244,11 @@ class Matrix:
 
     def set_option(self, key: str, value: int) -> None:
         _check(lib().hpccg_hip_set_option(self.h, key.encode(), int(value)), "set_option")
+
+    def get_option(self, key: str) -> int:
+        v = C.c_longlong(0)
+        _check(lib().hpccg_hip_get_option(self.h, key.encode(), C.byref(v)), "get_option")
+        return v.value
 
     def kernel_times(self) -> dict:
         """hipEvent timings of the last solve (needs set_option('event_timing', 1))."""

@@ -11,7 +11,7 @@ namespace hpccg {
 // the per-slice dot partials of every kernel aligned (deterministic sums).
 constexpr int kSliceRows = 512;
 constexpr int kNumXcd = 8;        // MI355X: 8 XCDs, blocks dealt round-robin
-constexpr int kFinalizeThreads = 1024;
+constexpr int kReduceThreads = 256;  // shape of every final dot reduction
 
 // Indices into the device scalar block.
 enum Scalar : int { kRR = 0, kPAP = 1 };
@@ -45,6 +45,10 @@ struct CgArgs {
     double* x;
     double* r;
     double* p;             // local rows of p; p - ghost_lo .. p + n + ghost_hi valid
+    double* p1;            // second p buffer (fuse_p: p_k lives in buffer k & 1)
+    int fuse_p;            // 1: p = r + beta p computed inside the SpMV (single rank)
+    int fold;              // 1: the last block of each producer reduces the partials
+    unsigned int* tickets; // [2] arrival counters for the folded reductions
     double* Ap;
     double* partial;       // [nslices] per-slice partial dot products
     double* g;             // [2] dot results after the all-reduce

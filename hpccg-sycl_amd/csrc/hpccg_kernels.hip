@@ -204,6 +204,91 @@ __device__ __forceinline__ void ld_cols(const int* __restrict__ p, int (&c)[kRpt
 // Vectors are allocated padded to a multiple of 512 rows, so full-width loads
 // are always in bounds; rows >= n are masked on store and in the dots.
 
+// p of iteration k. With fuse_p, p_k is written by the SpMV of iteration k
+// into buffer k & 1 while the gathers read p_{k-1} from the other buffer.
+__device__ __forceinline__ double* cur_p(const CgArgs& a, int k)
+{
+    return (a.fuse_p && (k & 1)) ? a.p1 : a.p;
+}
+
+template <int kRpt>
+__device__ __forceinline__ void st_rows(double* __restrict__ base, int row, int n, const Rows<kRpt>& o)
+{
+    if (row + kRpt <= n) {
+        st<kRpt>(base + row, o);
+    } else {
+        for (int i = 0; i < kRpt; i++)
+            if (row + i < n) base[row + i] = o.v[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Dot-product completion. Every producing block reduces its slice to one
+// partial (fixed shape). The partials are then summed in slice order by
+// kReduceThreads threads -- either by a separate one-block kernel
+// (k_finalize) or, with a.fold, by the block that arrives last at a ticket
+// counter (Guideline 16 hand-off: plain partial store -> agent release ->
+// s_waitcnt -> relaxed ticket add; the last arriver: agent acquire ->
+// s_waitcnt -> barrier -> plain loads). Both give bitwise the same sum.
+// which = kPAP: p.Ap (HPCCG.cpp:381); kRR: r.r (HPCCG.cpp:353, 367), which
+// closes iteration k and advances kst[0].
+// ---------------------------------------------------------------------------
+template <int kThreads>
+__device__ __forceinline__ void reduce_partials(const CgArgs& a, int which, int kfinal)
+{
+    // The fixed shape is kReduceThreads "virtual" threads: virtual thread t sums
+    // partial[t], partial[t + 256], ... in order; virtual waves are reduced by
+    // the shfl_xor butterfly and then added in wave order. Blocks of any size
+    // emulate exactly that shape, so every kernel produces the same bits.
+    constexpr int kVWaves = kReduceThreads / kWave;
+    constexpr int kRealWaves = kThreads / kWave;
+    __shared__ double wsum[kVWaves];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+    for (int vw = w; vw < kVWaves; vw += kRealWaves) {
+        double v = 0.0;
+        for (int i = vw * kWave + lane; i < a.nslices; i += kReduceThreads) v += a.partial[i];
+        v = wave_sum(v);
+        if (lane == 0) wsum[vw] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < kVWaves; i++) s += wsum[i];
+        a.loc[which] = s;
+        if (a.nranks == 1) a.g[which] = s;
+        if (which == kRR) a.kst[0] = kfinal;
+    }
+}
+
+template <int kThreads>
+__device__ __forceinline__ void complete_dot(const CgArgs& a, int s, double bs, int which, int kfinal)
+{
+    if (!a.fold) {
+        if (threadIdx.x == 0) a.partial[s] = bs;
+        return;
+    }
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+        a.partial[s] = bs;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(&a.tickets[which], 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        last = (t == (unsigned)a.nslices - 1u);
+        if (last) {
+            stamp(a, which == kRR ? kStampFinRR : kStampFinPAP);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    reduce_partials<kThreads>(a, which, kfinal);
+    if (threadIdx.x == 0) a.tickets[which] = 0u;  // re-armed for the next launch
+}
+
 // ---------------------------------------------------------------------------
 // Prologue: p = x + 0.0*x   (HPCCG.cpp:347, waxpby(nrow, 1.0, x, 0.0, x, p))
 // ---------------------------------------------------------------------------
@@ -217,16 +302,13 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_prologue_copy(CgArgs a)
     Rows<kRpt> xv = ld<kRpt>(a.x + row), o;
 #pragma unroll
     for (int i = 0; i < kRpt; i++) o.v[i] = xv.v[i] + 0.0 * xv.v[i];
-    if (row + kRpt <= a.n) {
-        st<kRpt>(a.p + row, o);
-    } else {
-        for (int i = 0; i < kRpt; i++)
-            if (row + i < a.n) a.p[row + i] = o.v[i];
-    }
+    st_rows<kRpt>(a.p, row, a.n, o);
 }
 
 // ---------------------------------------------------------------------------
 // p = r + beta*p  (HPCCG.cpp:362 for k == 1: p = r + 0*r; :366-369 otherwise)
+// Separate kernel only when the update is not fused into the SpMV (multi-rank:
+// the halo of p must be exchanged between the two).
 // ---------------------------------------------------------------------------
 template <int kRpt>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_p_update(CgArgs a)
@@ -250,27 +332,34 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_p_update(CgArgs a)
     Rows<kRpt> o;
 #pragma unroll
     for (int i = 0; i < kRpt; i++) o.v[i] = rv.v[i] + beta * yv.v[i];
-    if (row + kRpt <= a.n) {
-        st<kRpt>(a.p + row, o);
-    } else {
-        for (int i = 0; i < kRpt; i++)
-            if (row + i < a.n) a.p[row + i] = o.v[i];
-    }
+    st_rows<kRpt>(a.p, row, a.n, o);
 }
 
 // ---------------------------------------------------------------------------
-// SpMV over SELL-512 + fused per-slice partial of p.Ap
-// (HPC_sparsemv.cpp:68-89 then ddot.cpp:60-73 on (p, Ap)).
+// SpMV over SELL-512 (HPC_sparsemv.cpp:68-89) + fused p.Ap slice partial
+// (ddot.cpp:60-73), optionally + the p update (waxpby, HPCCG.cpp:362/369).
 //
 // Thread t of slice s owns rows s*512 + t*kRpt + [0, kRpt). Slot j of the
 // slice is a contiguous 512-entry run: lane loads are 16 B (vals) / 8 B (cols)
 // and a wave reads 1 KiB + 512 B per slot. x is gathered through L1/L2/MALL;
 // for the stencil the 64 lanes of a wave hit consecutive x.
+// Gather source G(c): p[c] (plain), or r[c] + beta*p_old[c] (fused p update:
+// the exact expression k_p_update stores, so every row sum is unchanged).
 // kW > 0: slice width known at compile time (27 / 7), fully unrolled.
 // ---------------------------------------------------------------------------
-template <int kRpt, int kW, bool kNT = false>
-__device__ __forceinline__ void spmv_rows(const CgArgs& a, const double* __restrict__ xext, int s,
-                                          double (&sum)[kRpt])
+struct GatherP {
+    const double* __restrict__ x;
+    __device__ __forceinline__ double operator()(int c) const { return x[c]; }
+};
+struct GatherRP {
+    const double* __restrict__ r;
+    const double* __restrict__ pold;
+    double beta;
+    __device__ __forceinline__ double operator()(int c) const { return r[c] + beta * pold[c]; }
+};
+
+template <int kRpt, int kW, bool kNT, class G>
+__device__ __forceinline__ void spmv_rows(const CgArgs& a, const G& gat, int s, double (&sum)[kRpt])
 {
     // kW > 0: every slice has exactly kW slots (host padded the image to a
     // uniform width), so slice s starts at s*kW and the loop fully unrolls.
@@ -289,7 +378,7 @@ __device__ __forceinline__ void spmv_rows(const CgArgs& a, const double* __restr
             const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
 #pragma unroll
             for (int i = 0; i < kRpt; i++) {
-                const double xv = (c[i] >= 0) ? xext[c[i]] : 0.0;
+                const double xv = (c[i] >= 0) ? gat(c[i]) : 0.0;
                 sum[i] = sum[i] + v.v[i] * xv;
             }
         }
@@ -301,7 +390,7 @@ __device__ __forceinline__ void spmv_rows(const CgArgs& a, const double* __restr
             const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
 #pragma unroll
             for (int i = 0; i < kRpt; i++) {
-                const double xv = (c[i] >= 0) ? xext[c[i]] : 0.0;
+                const double xv = (c[i] >= 0) ? gat(c[i]) : 0.0;
                 sum[i] = sum[i] + v.v[i] * xv;
             }
         }
@@ -311,13 +400,15 @@ __device__ __forceinline__ void spmv_rows(const CgArgs& a, const double* __restr
 // Padding slots add v*x = 0*0 = +0: a sum that starts at +0.0 is never -0 under
 // round-to-nearest, so +0 leaves every row sum bit-identical to skipping it.
 
-template <int kRpt, int kW, bool kDot, int kMinW = 1, bool kNT = false>
+template <int kRpt, int kW, int kMinW, bool kNT, bool kFuse>
 __global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, bool prologue)
 {
+    int k = 0;
     if (!prologue) {
-        const int k = a.kst[0];
-        const bool run = cg_run(a, k, false);
+        k = a.kst[0];
+        const bool run = cg_run(a, k, kFuse);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = a.g[kRR];
             if (run)
                 stamp(a, kStampSpmv);
             else
@@ -327,32 +418,37 @@ __global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, boo
     }
     const int s = xcd_slice(a.grid);
     if (s >= a.nslices) return;
-    const double* __restrict__ xext = a.p - a.ghost_lo;
-    double sum[kRpt];
-    spmv_rows<kRpt, kW, kNT>(a, xext, s, sum);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
+    double* __restrict__ p = cur_p(a, k);
+    double sum[kRpt];
+    Rows<kRpt> pv;
+    if constexpr (kFuse) {
+        // beta and p_{k-1} exactly as k_p_update uses them
+        const double beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+        const double* pold = (k == 1) ? a.r : cur_p(a, k - 1);
+        const GatherRP gat{a.r, pold, beta};
+        spmv_rows<kRpt, kW, kNT>(a, gat, s, sum);
+        const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+        const Rows<kRpt> yv = ld<kRpt>(pold + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + beta * yv.v[i];
+        st_rows<kRpt>(p, row, a.n, pv);
+    } else {
+        const GatherP gat{p - a.ghost_lo};
+        spmv_rows<kRpt, kW, kNT>(a, gat, s, sum);
+        pv = ld<kRpt>(p + row);
+    }
     Rows<kRpt> o;
 #pragma unroll
     for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+    st_rows<kRpt>(a.Ap, row, a.n, o);
+    if (prologue) return;  // HPCCG.cpp:351: the prologue SpMV has no p.Ap
     double d = 0.0;
-    if (row + kRpt <= a.n) {
-        st<kRpt>(a.Ap + row, o);
-        if constexpr (kDot) {
-            const Rows<kRpt> pv = ld<kRpt>(a.p + row);
 #pragma unroll
-            for (int i = 0; i < kRpt; i++) d += pv.v[i] * o.v[i];
-        }
-    } else {
-        for (int i = 0; i < kRpt; i++)
-            if (row + i < a.n) {
-                a.Ap[row + i] = o.v[i];
-                if constexpr (kDot) d += a.p[row + i] * o.v[i];
-            }
-    }
-    if constexpr (kDot) {
-        const double bs = block_sum<kSliceRows / kRpt>(d);
-        if (threadIdx.x == 0) a.partial[s] = bs;
-    }
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += pv.v[i] * o.v[i];
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
 }
 
 // Plain SpMV on arbitrary x (kernel-level C ABI): same body, no dot.
@@ -363,7 +459,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_plain(CgArgs a, cons
     const int s = xcd_slice(a.grid);
     if (s >= a.nslices) return;
     double sum[kRpt];
-    spmv_rows<kRpt, 0>(a, xext, s, sum);
+    spmv_rows<kRpt, 0, true>(a, GatherP{xext}, s, sum);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     for (int i = 0; i < kRpt; i++)
         if (row + i < a.n) y[row + i] = sum[i];
@@ -395,12 +491,8 @@ __global__ __launch_bounds__(256) void k_stream_diag(CgArgs a)
     }
 }
 
-// ---------------------------------------------------------------------------
-// Final reduction of the per-slice partials, one block, fixed order.
-// which = kPAP: p.Ap (HPCCG.cpp:381); which = kRR: r.r (HPCCG.cpp:353, 367).
-// The r.r finalize closes iteration k: it advances kst[0] to k+1.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int which, bool prologue)
+// Separate final reduction (a.fold == 0): same shape and order as the folded one.
+__global__ __launch_bounds__(kReduceThreads) void k_finalize(CgArgs a, int which, bool prologue)
 {
     const int k = a.kst[0];
     const bool run = prologue || cg_run(a, k, false);
@@ -411,14 +503,7 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
             mark_end(a);
     }
     if (!run) return;
-    double v = 0.0;
-    for (int i = threadIdx.x; i < a.nslices; i += kFinalizeThreads) v += a.partial[i];
-    const double s = block_sum<kFinalizeThreads>(v);
-    if (threadIdx.x == 0) {
-        a.loc[which] = s;
-        if (a.nranks == 1) a.g[which] = s;
-        if (which == kRR) a.kst[0] = prologue ? 1 : k + 1;
-    }
+    reduce_partials<kReduceThreads>(a, which, prologue ? 1 : k + 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -431,8 +516,9 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
 template <int kRpt, bool kPrologue>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
 {
+    int k = 0;
     if constexpr (!kPrologue) {
-        const int k = a.kst[0];
+        k = a.kst[0];
         const bool run = cg_run(a, k, false);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             if (run)
@@ -454,7 +540,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
     } else {
         const double alpha = a.g[kRR] / a.g[kPAP];
         const Rows<kRpt> xv = ld<kRpt>(a.x + row);
-        const Rows<kRpt> pv = ld<kRpt>(a.p + row);
+        const Rows<kRpt> pv = ld<kRpt>(cur_p(a, k) + row);
         const Rows<kRpt> rv = ld<kRpt>(a.r + row);
         Rows<kRpt> xn;
 #pragma unroll
@@ -462,27 +548,15 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
             xn.v[i] = xv.v[i] + alpha * pv.v[i];
             rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
         }
-        if (row + kRpt <= a.n) {
-            st<kRpt>(a.x + row, xn);
-        } else {
-            for (int i = 0; i < kRpt; i++)
-                if (row + i < a.n) a.x[row + i] = xn.v[i];
-        }
+        st_rows<kRpt>(a.x, row, a.n, xn);
     }
+    st_rows<kRpt>(a.r, row, a.n, rn);
     double d = 0.0;
-    if (row + kRpt <= a.n) {
-        st<kRpt>(a.r + row, rn);
 #pragma unroll
-        for (int i = 0; i < kRpt; i++) d += rn.v[i] * rn.v[i];
-    } else {
-        for (int i = 0; i < kRpt; i++)
-            if (row + i < a.n) {
-                a.r[row + i] = rn.v[i];
-                d += rn.v[i] * rn.v[i];
-            }
-    }
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += rn.v[i] * rn.v[i];
     const double bs = block_sum<kSliceRows / kRpt>(d);
-    if (threadIdx.x == 0) a.partial[s] = bs;
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kRR, kPrologue ? 1 : k + 1);
 }
 
 // Timestamp-only kernel around RCCL calls (multi-rank): one lane, one store.
@@ -521,6 +595,7 @@ __global__ __launch_bounds__(256) void k_waxpby(int n, double alpha, const doubl
 }
 
 constexpr int kDotChunk = 4096;  // rows per partial: fixed shape, deterministic
+constexpr int kDotFinalThreads = 1024;
 
 __global__ __launch_bounds__(256) void k_dot_partial(int n, const double* x, const double* y,
                                                      double* partial)
@@ -533,12 +608,12 @@ __global__ __launch_bounds__(256) void k_dot_partial(int n, const double* x, con
     if (threadIdx.x == 0) partial[blockIdx.x] = s;
 }
 
-__global__ __launch_bounds__(kFinalizeThreads) void k_dot_final(const double* partial, int nparts,
+__global__ __launch_bounds__(kDotFinalThreads) void k_dot_final(const double* partial, int nparts,
                                                                 double* out)
 {
     double v = 0.0;
-    for (int i = threadIdx.x; i < nparts; i += kFinalizeThreads) v += partial[i];
-    const double s = block_sum<kFinalizeThreads>(v);
+    for (int i = threadIdx.x; i < nparts; i += kDotFinalThreads) v += partial[i];
+    const double s = block_sum<kDotFinalThreads>(v);
     if (threadIdx.x == 0) *out = s;
 }
 
@@ -624,19 +699,24 @@ void launch_cg_p_update(const CgArgs& a, hipStream_t s)
 //   0 runtime width, 2 rows/thread      1 runtime width, 1 row/thread
 //   2 runtime width, 4 rows/thread
 //   27 / 7  uniform width, fully unrolled, 2 rows/thread
-//   100*w + 27: same with __launch_bounds__ min waves/SIMD w (w = 1..4)
+//   327 / 427: same with __launch_bounds__ min waves/SIMD 3 / 4
 //   +1000: non-temporal loads of vals/cols (1000 = the default: runtime
 //   width, 2 rows/thread, nt -- within ~3 % of the matrix-streaming ceiling)
 //   9999: diagnostic matrix stream without the gather (not an SpMV)
 #define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
-    hipLaunchKernelGGL((k_spmv<RPT, W, true, MINW, NT>), dim3(a.grid), dim3(kSliceRows / RPT), 0, s, \
-                       a, prologue)
+    do {                                                                                            \
+        if (a.fuse_p && !prologue)                                                                  \
+            hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, true>), dim3(a.grid), dim3(kSliceRows / RPT), \
+                               0, s, a, prologue);                                                  \
+        else                                                                                        \
+            hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, false>), dim3(a.grid),                    \
+                               dim3(kSliceRows / RPT), 0, s, a, prologue);                          \
+    } while (0)
 bool spmv_variant_ok(int v)
 {
     switch (v) {
-    case 0: case 1: case 2: case 27: case 7: case 127: case 227: case 327: case 427: case 527:
-    case 627: case 1000: case 1027: case 1007: case 1127: case 1227: case 1327: case 1427:
-    case 1527: case 1627: case 1001: case 1002: case 9999:
+    case 0: case 1: case 2: case 27: case 7: case 327: case 427:
+    case 1000: case 1001: case 1002: case 1027: case 1007: case 9999:
         return true;
     default:
         return false;
@@ -649,23 +729,13 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 1: HPCCG_SPMV(1, 0, 1, false); break;
     case 2: HPCCG_SPMV(4, 0, 1, false); break;
     case 27: HPCCG_SPMV(2, 27, 1, false); break;
-    case 127: HPCCG_SPMV(2, 27, 1, false); break;
-    case 227: HPCCG_SPMV(2, 27, 2, false); break;
     case 327: HPCCG_SPMV(2, 27, 3, false); break;
     case 427: HPCCG_SPMV(2, 27, 4, false); break;
-    case 527: HPCCG_SPMV(2, 27, 5, false); break;
-    case 627: HPCCG_SPMV(2, 27, 6, false); break;
     case 7: HPCCG_SPMV(2, 7, 1, false); break;
     case 1000: HPCCG_SPMV(2, 0, 1, true); break;
     case 1001: HPCCG_SPMV(1, 0, 1, true); break;
     case 1002: HPCCG_SPMV(4, 0, 1, true); break;
     case 1027: HPCCG_SPMV(2, 27, 1, true); break;
-    case 1127: HPCCG_SPMV(2, 27, 1, true); break;
-    case 1227: HPCCG_SPMV(2, 27, 2, true); break;
-    case 1327: HPCCG_SPMV(2, 27, 3, true); break;
-    case 1427: HPCCG_SPMV(2, 27, 4, true); break;
-    case 1527: HPCCG_SPMV(2, 27, 5, true); break;
-    case 1627: HPCCG_SPMV(2, 27, 6, true); break;
     case 1007: HPCCG_SPMV(2, 7, 1, true); break;
     case 9999: hipLaunchKernelGGL(k_stream_diag<27>, dim3(a.grid), dim3(256), 0, s, a); break;
     default: HPCCG_SPMV(2, 0, 1, false); break;
@@ -675,7 +745,7 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kFinalizeThreads), 0, s, a, which, prologue);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kReduceThreads), 0, s, a, which, prologue);
 }
 
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)
@@ -711,7 +781,7 @@ void launch_ddot(int n, const double* x, const double* y, double* partial, int n
                  hipStream_t s)
 {
     if (n > 0) hipLaunchKernelGGL(k_dot_partial, dim3(nparts), dim3(256), 0, s, n, x, y, partial);
-    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(kFinalizeThreads), 0, s, partial,
+    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(kDotFinalThreads), 0, s, partial,
                        n > 0 ? nparts : 0, out);
 }
 

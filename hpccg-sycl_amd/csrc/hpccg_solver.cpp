@@ -154,6 +154,8 @@ struct hpccg_hip_matrix {
     int nslices = 0, grid = 0, width = 0, uniform = 0;
     int spmv_variant = 0;
     int use_graph = 1;
+    int fuse_p = 1;  // p = r + beta p inside the SpMV (single rank only)
+    int fold = 1;    // dot finalization folded into the producing kernels
     unsigned int* d_slice_base = nullptr;
     int* d_cols = nullptr;
     double* d_vals = nullptr;
@@ -161,6 +163,7 @@ struct hpccg_hip_matrix {
     size_t npad = 0;
     double* d_pbuf = nullptr;  // ghost_lo_pad + npad + ghost_hi
     double* d_p = nullptr;
+    double* d_p1 = nullptr;  // second p buffer (fuse_p)
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_partial = nullptr;
     double* d_scal = nullptr;  // g[2], loc[2], scratch[4]
@@ -193,7 +196,7 @@ int free_matrix(hpccg_hip_matrix* M)
     if (!M) return 0;
     (void)hipSetDevice(M->device);
     if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
-    void* ptrs[] = {M->d_slice_base, M->d_cols,    M->d_vals,  M->d_pbuf,         M->d_r,
+    void* ptrs[] = {M->d_slice_base, M->d_cols,    M->d_vals,  M->d_pbuf,  M->d_p1,  M->d_r,
                     M->d_Ap,         M->d_x,       M->d_b,     M->d_partial,      M->d_scal,
                     M->d_kst,        M->d_hist,    M->d_stamps, M->d_ddot_partial, M->d_gen_b,
                     M->d_gen_x0,     M->d_gen_xexact};
@@ -242,7 +245,7 @@ int alloc_workspace(hpccg_hip_matrix* M)
     HIP_TRY(hipMalloc(&M->d_pbuf, sizeof(double) * (glo_pad + M->npad + M->ghost_hi + 2)));
     HIP_TRY(hipMemset(M->d_pbuf, 0, sizeof(double) * (glo_pad + M->npad + M->ghost_hi + 2)));
     M->d_p = M->d_pbuf + glo_pad;
-    double** vecs[] = {&M->d_r, &M->d_Ap, &M->d_x, &M->d_b};
+    double** vecs[] = {&M->d_r, &M->d_Ap, &M->d_x, &M->d_b, &M->d_p1};
     for (double** v : vecs) {
         HIP_TRY(hipMalloc(v, sizeof(double) * M->npad));
         HIP_TRY(hipMemset(*v, 0, sizeof(double) * M->npad));
@@ -250,7 +253,8 @@ int alloc_workspace(hpccg_hip_matrix* M)
     HIP_TRY(hipMalloc(&M->d_partial, sizeof(double) * std::max(1, M->nslices)));
     HIP_TRY(hipMalloc(&M->d_scal, sizeof(double) * 8));
     HIP_TRY(hipMemset(M->d_scal, 0, sizeof(double) * 8));
-    HIP_TRY(hipMalloc(&M->d_kst, sizeof(int) * 4));
+    HIP_TRY(hipMalloc(&M->d_kst, sizeof(int) * 8));  // kst[0..3] + tickets[2] (+pad)
+    HIP_TRY(hipMemset(M->d_kst, 0, sizeof(int) * 8));
     return 0;
 }
 
@@ -286,6 +290,10 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.x = x;
     a.r = M->d_r;
     a.p = M->d_p;
+    a.p1 = M->d_p1;
+    a.fuse_p = (M->fuse_p && g_comm.nranks == 1) ? 1 : 0;
+    a.fold = M->fold ? 1 : 0;
+    a.tickets = reinterpret_cast<unsigned int*>(M->d_kst + 4);
     a.Ap = M->d_Ap;
     a.partial = M->d_partial;
     a.g = M->d_scal;
@@ -343,7 +351,7 @@ int ensure_events(hpccg_hip_matrix* M, int slots)
 int enqueue_iteration(hpccg_hip_matrix* M, const CgArgs& a, int slot = -1)
 {
     hipStream_t s = M->stream;
-    launch_cg_p_update(a, s);
+    if (!a.fuse_p) launch_cg_p_update(a, s);
     if (g_comm.nranks > 1) {
         launch_cg_stamp(a, kStampHalo, false, s);
         TRY(enqueue_halo(M, a.p));
@@ -351,7 +359,7 @@ int enqueue_iteration(hpccg_hip_matrix* M, const CgArgs& a, int slot = -1)
     if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], s));
     launch_cg_spmv(a, M->spmv_variant, false, s);
     if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], s));
-    launch_cg_finalize(a, kPAP, false, s);
+    if (!a.fold) launch_cg_finalize(a, kPAP, false, s);
     if (g_comm.nranks > 1) {
         launch_cg_stamp(a, kStampArPAP, false, s);
         TRY(enqueue_allreduce(M, a, kPAP));
@@ -359,7 +367,7 @@ int enqueue_iteration(hpccg_hip_matrix* M, const CgArgs& a, int slot = -1)
     if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], s));
     launch_cg_update(a, false, s);
     if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 3], s));
-    launch_cg_finalize(a, kRR, false, s);
+    if (!a.fold) launch_cg_finalize(a, kRR, false, s);
     if (g_comm.nranks > 1) {
         launch_cg_stamp(a, kStampArRR, false, s);
         TRY(enqueue_allreduce(M, a, kRR));
@@ -382,7 +390,7 @@ int enqueue_prologue(hpccg_hip_matrix* M, const CgArgs& a, bool events)
     if (events) HIP_TRY(hipEventRecord(M->ev[2], s));
     launch_cg_update(a, true, s);                  // r = b - Ap (+ r.r partials)
     if (events) HIP_TRY(hipEventRecord(M->ev[3], s));
-    launch_cg_finalize(a, kRR, true, s);           // rtrans, k = 1
+    if (!a.fold) launch_cg_finalize(a, kRR, true, s);  // rtrans, k = 1
     if (g_comm.nranks > 1) {
         launch_cg_stamp(a, kStampArRR, true, s);
         TRY(enqueue_allreduce(M, a, kRR));
@@ -458,7 +466,7 @@ int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_
     const int iters = std::max(0, max_iter - 1);
     const bool events = M->event_timing != 0;
     if (events) TRY(ensure_events(M, iters + 1));
-    HIP_TRY(hipMemsetAsync(M->d_kst, 0, sizeof(int) * 4, M->stream));
+    HIP_TRY(hipMemsetAsync(M->d_kst, 0, sizeof(int) * 8, M->stream));  // state + tickets
     TRY(enqueue_prologue(M, a, events));
     const bool graph = !events && M->use_graph && g_comm.nranks == 1 && iters >= kGraphChunk;
     int done = 0;
@@ -873,6 +881,10 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->use_graph = (int)value;
     } else if (!std::strcmp(key, "event_timing")) {
         M->event_timing = (int)value;
+    } else if (!std::strcmp(key, "fuse_p")) {
+        M->fuse_p = (int)value;
+    } else if (!std::strcmp(key, "fold")) {
+        M->fold = (int)value;
     } else if (!std::strcmp(key, "spmv_variant")) {
         const int v = (int)value;
         const int w = v % 100;  // 27 / 7 for the fixed-width variants
@@ -948,6 +960,18 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     *avg_us = 1e3 * ms / reps;
+    return 0;
+}
+
+int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* value)
+{
+    if (!M || !key || !value) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    if (!std::strcmp(key, "use_graph")) *value = M->use_graph;
+    else if (!std::strcmp(key, "spmv_variant")) *value = M->spmv_variant;
+    else if (!std::strcmp(key, "event_timing")) *value = M->event_timing;
+    else if (!std::strcmp(key, "fuse_p")) *value = (M->fuse_p && g_comm.nranks == 1) ? 1 : 0;
+    else if (!std::strcmp(key, "fold")) *value = M->fold;
+    else return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
     return 0;
 }
 

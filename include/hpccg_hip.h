@@ -103,10 +103,14 @@ int hpccg_hip_solve_device(hpccg_hip_matrix* M, const double* b_dev, double* x_d
  * residual, out[k] = iteration k (k <= niters). Returns entries written. */
 int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
 /* Solver knobs: "use_graph" (capture CG iterations in a hipGraph; default
- * on for nranks == 1), "spmv_variant" (0 = auto), "event_timing" (1 = bracket
- * every SpMV and fused-update launch with hipEvents on the solver stream;
- * eager launches). */
+ * on for nranks == 1), "spmv_variant" (SpMV kernel, see hpccg_kernels.hip),
+ * "event_timing" (1 = bracket every SpMV and fused-update launch with
+ * hipEvents on the solver stream; eager launches), "fuse_p" (1 = compute
+ * p = r + beta*p inside the SpMV; single rank only), "fold" (1 = the last
+ * block of each producing kernel completes the dot product). None of them
+ * changes a computed value: fuse_p/fold on and off are bitwise equal. */
 int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value);
+int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* value);
 /* hipEvent kernel timings of the last solve with event_timing on:
  * out[0] SpMV total ms, out[1] SpMV launches, out[2] fused-update total ms,
  * out[3] update launches (launches that did work, i.e. <= niters + 1). */

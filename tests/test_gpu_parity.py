@@ -52,8 +52,7 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
     assert np.array_equal(host(y), prob.b)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 527, 627, 1000, 1001, 1002, 1027,
-                                     1327, 1427])
+@pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 1000, 1001, 1002, 1027])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
@@ -74,6 +73,26 @@ def test_sparsemv_variants_agree(hp, gpu, variant):
         assert nr == nr0
         assert np.array_equal(tr, M.last_trace())
         assert np.array_equal(x, x0)
+
+
+@pytest.mark.parametrize("dims", [(24, 20, 18), (13, 7, 5), (40, 40, 40)])
+def test_fusion_options_bitwise_equal(hp, gpu, dims):
+    """fuse_p (p update inside the SpMV gather) and fold (last-block dot
+    completion) change only where work happens, never a value: all four
+    combinations, eager and graph launches, give bitwise the same solve."""
+    prob = hp.generate_matrix(*dims)
+    M = hp.Matrix.from_hpc(prob)
+    results = []
+    for fuse in (0, 1):
+        for fold in (0, 1):
+            for graph in (0, 1):
+                M.set_option("fuse_p", fuse)
+                M.set_option("fold", fold)
+                M.set_option("use_graph", graph)
+                x = prob.x
+                _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
+                results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    assert all(r == results[0] for r in results)
 
 
 def test_waxpby_bitwise_vs_reference(hp, gpu, golden):

@@ -17,6 +17,6 @@ step() {
 }
 N=${N:-200}
 step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --steps 2 --warmup 1 --no-cpu-baseline
-step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python tools/spmv_sweep.py --n $N --variants 1000 9999 --reps 3
-step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python tools/spmv_sweep.py --n $N --variants 1000 9999 --reps 3
+step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python tools/pmc_workload.py --n $N
+step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python tools/pmc_workload.py --n $N
 find $OUT -name "*.csv" | head -20

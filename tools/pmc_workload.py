@@ -1,0 +1,25 @@
+#!/usr/bin/env python3
+"""Workload for the rocprofv3 --pmc passes: the known-bytes streaming kernel
+(FETCH_SIZE calibration) and a short CG solve with the production kernels."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import load_pkg  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=200)
+ap.add_argument("--iters", type=int, default=12)
+args = ap.parse_args()
+import torch  # noqa: E402,F401
+hp = load_pkg()
+hp.set_device(0)
+M = hp.Matrix.generate(args.n, args.n, args.n)
+M.diag_spmv(9999, 3)
+b, _, _ = M.vectors()
+x = torch.zeros(args.n ** 3, dtype=torch.float64, device="cuda:0")
+M.set_option("use_graph", 0)
+hp.HPCCG(M, b, x, max_iter=args.iters, device=True)
+print("fuse_p", M.get_option("fuse_p"), "variant", M.get_option("spmv_variant"))
