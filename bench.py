@@ -117,6 +117,8 @@ def main():
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=-1, help="SpMV kernel variant (-1 auto)")
+    ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1 default)")
+    ap.add_argument("--fold", type=int, default=-1, help="last-block dot completion (-1 default)")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: hipGraph launches, no per-kernel events (roofline from stamps)")
     args = ap.parse_args()
@@ -145,6 +147,10 @@ def main():
     info = M.info()
     if args.variant >= 0:
         M.set_option("spmv_variant", args.variant)
+    if args.fuse_p >= 0:
+        M.set_option("fuse_p", args.fuse_p)
+    if args.fold >= 0:
+        M.set_option("fold", args.fold)
     M.set_option("event_timing", 0 if args.graph else 1)
     b, x0, _ = M.vectors()
     nrow = n * n * n
