@@ -11,7 +11,7 @@ namespace hpccg {
 // the per-slice dot partials of every kernel aligned (deterministic sums).
 constexpr int kSliceRows = 512;
 constexpr int kNumXcd = 8;        // MI355X: 8 XCDs, blocks dealt round-robin
-constexpr int kReduceThreads = 256;  // shape of every final dot reduction
+constexpr int kReduceThreads = 1024;  // shape of every final dot reduction
 
 // Indices into the device scalar block.
 enum Scalar : int { kRR = 0, kPAP = 1 };

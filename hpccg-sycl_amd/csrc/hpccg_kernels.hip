@@ -230,24 +230,39 @@ __device__ __forceinline__ void st_rows(double* __restrict__ base, int row, int 
 // counter (Guideline 16 hand-off: plain partial store -> agent release ->
 // s_waitcnt -> relaxed ticket add; the last arriver: agent acquire ->
 // s_waitcnt -> barrier -> plain loads). Both give bitwise the same sum.
+// Measured (r01): with fold every block's agent release (buffer_wbl2) writes
+// back its XCD's dirty L2 lines -- the update kernel went 57 -> 653 us -- so
+// fold is off by default and the separate 1024-thread k_finalize is used.
 // which = kPAP: p.Ap (HPCCG.cpp:381); kRR: r.r (HPCCG.cpp:353, 367), which
 // closes iteration k and advances kst[0].
 // ---------------------------------------------------------------------------
 template <int kThreads>
 __device__ __forceinline__ void reduce_partials(const CgArgs& a, int which, int kfinal)
 {
-    // The fixed shape is kReduceThreads "virtual" threads: virtual thread t sums
-    // partial[t], partial[t + 256], ... in order; virtual waves are reduced by
-    // the shfl_xor butterfly and then added in wave order. Blocks of any size
-    // emulate exactly that shape, so every kernel produces the same bits.
+    // Fixed shape, independent of the block that runs it: kReduceThreads
+    // "virtual" threads; virtual thread t adds the contiguous chunk
+    // partial[t*C, (t+1)*C) (C = ceil(nslices / kReduceThreads)) in order,
+    // loading 8 at a time so the loads are in flight together; virtual waves
+    // are reduced by the shfl_xor butterfly, then added in wave order.
     constexpr int kVWaves = kReduceThreads / kWave;
     constexpr int kRealWaves = kThreads / kWave;
     __shared__ double wsum[kVWaves];
     const int lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
+    const int chunk = (a.nslices + kReduceThreads - 1) / kReduceThreads;
     for (int vw = w; vw < kVWaves; vw += kRealWaves) {
+        const int vt = vw * kWave + lane;
+        const int i0 = vt * chunk;
+        const int i1 = min(i0 + chunk, a.nslices);
         double v = 0.0;
-        for (int i = vw * kWave + lane; i < a.nslices; i += kReduceThreads) v += a.partial[i];
+        for (int i = i0; i < i1; i += 8) {
+            double t[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) t[u] = a.partial[min(i + u, i1 - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (i + u < i1) v += t[u];
+        }
         v = wave_sum(v);
         if (lane == 0) wsum[vw] = v;
     }

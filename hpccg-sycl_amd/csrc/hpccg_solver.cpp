@@ -155,7 +155,7 @@ struct hpccg_hip_matrix {
     int spmv_variant = 0;
     int use_graph = 1;
     int fuse_p = 1;  // p = r + beta p inside the SpMV (single rank only)
-    int fold = 1;    // dot finalization folded into the producing kernels
+    int fold = 0;    // dot finalization folded into the producing kernels (slower: see kernels)
     unsigned int* d_slice_base = nullptr;
     int* d_cols = nullptr;
     double* d_vals = nullptr;
