@@ -61,7 +61,18 @@ struct CgArgs {
     const unsigned int* slice_base;  // [nslices + 1], units of kSliceRows slots
     const int* cols;       // local column (ghost-inclusive base), -1 = padding
     const double* vals;
+    // SELL-512-L: per-slice x windows staged in LDS + slice-local indices
+    const unsigned short* lcols;  // LDS index of the column, kLdsPad = padding
+    const int* win_ptr;    // [nslices + 1] into the window arrays
+    const int* win_start;  // first local column of the window
+    const int* win_len;    // entries
+    const int* win_off;    // LDS offset (doubles)
+    int lds_doubles;       // dynamic LDS per block (max staged entries over slices)
 };
+
+constexpr unsigned short kLdsPad = 0xFFFF;
+constexpr int kLdsMaxDoubles = 8192;  // 64 KiB of LDS per block at most
+constexpr int kLdsMaxWindows = 16;
 
 // ---- launches (hpccg_kernels.hip) -----------------------------------------
 // CG iteration pieces; all take the same CgArgs.
@@ -83,8 +94,10 @@ int ddot_nparts(int n);
 void launch_sparsemv(const CgArgs& a, const double* xext, double* y, int variant, hipStream_t s);
 
 // Device generator: writes the SELL-512 image, b, xexact.
+// With win_* non-null it also writes the SELL-512-L index image (lcols).
 void launch_generate(int nx, int ny, int nz, int rank, int size, int use_7pt, long long col_base,
                      const unsigned int* slice_base, int* cols, double* vals, double* b,
-                     double* xexact, int nrow, hipStream_t s);
+                     double* xexact, int nrow, const int* win_ptr, const int* win_start,
+                     const int* win_len, const int* win_off, unsigned short* lcols, hipStream_t s);
 
 }  // namespace hpccg

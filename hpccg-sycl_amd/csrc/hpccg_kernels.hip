@@ -466,6 +466,97 @@ __global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, boo
     complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
 }
 
+// ---------------------------------------------------------------------------
+// SELL-512-L SpMV: the slice's x windows (host-computed union of the column
+// ranges the slice touches; 3 windows of 512 + 2(nx+1) for the stencils) are
+// staged into LDS with coalesced loads, then every entry reads x from LDS
+// through a 16-bit slice-local index. Same per-row order and products as
+// k_spmv, so the same bits; 10 B per stored entry instead of 12.
+// ---------------------------------------------------------------------------
+template <int kRpt, bool kNT>
+__device__ __forceinline__ void ld_lcols(const unsigned short* __restrict__ p, unsigned (&c)[kRpt])
+{
+    if constexpr (kRpt == 1) {
+        c[0] = kNT ? __builtin_nontemporal_load(p) : p[0];
+    } else if constexpr (kRpt == 2) {
+        const unsigned t = kNT ? __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p))
+                               : *reinterpret_cast<const unsigned*>(p);
+        c[0] = t & 0xFFFFu;
+        c[1] = t >> 16;
+    } else {
+#pragma unroll
+        for (int i = 0; i < kRpt; i += 4) {
+            typedef unsigned u2v __attribute__((ext_vector_type(2)));
+            const u2v t = kNT ? __builtin_nontemporal_load(reinterpret_cast<const u2v*>(p + i))
+                              : *reinterpret_cast<const u2v*>(p + i);
+            c[i] = t.x & 0xFFFFu;
+            c[i + 1] = t.x >> 16;
+            c[i + 2] = t.y & 0xFFFFu;
+            c[i + 3] = t.y >> 16;
+        }
+    }
+}
+
+template <int kRpt, bool kNT>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool prologue)
+{
+    extern __shared__ __attribute__((aligned(16))) double xs[];
+    int k = 0;
+    if (!prologue) {
+        k = a.kst[0];
+        const bool run = cg_run(a, k, false);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (run)
+                stamp(a, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    double* __restrict__ p = cur_p(a, k);
+    const double* __restrict__ xext = p - a.ghost_lo;
+    // stage the windows
+    const int w0 = a.win_ptr[s], w1 = a.win_ptr[s + 1];
+    for (int w = w0; w < w1; w++) {
+        const int st0 = a.win_start[w], len = a.win_len[w], off = a.win_off[w];
+        for (int i = threadIdx.x; i < len; i += kSliceRows / kRpt) xs[off + i] = xext[st0 + i];
+    }
+    __syncthreads();
+    const size_t base = (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
+    const int wdt = (int)(a.slice_base[s + 1] - a.slice_base[s]);
+    const double* __restrict__ vp = a.vals + base;
+    const unsigned short* __restrict__ cp = a.lcols + base;
+    double sum[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+#pragma unroll 3
+    for (int j = 0; j < wdt; j++) {
+        unsigned c[kRpt];
+        ld_lcols<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
+        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            const double xv = (c[i] != kLdsPad) ? xs[c[i]] : 0.0;
+            sum[i] = sum[i] + v.v[i] * xv;
+        }
+    }
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    Rows<kRpt> o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+    st_rows<kRpt>(a.Ap, row, a.n, o);
+    if (prologue) return;
+    const Rows<kRpt> pv = ld<kRpt>(p + row);
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += pv.v[i] * o.v[i];
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
+}
+
 // Plain SpMV on arbitrary x (kernel-level C ABI): same body, no dot.
 template <int kRpt>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_plain(CgArgs a, const double* xext,
@@ -638,10 +729,22 @@ __global__ __launch_bounds__(kDotFinalThreads) void k_dot_final(const double* pa
 // past the row length padded with col = -1, val = 0. Local columns are
 // global - col_base (col_base = start_row - ghost_lo).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned short lds_index(int lc, const int* win_start, const int* win_len,
+                                                    const int* win_off, int w0, int w1)
+{
+    for (int w = w0; w < w1; w++)
+        if (lc >= win_start[w] && lc < win_start[w] + win_len[w])
+            return (unsigned short)(win_off[w] + lc - win_start[w]);
+    return kLdsPad;  // not reached: windows cover every column of the slice
+}
+
 __global__ __launch_bounds__(256) void k_generate(int nx, int ny, int nz, int rank, int size,
                                                   int use_7pt, long long col_base,
                                                   const unsigned int* slice_base, int* cols,
-                                                  double* vals, double* b, double* xexact, int nrow)
+                                                  double* vals, double* b, double* xexact, int nrow,
+                                                  const int* win_ptr, const int* win_start,
+                                                  const int* win_len, const int* win_off,
+                                                  unsigned short* lcols)
 {
     const int lrow = blockIdx.x * blockDim.x + threadIdx.x;
     if (lrow >= nrow) return;
@@ -666,6 +769,10 @@ __global__ __launch_bounds__(256) void k_generate(int nx, int ny, int nz, int ra
                     curcol < total_nrow && (!use_7pt || sz * sz + sy * sy + sx * sx <= 1)) {
                     vals[base + (size_t)j * kSliceRows] = (curcol == currow) ? 27.0 : -1.0;
                     cols[base + (size_t)j * kSliceRows] = (int)(curcol - col_base);
+                    if (lcols)
+                        lcols[base + (size_t)j * kSliceRows] =
+                            lds_index((int)(curcol - col_base), win_start, win_len, win_off,
+                                      win_ptr[s], win_ptr[s + 1]);
                     j++;
                 }
             }
@@ -674,12 +781,13 @@ __global__ __launch_bounds__(256) void k_generate(int nx, int ny, int nz, int ra
     for (; j < w; j++) {
         vals[base + (size_t)j * kSliceRows] = 0.0;
         cols[base + (size_t)j * kSliceRows] = -1;
+        if (lcols) lcols[base + (size_t)j * kSliceRows] = kLdsPad;
     }
 }
 
 // Rows of the last slice past nrow: all slots padding.
 __global__ void k_generate_tail(int nrow, int nslices, const unsigned int* slice_base, int* cols,
-                                double* vals)
+                                double* vals, unsigned short* lcols)
 {
     const int s = nslices - 1;
     const int lane = threadIdx.x;
@@ -689,6 +797,7 @@ __global__ void k_generate_tail(int nrow, int nslices, const unsigned int* slice
     for (int j = 0; j < w; j++) {
         vals[(size_t)b0 * kSliceRows + (size_t)j * kSliceRows + lane] = 0.0;
         cols[(size_t)b0 * kSliceRows + (size_t)j * kSliceRows + lane] = -1;
+        if (lcols) lcols[(size_t)b0 * kSliceRows + (size_t)j * kSliceRows + lane] = kLdsPad;
     }
 }
 
@@ -717,6 +826,8 @@ void launch_cg_p_update(const CgArgs& a, hipStream_t s)
 //   327 / 427: same with __launch_bounds__ min waves/SIMD 3 / 4
 //   +1000: non-temporal loads of vals/cols (1000 = the default: runtime
 //   width, 2 rows/thread, nt -- within ~3 % of the matrix-streaming ceiling)
+//   2000 / 2001 / 2002 / 2100: SELL-512-L (x windows staged in LDS, 16-bit
+//   slice-local indices) with 2 / 1 / 4 rows per thread, nt; 2100 = 2 rows, no nt
 //   9999: diagnostic matrix stream without the gather (not an SpMV)
 #define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
     do {                                                                                            \
@@ -732,6 +843,7 @@ bool spmv_variant_ok(int v)
     switch (v) {
     case 0: case 1: case 2: case 27: case 7: case 327: case 427:
     case 1000: case 1001: case 1002: case 1027: case 1007: case 9999:
+    case 2000: case 2001: case 2002: case 2100:
         return true;
     default:
         return false;
@@ -753,6 +865,22 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 1027: HPCCG_SPMV(2, 27, 1, true); break;
     case 1007: HPCCG_SPMV(2, 7, 1, true); break;
     case 9999: hipLaunchKernelGGL(k_stream_diag<27>, dim3(a.grid), dim3(256), 0, s, a); break;
+    case 2000:
+        hipLaunchKernelGGL((k_spmv_lds<2, true>), dim3(a.grid), dim3(kSliceRows / 2),
+                           a.lds_doubles * sizeof(double), s, a, prologue);
+        break;
+    case 2001:
+        hipLaunchKernelGGL((k_spmv_lds<1, true>), dim3(a.grid), dim3(kSliceRows),
+                           a.lds_doubles * sizeof(double), s, a, prologue);
+        break;
+    case 2002:
+        hipLaunchKernelGGL((k_spmv_lds<4, true>), dim3(a.grid), dim3(kSliceRows / 4),
+                           a.lds_doubles * sizeof(double), s, a, prologue);
+        break;
+    case 2100:
+        hipLaunchKernelGGL((k_spmv_lds<2, false>), dim3(a.grid), dim3(kSliceRows / 2),
+                           a.lds_doubles * sizeof(double), s, a, prologue);
+        break;
     default: HPCCG_SPMV(2, 0, 1, false); break;
     }
 }
@@ -808,13 +936,15 @@ void launch_sparsemv(const CgArgs& a, const double* xext, double* y, int variant
 
 void launch_generate(int nx, int ny, int nz, int rank, int size, int use_7pt, long long col_base,
                      const unsigned int* slice_base, int* cols, double* vals, double* b,
-                     double* xexact, int nrow, hipStream_t s)
+                     double* xexact, int nrow, const int* win_ptr, const int* win_start,
+                     const int* win_len, const int* win_off, unsigned short* lcols, hipStream_t s)
 {
     const int nslices = (nrow + kSliceRows - 1) / kSliceRows;
     hipLaunchKernelGGL(k_generate, dim3((nrow + 255) / 256), dim3(256), 0, s, nx, ny, nz, rank, size,
-                       use_7pt, col_base, slice_base, cols, vals, b, xexact, nrow);
+                       use_7pt, col_base, slice_base, cols, vals, b, xexact, nrow, win_ptr,
+                       win_start, win_len, win_off, lcols);
     hipLaunchKernelGGL(k_generate_tail, dim3(1), dim3(kSliceRows), 0, s, nrow, nslices, slice_base,
-                       cols, vals);
+                       cols, vals, lcols);
 }
 
 }  // namespace hpccg

@@ -154,11 +154,15 @@ struct hpccg_hip_matrix {
     int nslices = 0, grid = 0, width = 0, uniform = 0;
     int spmv_variant = 0;
     int use_graph = 1;
-    int fuse_p = 1;  // p = r + beta p inside the SpMV (single rank only)
+    int fuse_p = 0;  // p = r + beta p inside the SpMV (single rank; slower: doubles the gather)
     int fold = 0;    // dot finalization folded into the producing kernels (slower: see kernels)
     unsigned int* d_slice_base = nullptr;
     int* d_cols = nullptr;
     double* d_vals = nullptr;
+    // SELL-512-L (LDS-staged x windows)
+    int has_lds = 0, lds_doubles = 0, nwin = 0;
+    unsigned short* d_lcols = nullptr;
+    int *d_win_ptr = nullptr, *d_win_start = nullptr, *d_win_len = nullptr, *d_win_off = nullptr;
     // workspace (padded to a multiple of kSliceRows rows)
     size_t npad = 0;
     double* d_pbuf = nullptr;  // ghost_lo_pad + npad + ghost_hi
@@ -199,7 +203,8 @@ int free_matrix(hpccg_hip_matrix* M)
     void* ptrs[] = {M->d_slice_base, M->d_cols,    M->d_vals,  M->d_pbuf,  M->d_p1,  M->d_r,
                     M->d_Ap,         M->d_x,       M->d_b,     M->d_partial,      M->d_scal,
                     M->d_kst,        M->d_hist,    M->d_stamps, M->d_ddot_partial, M->d_gen_b,
-                    M->d_gen_x0,     M->d_gen_xexact};
+                    M->d_gen_x0,     M->d_gen_xexact, M->d_lcols, M->d_win_ptr, M->d_win_start,
+                    M->d_win_len,    M->d_win_off};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -305,6 +310,12 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.slice_base = M->d_slice_base;
     a.cols = M->d_cols;
     a.vals = M->d_vals;
+    a.lcols = M->d_lcols;
+    a.win_ptr = M->d_win_ptr;
+    a.win_start = M->d_win_start;
+    a.win_len = M->d_win_len;
+    a.win_off = M->d_win_off;
+    a.lds_doubles = M->lds_doubles;
     return a;
 }
 
@@ -404,6 +415,9 @@ constexpr int kGraphChunk = 8;  // CG iterations per captured graph
 // loads: 450 us at 200^3 (6.05 TB/s algorithmic) vs 436 us for a bare
 // stream of the same image (profiles/spmv_sweep_r01.jsonl).
 constexpr int kDefaultSpmvVariant = 1000;
+// SELL-512-L (x windows in LDS, 16-bit slice-local indices) when every slice
+// qualifies.
+constexpr int kDefaultLdsSpmvVariant = 2000;
 
 int build_graph(hpccg_hip_matrix* M, const CgArgs& a)
 {
@@ -538,6 +552,142 @@ int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// SELL-512-L windows. Per slice: the sorted distinct columns the slice reads,
+// merged into windows when the gap is <= kWinGap entries (staging a few unused
+// x is cheaper than another window). A matrix qualifies when every slice fits
+// kLdsMaxDoubles entries in <= kLdsMaxWindows windows; otherwise the plain
+// SELL-512 kernels are used.
+// ---------------------------------------------------------------------------
+constexpr int kWinGap = 16;
+
+struct Windows {
+    std::vector<int> ptr, start, len, off;
+    int max_staged = 0;
+};
+
+bool windows_from_cols(std::vector<int>& cols, Windows& W)
+{
+    std::sort(cols.begin(), cols.end());
+    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+    int staged = 0, nw = 0;
+    size_t i = 0;
+    while (i < cols.size()) {
+        const int st = cols[i];
+        int last = st;
+        size_t j = i + 1;
+        while (j < cols.size() && cols[j] - last <= kWinGap) last = cols[j++];
+        W.start.push_back(st);
+        W.len.push_back(last - st + 1);
+        W.off.push_back(staged);
+        staged += last - st + 1;
+        nw++;
+        i = j;
+    }
+    W.ptr.push_back((int)W.start.size());
+    W.max_staged = std::max(W.max_staged, staged);
+    return staged <= kLdsMaxDoubles && nw <= kLdsMaxWindows;
+}
+
+// From the host SELL image (local columns, -1 padding). Fills lcols.
+bool build_windows_from_image(int nslices, const std::vector<unsigned int>& sb, const std::vector<int>& hc,
+                              Windows& W, std::vector<unsigned short>& lcols)
+{
+    W = Windows();
+    W.ptr.push_back(0);
+    std::vector<int> cols;
+    for (int s = 0; s < nslices; s++) {
+        cols.clear();
+        const size_t e0 = (size_t)sb[s] * kSliceRows, e1 = (size_t)sb[s + 1] * kSliceRows;
+        for (size_t e = e0; e < e1; e++)
+            if (hc[e] >= 0) cols.push_back(hc[e]);
+        if (!windows_from_cols(cols, W)) return false;
+    }
+    lcols.assign(hc.size(), kLdsPad);
+    const int nth = std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
+    auto work = [&](int t) {
+        for (int s = t; s < nslices; s += nth) {
+            const int w0 = W.ptr[s], w1 = W.ptr[s + 1];
+            const size_t e0 = (size_t)sb[s] * kSliceRows, e1 = (size_t)sb[s + 1] * kSliceRows;
+            for (size_t e = e0; e < e1; e++) {
+                const int c = hc[e];
+                if (c < 0) continue;
+                int w = w0;
+                while (w + 1 < w1 && W.start[w + 1] <= c) w++;
+                lcols[e] = (unsigned short)(W.off[w] + c - W.start[w]);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    return true;
+}
+
+// Stencil slabs, analytically: a superset of the columns a slice of rows
+// [r0, r1) can touch -- the three z-planes' ranges widened by nx + 1.
+bool build_windows_stencil(int nslices, int nrow, int nx, int nxy, int ghost_lo, long long ncol_ext,
+                           Windows& W)
+{
+    W = Windows();
+    W.ptr.push_back(0);
+    for (int s = 0; s < nslices; s++) {
+        const long long r0 = (long long)s * kSliceRows, r1 = std::min<long long>(nrow, r0 + kSliceRows);
+        std::vector<std::pair<long long, long long>> iv;
+        for (int sz = -1; sz <= 1; sz++) {
+            long long lo = ghost_lo + r0 + (long long)sz * nxy - nx - 1;
+            long long hi = ghost_lo + r1 - 1 + (long long)sz * nxy + nx + 1;
+            lo = std::max(0LL, lo);
+            hi = std::min(ncol_ext - 1, hi);
+            if (lo <= hi) iv.push_back({lo, hi});
+        }
+        std::sort(iv.begin(), iv.end());
+        int staged = 0, nw = 0;
+        long long cs = -1, ce = -2;
+        auto flush = [&]() {
+            if (cs < 0) return;
+            W.start.push_back((int)cs);
+            W.len.push_back((int)(ce - cs + 1));
+            W.off.push_back(staged);
+            staged += (int)(ce - cs + 1);
+            nw++;
+        };
+        for (auto& p : iv) {
+            if (cs >= 0 && p.first <= ce + kWinGap) {
+                ce = std::max(ce, p.second);
+            } else {
+                flush();
+                cs = p.first;
+                ce = p.second;
+            }
+        }
+        flush();
+        W.ptr.push_back((int)W.start.size());
+        W.max_staged = std::max(W.max_staged, staged);
+        if (staged > kLdsMaxDoubles || nw > kLdsMaxWindows) return false;
+    }
+    return true;
+}
+
+int upload_windows(hpccg_hip_matrix* M, const Windows& W)
+{
+    M->nwin = (int)W.start.size();
+    const size_t nw = std::max<size_t>(1, W.start.size());
+    HIP_TRY(hipMalloc(&M->d_win_ptr, sizeof(int) * W.ptr.size()));
+    HIP_TRY(hipMemcpy(M->d_win_ptr, W.ptr.data(), sizeof(int) * W.ptr.size(), hipMemcpyHostToDevice));
+    int** dst[] = {&M->d_win_start, &M->d_win_len, &M->d_win_off};
+    const std::vector<int>* src[] = {&W.start, &W.len, &W.off};
+    for (int i = 0; i < 3; i++) {
+        HIP_TRY(hipMalloc(dst[i], sizeof(int) * nw));
+        if (!src[i]->empty())
+            HIP_TRY(hipMemcpy(*dst[i], src[i]->data(), sizeof(int) * src[i]->size(), hipMemcpyHostToDevice));
+    }
+    M->lds_doubles = std::max(1, W.max_staged);
+    M->has_lds = 1;
+    return 0;
+}
+
 template <class RowLen, class RowAt>
 int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_nrow, RowLen row_len,
                      RowAt row_at)
@@ -594,7 +744,10 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
         free_matrix(M);
         return set_err(HPCCG_HIP_EPLAN, "column index outside the halo plan");
     }
-    M->spmv_variant = kDefaultSpmvVariant;
+    Windows W;
+    std::vector<unsigned short> lc;
+    const bool lds_ok = nrow > 0 && build_windows_from_image(M->nslices, sb, hc, W, lc);
+    M->spmv_variant = lds_ok ? kDefaultLdsSpmvVariant : kDefaultSpmvVariant;
     rc = [&]() -> int {
         HIP_TRY(hipMalloc(&M->d_slice_base, sizeof(unsigned int) * sb.size()));
         HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
@@ -602,6 +755,11 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
         HIP_TRY(hipMemcpy(M->d_cols, hc.data(), sizeof(int) * hc.size(), hipMemcpyHostToDevice));
         HIP_TRY(hipMalloc(&M->d_vals, sizeof(double) * hv.size()));
         HIP_TRY(hipMemcpy(M->d_vals, hv.data(), sizeof(double) * hv.size(), hipMemcpyHostToDevice));
+        if (lds_ok) {
+            TRY(upload_windows(M, W));
+            HIP_TRY(hipMalloc(&M->d_lcols, sizeof(unsigned short) * lc.size()));
+            HIP_TRY(hipMemcpy(M->d_lcols, lc.data(), sizeof(unsigned short) * lc.size(), hipMemcpyHostToDevice));
+        }
         return alloc_workspace(M);
     }();
     if (rc) {
@@ -822,10 +980,17 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     sb[M->nslices] = (unsigned int)acc;
     M->nslots = acc * kSliceRows;
     M->width = M->uniform ? wmax : 0;
-    M->spmv_variant = kDefaultSpmvVariant;
+    Windows W;
+    const long long ncol_ext = (long long)M->ghost_lo + n + M->ghost_hi;
+    const bool lds_ok = build_windows_stencil(M->nslices, n, nx, nxy, M->ghost_lo, ncol_ext, W);
+    M->spmv_variant = lds_ok ? kDefaultLdsSpmvVariant : kDefaultSpmvVariant;
     rc = [&]() -> int {
         HIP_TRY(hipMalloc(&M->d_slice_base, sizeof(unsigned int) * sb.size()));
         HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
+        if (lds_ok) {
+            TRY(upload_windows(M, W));
+            HIP_TRY(hipMalloc(&M->d_lcols, sizeof(unsigned short) * std::max(1LL, M->nslots)));
+        }
         HIP_TRY(hipMalloc(&M->d_cols, sizeof(int) * std::max(1LL, M->nslots)));
         HIP_TRY(hipMalloc(&M->d_vals, sizeof(double) * std::max(1LL, M->nslots)));
         TRY(alloc_workspace(M));
@@ -836,7 +1001,8 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
         HIP_TRY(hipMemset(M->d_gen_x0, 0, sizeof(double) * M->npad));
         HIP_TRY(hipMemset(M->d_gen_xexact, 0, sizeof(double) * M->npad));
         launch_generate(nx, ny, nz, rank, size, use_7pt, start - M->ghost_lo, M->d_slice_base, M->d_cols,
-                        M->d_vals, M->d_gen_b, M->d_gen_xexact, n, M->stream);
+                        M->d_vals, M->d_gen_b, M->d_gen_xexact, n, M->d_win_ptr, M->d_win_start,
+                        M->d_win_len, M->d_win_off, M->d_lcols, M->stream);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipStreamSynchronize(M->stream));
         return 0;
@@ -892,6 +1058,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
             return set_err(HPCCG_HIP_EINVAL, "unknown spmv variant %lld", value);
         if ((w == 27 || w == 7) && !(M->uniform && M->width == w))
             return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform width-%d SELL image", v, w);
+        if (v >= 2000 && v < 3000 && !M->has_lds)
+            return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-L windows (not built)", v);
         M->spmv_variant = v;
     } else {
         return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
@@ -941,6 +1109,8 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_
     if (!M || !avg_us || reps < 1) return set_err(HPCCG_HIP_EINVAL, "bad argument");
     const int w = variant % 100;
     if (!spmv_variant_ok(variant)) return set_err(HPCCG_HIP_EINVAL, "unknown variant %d", variant);
+    if (variant >= 2000 && variant < 3000 && !M->has_lds)
+        return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-L windows", variant);
     if ((w == 27 || w == 7 || variant == 9999) && !(M->uniform && M->width == (variant == 9999 ? 27 : w)))
         return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform SELL image of that width", variant);
     HIP_TRY(hipSetDevice(M->device));
@@ -971,6 +1141,8 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "event_timing")) *value = M->event_timing;
     else if (!std::strcmp(key, "fuse_p")) *value = (M->fuse_p && g_comm.nranks == 1) ? 1 : 0;
     else if (!std::strcmp(key, "fold")) *value = M->fold;
+    else if (!std::strcmp(key, "lds_doubles")) *value = M->has_lds ? M->lds_doubles : 0;
+    else if (!std::strcmp(key, "windows")) *value = M->nwin;
     else return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
     return 0;
 }

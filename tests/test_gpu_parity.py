@@ -52,7 +52,8 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
     assert np.array_equal(host(y), prob.b)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 1000, 1001, 1002, 1027])
+@pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 1000, 1001, 1002, 1027, 2000, 2001,
+                                     2002, 2100])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
@@ -67,7 +68,7 @@ def test_sparsemv_variants_agree(hp, gpu, variant):
     x0 = prob.x
     _, it0, nr0, _ = hp.HPCCG(M, prob.b, x0, max_iter=60)
     assert it == it0
-    if variant in (1, 2, 1001, 1002):
+    if variant in (1, 2, 1001, 1002, 2001, 2002):
         assert check_trace(tr, M.last_trace(), RTRANS_RTOL_1GPU) > 10
     else:
         assert nr == nr0
