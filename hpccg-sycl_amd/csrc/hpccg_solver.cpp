@@ -280,6 +280,12 @@ int ensure_hist(hpccg_hip_matrix* M, int max_iter)
     return 0;
 }
 
+// fuse_p is implemented by the SELL-512 kernels (variants < 2000) on one rank.
+bool fuse_p_effective(const hpccg_hip_matrix* M)
+{
+    return M->fuse_p && g_comm.nranks == 1 && M->spmv_variant < 2000;
+}
+
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
 {
     CgArgs a;
@@ -296,7 +302,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.r = M->d_r;
     a.p = M->d_p;
     a.p1 = M->d_p1;
-    a.fuse_p = (M->fuse_p && g_comm.nranks == 1) ? 1 : 0;
+    a.fuse_p = fuse_p_effective(M) ? 1 : 0;
     a.fold = M->fold ? 1 : 0;
     a.tickets = reinterpret_cast<unsigned int*>(M->d_kst + 4);
     a.Ap = M->d_Ap;
@@ -1139,7 +1145,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     if (!std::strcmp(key, "use_graph")) *value = M->use_graph;
     else if (!std::strcmp(key, "spmv_variant")) *value = M->spmv_variant;
     else if (!std::strcmp(key, "event_timing")) *value = M->event_timing;
-    else if (!std::strcmp(key, "fuse_p")) *value = (M->fuse_p && g_comm.nranks == 1) ? 1 : 0;
+    else if (!std::strcmp(key, "fuse_p")) *value = fuse_p_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "fold")) *value = M->fold;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_lds ? M->lds_doubles : 0;
     else if (!std::strcmp(key, "windows")) *value = M->nwin;

@@ -84,6 +84,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     prob = hp.generate_matrix(*dims)
     M = hp.Matrix.from_hpc(prob)
     results = []
+    M.set_option("spmv_variant", 1000)  # fuse_p is implemented by the SELL-512 kernels
     for fuse in (0, 1):
         for fold in (0, 1):
             for graph in (0, 1):
@@ -92,7 +93,15 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
                 M.set_option("use_graph", graph)
                 x = prob.x
                 _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
+                assert M.get_option("fuse_p") == fuse
                 results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    # and the LDS kernel (same rows per thread) gives the same bits as well
+    M.set_option("spmv_variant", 2000)
+    M.set_option("fuse_p", 1)
+    assert M.get_option("fuse_p") == 0
+    x = prob.x
+    _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
+    results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     assert all(r == results[0] for r in results)
 
 
