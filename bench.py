@@ -119,6 +119,7 @@ def main():
     ap.add_argument("--variant", type=int, default=-1, help="SpMV kernel variant (-1 auto)")
     ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1 default)")
     ap.add_argument("--fold", type=int, default=-1, help="last-block dot completion (-1 default)")
+    ap.add_argument("--x-defer", type=int, default=-1, help="batched x update (-1 default)")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: hipGraph launches, no per-kernel events (roofline from stamps)")
     args = ap.parse_args()
@@ -151,6 +152,8 @@ def main():
         M.set_option("fuse_p", args.fuse_p)
     if args.fold >= 0:
         M.set_option("fold", args.fold)
+    if args.x_defer >= 0:
+        M.set_option("x_defer", args.x_defer)
     M.set_option("event_timing", 0 if args.graph else 1)
     b, x0, _ = M.vectors()
     nrow = n * n * n

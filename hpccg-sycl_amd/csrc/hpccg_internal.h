@@ -45,7 +45,10 @@ struct CgArgs {
     double* x;
     double* r;
     double* p;             // local rows of p; p - ghost_lo .. p + n + ghost_hi valid
-    double* p1;            // second p buffer (fuse_p: p_k lives in buffer k & 1)
+    long long pstride;     // distance between ring buffers of p (doubles)
+    int nring;             // p_k lives in ring buffer k % nring (1 = in place)
+    int xdefer;            // 1: x += alpha_j p_j applied every nring iterations
+    double* ahist;         // [max_iter + 1]: alpha_k (for the deferred x update)
     int fuse_p;            // 1: p = r + beta p computed inside the SpMV (single rank)
     int fold;              // 1: the last block of each producer reduces the partials
     unsigned int* tickets; // [2] arrival counters for the folded reductions
@@ -73,6 +76,7 @@ struct CgArgs {
 constexpr unsigned short kLdsPad = 0xFFFF;
 constexpr int kLdsMaxDoubles = 8192;  // 64 KiB of LDS per block at most
 constexpr int kLdsMaxWindows = 16;
+constexpr int kXDefer = 8;  // p ring length = x-update deferral depth
 
 // ---- launches (hpccg_kernels.hip) -----------------------------------------
 // CG iteration pieces; all take the same CgArgs.
@@ -84,6 +88,7 @@ void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);
 void launch_cg_end(const CgArgs& a, hipStream_t s);
+void launch_cg_xflush(const CgArgs& a, hipStream_t s);  // pending deferred x updates
 
 // Kernel-level ops on arbitrary device pointers.
 void launch_waxpby(int n, double alpha, const double* x, double beta, const double* y, double* w,

@@ -204,11 +204,12 @@ __device__ __forceinline__ void ld_cols(const int* __restrict__ p, int (&c)[kRpt
 // Vectors are allocated padded to a multiple of 512 rows, so full-width loads
 // are always in bounds; rows >= n are masked on store and in the dots.
 
-// p of iteration k. With fuse_p, p_k is written by the SpMV of iteration k
-// into buffer k & 1 while the gathers read p_{k-1} from the other buffer.
+// p of iteration k lives in ring buffer k % nring: the update of p reads
+// p_{k-1} from the previous buffer, and with x deferral the last nring p's
+// stay available for the batched x update.
 __device__ __forceinline__ double* cur_p(const CgArgs& a, int k)
 {
-    return (a.fuse_p && (k & 1)) ? a.p1 : a.p;
+    return a.p + (size_t)(k % a.nring) * (size_t)a.pstride;
 }
 
 template <int kRpt>
@@ -343,11 +344,11 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_p_update(CgArgs a)
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     const double beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
     const Rows<kRpt> rv = ld<kRpt>(a.r + row);
-    const Rows<kRpt> yv = (k == 1) ? rv : ld<kRpt>(a.p + row);
+    const Rows<kRpt> yv = (k == 1) ? rv : ld<kRpt>(cur_p(a, k - 1) + row);
     Rows<kRpt> o;
 #pragma unroll
     for (int i = 0; i < kRpt; i++) o.v[i] = rv.v[i] + beta * yv.v[i];
-    st_rows<kRpt>(a.p, row, a.n, o);
+    st_rows<kRpt>(cur_p(a, k), row, a.n, o);
 }
 
 // ---------------------------------------------------------------------------
@@ -645,16 +646,29 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
         for (int i = 0; i < kRpt; i++) rn.v[i] = bv.v[i] + (-1.0) * apv.v[i];
     } else {
         const double alpha = a.g[kRR] / a.g[kPAP];
-        const Rows<kRpt> xv = ld<kRpt>(a.x + row);
-        const Rows<kRpt> pv = ld<kRpt>(cur_p(a, k) + row);
+        if (blockIdx.x == 0 && threadIdx.x == 0) a.ahist[k] = alpha;
         const Rows<kRpt> rv = ld<kRpt>(a.r + row);
-        Rows<kRpt> xn;
 #pragma unroll
-        for (int i = 0; i < kRpt; i++) {
-            xn.v[i] = xv.v[i] + alpha * pv.v[i];
-            rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
+        for (int i = 0; i < kRpt; i++) rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
+        if (!a.xdefer) {
+            const Rows<kRpt> xv = ld<kRpt>(a.x + row);
+            const Rows<kRpt> pv = ld<kRpt>(cur_p(a, k) + row);
+            Rows<kRpt> xn;
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) xn.v[i] = xv.v[i] + alpha * pv.v[i];
+            st_rows<kRpt>(a.x, row, a.n, xn);
+        } else if (k % a.nring == 0) {
+            // deferred x update (HPCCG.cpp:383 for iterations k-nring+1 .. k): the same
+            // x + alpha_j p_j roundings in the same order, one pass over x
+            Rows<kRpt> xn = ld<kRpt>(a.x + row);
+            for (int j = k - a.nring + 1; j <= k; j++) {
+                const double aj = (j == k) ? alpha : a.ahist[j];
+                const Rows<kRpt> pj = ld<kRpt>(cur_p(a, j) + row);
+#pragma unroll
+                for (int i = 0; i < kRpt; i++) xn.v[i] = xn.v[i] + aj * pj.v[i];
+            }
+            st_rows<kRpt>(a.x, row, a.n, xn);
         }
-        st_rows<kRpt>(a.x, row, a.n, xn);
     }
     st_rows<kRpt>(a.r, row, a.n, rn);
     double d = 0.0;
@@ -680,6 +694,27 @@ __global__ void k_stamp(CgArgs a, int slot, bool prologue)
 }
 
 __global__ void k_end(CgArgs a) { mark_end(a); }
+
+// After the loop: x += alpha_j p_j for the iterations since the last batched
+// update (niters = kst[0] - 1 is final here).
+template <int kRpt>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_xflush(CgArgs a)
+{
+    const int niters = a.kst[0] - 1;
+    const int first = (niters / a.nring) * a.nring + 1;
+    if (!a.xdefer || first > niters) return;
+    const int s = xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    Rows<kRpt> xn = ld<kRpt>(a.x + row);
+    for (int j = first; j <= niters; j++) {
+        const double aj = a.ahist[j];
+        const Rows<kRpt> pj = ld<kRpt>(cur_p(a, j) + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) xn.v[i] = xn.v[i] + aj * pj.v[i];
+    }
+    st_rows<kRpt>(a.x, row, a.n, xn);
+}
 
 // ---------------------------------------------------------------------------
 // Kernel-level ops on arbitrary device pointers.
@@ -907,6 +942,11 @@ void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s)
 void launch_cg_end(const CgArgs& a, hipStream_t s)
 {
     hipLaunchKernelGGL(k_end, dim3(1), dim3(64), 0, s, a);
+}
+
+void launch_cg_xflush(const CgArgs& a, hipStream_t s)
+{
+    if (a.xdefer) hipLaunchKernelGGL(k_xflush<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
 }
 
 void launch_waxpby(int n, double alpha, const double* x, double beta, const double* y, double* w,

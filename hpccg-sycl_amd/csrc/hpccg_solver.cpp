@@ -165,9 +165,11 @@ struct hpccg_hip_matrix {
     int *d_win_ptr = nullptr, *d_win_start = nullptr, *d_win_len = nullptr, *d_win_off = nullptr;
     // workspace (padded to a multiple of kSliceRows rows)
     size_t npad = 0;
-    double* d_pbuf = nullptr;  // ghost_lo_pad + npad + ghost_hi
-    double* d_p = nullptr;
-    double* d_p1 = nullptr;  // second p buffer (fuse_p)
+    double* d_pbuf = nullptr;  // kXDefer ring buffers of [ghost_lo_pad | npad | ghost_hi_pad]
+    double* d_p = nullptr;     // local rows of ring buffer 0
+    long long pstride = 0;     // doubles between ring buffers
+    double* d_ahist = nullptr;
+    int x_defer = 1;           // batched x update every kXDefer iterations
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_partial = nullptr;
     double* d_scal = nullptr;  // g[2], loc[2], scratch[4]
@@ -200,7 +202,7 @@ int free_matrix(hpccg_hip_matrix* M)
     if (!M) return 0;
     (void)hipSetDevice(M->device);
     if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
-    void* ptrs[] = {M->d_slice_base, M->d_cols,    M->d_vals,  M->d_pbuf,  M->d_p1,  M->d_r,
+    void* ptrs[] = {M->d_slice_base, M->d_cols,    M->d_vals,  M->d_pbuf,  M->d_ahist,  M->d_r,
                     M->d_Ap,         M->d_x,       M->d_b,     M->d_partial,      M->d_scal,
                     M->d_kst,        M->d_hist,    M->d_stamps, M->d_ddot_partial, M->d_gen_b,
                     M->d_gen_x0,     M->d_gen_xexact, M->d_lcols, M->d_win_ptr, M->d_win_start,
@@ -247,10 +249,13 @@ int alloc_workspace(hpccg_hip_matrix* M)
     if (M->npad == 0) M->npad = kSliceRows;
     // p = [ghost_lo | n | ghost_hi]; local rows start 512-row aligned
     const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
-    HIP_TRY(hipMalloc(&M->d_pbuf, sizeof(double) * (glo_pad + M->npad + M->ghost_hi + 2)));
-    HIP_TRY(hipMemset(M->d_pbuf, 0, sizeof(double) * (glo_pad + M->npad + M->ghost_hi + 2)));
+    const size_t ghi_pad = ((size_t)M->ghost_hi + 2 + kSliceRows - 1) / kSliceRows * kSliceRows;
+    M->pstride = (long long)(glo_pad + M->npad + ghi_pad);
+    const size_t ptotal = (size_t)M->pstride * kXDefer;
+    HIP_TRY(hipMalloc(&M->d_pbuf, sizeof(double) * ptotal));
+    HIP_TRY(hipMemset(M->d_pbuf, 0, sizeof(double) * ptotal));
     M->d_p = M->d_pbuf + glo_pad;
-    double** vecs[] = {&M->d_r, &M->d_Ap, &M->d_x, &M->d_b, &M->d_p1};
+    double** vecs[] = {&M->d_r, &M->d_Ap, &M->d_x, &M->d_b};
     for (double** v : vecs) {
         HIP_TRY(hipMalloc(v, sizeof(double) * M->npad));
         HIP_TRY(hipMemset(*v, 0, sizeof(double) * M->npad));
@@ -268,7 +273,9 @@ int ensure_hist(hpccg_hip_matrix* M, int max_iter)
     const int need = std::max(2, max_iter + 1);
     if (need > M->hist_cap) {
         if (M->d_hist) (void)hipFree(M->d_hist);
+        if (M->d_ahist) (void)hipFree(M->d_ahist);
         HIP_TRY(hipMalloc(&M->d_hist, sizeof(double) * need));
+        HIP_TRY(hipMalloc(&M->d_ahist, sizeof(double) * need));
         M->hist_cap = need;
     }
     const int scap = 16 + (max_iter + 2) * kNumStampSlots;
@@ -278,6 +285,22 @@ int ensure_hist(hpccg_hip_matrix* M, int max_iter)
         M->stamp_cap = scap;
     }
     return 0;
+}
+
+// Default SpMV kernel for a matrix (measured r01, profiles/r01/spmv_sweep_*.jsonl):
+// SELL-512-L when the staged x per row is small against the row length (27-pt:
+// 5.4 staged doubles vs 26.7 entries per row -> 1.33x faster; 7-pt: 6 vs 7 ->
+// 1.14x slower), non-temporal matrix loads once the image outgrows the 256 MB
+// Infinity Cache (>= 128^3: nt 5-12 % faster; <= 100^3: default policy 2-20 %
+// faster).
+int choose_variant(const hpccg_hip_matrix* M)
+{
+    const double rows = std::max(1, M->nrow);
+    const bool lds = M->has_lds && (double)M->nnz / rows >= 2.5 * M->lds_doubles / (double)kSliceRows;
+    const double image = (double)M->nslots * (lds ? 10.0 : 12.0);
+    const bool big = image > 300e6;
+    if (lds) return big ? 2000 : 2100;
+    return big ? 1000 : 0;
 }
 
 // fuse_p is implemented by the SELL-512 kernels (variants < 2000) on one rank.
@@ -301,8 +324,11 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.x = x;
     a.r = M->d_r;
     a.p = M->d_p;
-    a.p1 = M->d_p1;
+    a.pstride = M->pstride;
     a.fuse_p = fuse_p_effective(M) ? 1 : 0;
+    a.xdefer = M->x_defer ? 1 : 0;
+    a.nring = a.xdefer ? kXDefer : (a.fuse_p ? 2 : 1);
+    a.ahist = M->d_ahist;
     a.fold = M->fold ? 1 : 0;
     a.tickets = reinterpret_cast<unsigned int*>(M->d_kst + 4);
     a.Ap = M->d_Ap;
@@ -363,15 +389,20 @@ int ensure_events(hpccg_hip_matrix* M, int slots)
     return 0;
 }
 
+// p_k's ring buffer (local rows), as the kernels' cur_p computes it.
+double* ring_p(const CgArgs& a, int k) { return a.p + (size_t)(k % a.nring) * (size_t)a.pstride; }
+
 // One CG iteration k (HPCCG.cpp:358-386), fully device resident. slot >= 0:
-// bracket the SpMV and the fused update with that slot's hipEvents.
-int enqueue_iteration(hpccg_hip_matrix* M, const CgArgs& a, int slot = -1)
+// bracket the SpMV and the fused update with that slot's hipEvents. k_host is
+// the iteration the host enqueues (used only to address the halo buffer on
+// multi-rank runs, which launch eagerly).
+int enqueue_iteration(hpccg_hip_matrix* M, const CgArgs& a, int slot = -1, int k_host = 1)
 {
     hipStream_t s = M->stream;
     if (!a.fuse_p) launch_cg_p_update(a, s);
     if (g_comm.nranks > 1) {
         launch_cg_stamp(a, kStampHalo, false, s);
-        TRY(enqueue_halo(M, a.p));
+        TRY(enqueue_halo(M, ring_p(a, k_host)));
     }
     if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], s));
     launch_cg_spmv(a, M->spmv_variant, false, s);
@@ -417,13 +448,7 @@ int enqueue_prologue(hpccg_hip_matrix* M, const CgArgs& a, bool events)
 }
 
 constexpr int kGraphChunk = 8;  // CG iterations per captured graph
-// SELL-512 SpMV, runtime slice width, 2 rows/thread, non-temporal matrix
-// loads: 450 us at 200^3 (6.05 TB/s algorithmic) vs 436 us for a bare
-// stream of the same image (profiles/spmv_sweep_r01.jsonl).
-constexpr int kDefaultSpmvVariant = 1000;
-// SELL-512-L (x windows in LDS, 16-bit slice-local indices) when every slice
-// qualifies.
-constexpr int kDefaultLdsSpmvVariant = 2000;
+
 
 int build_graph(hpccg_hip_matrix* M, const CgArgs& a)
 {
@@ -501,8 +526,9 @@ int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_
         for (; done + kGraphChunk <= iters; done += kGraphChunk)
             HIP_TRY(hipGraphLaunch(M->graph_exec, M->stream));
     }
-    for (; done < iters; done++) TRY(enqueue_iteration(M, a, events ? done + 1 : -1));
+    for (; done < iters; done++) TRY(enqueue_iteration(M, a, events ? done + 1 : -1, done + 1));
     launch_cg_end(a, M->stream);
+    launch_cg_xflush(a, M->stream);  // x += alpha_j p_j still pending (x_defer)
     HIP_TRY(hipGetLastError());
     // results
     int kst[4];
@@ -753,7 +779,6 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
     Windows W;
     std::vector<unsigned short> lc;
     const bool lds_ok = nrow > 0 && build_windows_from_image(M->nslices, sb, hc, W, lc);
-    M->spmv_variant = lds_ok ? kDefaultLdsSpmvVariant : kDefaultSpmvVariant;
     rc = [&]() -> int {
         HIP_TRY(hipMalloc(&M->d_slice_base, sizeof(unsigned int) * sb.size()));
         HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
@@ -766,6 +791,7 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
             HIP_TRY(hipMalloc(&M->d_lcols, sizeof(unsigned short) * lc.size()));
             HIP_TRY(hipMemcpy(M->d_lcols, lc.data(), sizeof(unsigned short) * lc.size(), hipMemcpyHostToDevice));
         }
+        M->spmv_variant = choose_variant(M);
         return alloc_workspace(M);
     }();
     if (rc) {
@@ -989,7 +1015,6 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     Windows W;
     const long long ncol_ext = (long long)M->ghost_lo + n + M->ghost_hi;
     const bool lds_ok = build_windows_stencil(M->nslices, n, nx, nxy, M->ghost_lo, ncol_ext, W);
-    M->spmv_variant = lds_ok ? kDefaultLdsSpmvVariant : kDefaultSpmvVariant;
     rc = [&]() -> int {
         HIP_TRY(hipMalloc(&M->d_slice_base, sizeof(unsigned int) * sb.size()));
         HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
@@ -1006,6 +1031,7 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
         HIP_TRY(hipMemset(M->d_gen_b, 0, sizeof(double) * M->npad));
         HIP_TRY(hipMemset(M->d_gen_x0, 0, sizeof(double) * M->npad));
         HIP_TRY(hipMemset(M->d_gen_xexact, 0, sizeof(double) * M->npad));
+        M->spmv_variant = choose_variant(M);
         launch_generate(nx, ny, nz, rank, size, use_7pt, start - M->ghost_lo, M->d_slice_base, M->d_cols,
                         M->d_vals, M->d_gen_b, M->d_gen_xexact, n, M->d_win_ptr, M->d_win_start,
                         M->d_win_len, M->d_win_off, M->d_lcols, M->stream);
@@ -1055,6 +1081,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->event_timing = (int)value;
     } else if (!std::strcmp(key, "fuse_p")) {
         M->fuse_p = (int)value;
+    } else if (!std::strcmp(key, "x_defer")) {
+        M->x_defer = (int)value;
     } else if (!std::strcmp(key, "fold")) {
         M->fold = (int)value;
     } else if (!std::strcmp(key, "spmv_variant")) {
@@ -1147,6 +1175,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "event_timing")) *value = M->event_timing;
     else if (!std::strcmp(key, "fuse_p")) *value = fuse_p_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "fold")) *value = M->fold;
+    else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_lds ? M->lds_doubles : 0;
     else if (!std::strcmp(key, "windows")) *value = M->nwin;
     else return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);

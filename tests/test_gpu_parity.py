@@ -78,23 +78,24 @@ def test_sparsemv_variants_agree(hp, gpu, variant):
 
 @pytest.mark.parametrize("dims", [(24, 20, 18), (13, 7, 5), (40, 40, 40)])
 def test_fusion_options_bitwise_equal(hp, gpu, dims):
-    """fuse_p (p update inside the SpMV gather) and fold (last-block dot
-    completion) change only where work happens, never a value: all four
-    combinations, eager and graph launches, give bitwise the same solve."""
+    """fuse_p (p update inside the SpMV gather), fold (last-block dot
+    completion) and x_defer (x updated every 8 iterations) change only where
+    work happens, never a value: every combination, eager and graph launches,
+    gives bitwise the same solve."""
     prob = hp.generate_matrix(*dims)
     M = hp.Matrix.from_hpc(prob)
     results = []
     M.set_option("spmv_variant", 1000)  # fuse_p is implemented by the SELL-512 kernels
-    for fuse in (0, 1):
-        for fold in (0, 1):
-            for graph in (0, 1):
-                M.set_option("fuse_p", fuse)
-                M.set_option("fold", fold)
-                M.set_option("use_graph", graph)
-                x = prob.x
-                _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
-                assert M.get_option("fuse_p") == fuse
-                results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    import itertools
+    for fuse, fold, graph, defer in itertools.product((0, 1), (0, 1), (0, 1), (0, 1)):
+        M.set_option("fuse_p", fuse)
+        M.set_option("fold", fold)
+        M.set_option("use_graph", graph)
+        M.set_option("x_defer", defer)
+        x = prob.x
+        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)  # 119 iterations: 7 pending x updates
+        assert M.get_option("fuse_p") == fuse
+        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # and the LDS kernel (same rows per thread) gives the same bits as well
     M.set_option("spmv_variant", 2000)
     M.set_option("fuse_p", 1)

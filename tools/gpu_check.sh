@@ -18,8 +18,9 @@ step pytest_gpu 900 python -m pytest tests -m gpu -q
 step sweep 300 python tools/spmv_sweep.py
 step bench_events 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline
 step bench_graph 300 python bench.py --steps 3 --warmup 1 --graph 1 --no-cpu-baseline
-step bench_nofuse 300 python bench.py --steps 3 --warmup 1 --fuse-p 0 --no-cpu-baseline
-step bench_100_nofuse 300 python bench.py --n 100 --steps 5 --warmup 1 --graph 1 --fuse-p 0 --no-cpu-baseline
+step bench_nodefer 300 python bench.py --steps 3 --warmup 1 --x-defer 0 --no-cpu-baseline
+step bench_7pt 300 python bench.py --n 256 --stencil 7 --steps 3 --warmup 1 --no-cpu-baseline
+step bench_7pt_nodefer 300 python bench.py --n 256 --stencil 7 --steps 3 --warmup 1 --x-defer 0 --no-cpu-baseline
 step bench_100 300 python bench.py --n 100 --steps 5 --warmup 1 --no-cpu-baseline
 step bench_100_graph 300 python bench.py --n 100 --steps 5 --warmup 1 --graph 1 --no-cpu-baseline
 step cli_100 120 hpccg-sycl_amd/bin/test_HPCCG 100 100 100
