@@ -17,8 +17,11 @@ value = (CG iterations x ranks x K) / max-over-ranks wall time of the K steps
       = 200^3-slab CG iterations per second summed over GPUs (at N = 1:
         plain CG iterations/s).
 roofline: the SpMV kernel (84 % of the reference's time, SURVEY 6);
-  achieved = (12 nnz + 20 n) bytes per launch / average launch duration from
-  hipEvents on the solver stream over the timed steps; peak 8 TB/s.
+  achieved = algorithmic bytes of the reference operations it performs
+  (12 nnz + 20 n SpMV, 16 n ddot(p, Ap), + 24 n waxpby when the p update is
+  fused) per launch / average launch duration from hipEvents on the solver
+  stream in the first --event-steps timed steps (launched eagerly; the other
+  timed steps replay hipGraphs); peak 8 TB/s.
 cpu_baseline: the reference compiled from its own sources (oracle/_ref, OpenMP)
   -- or the oracle port if that build is absent -- on a bounded sample of the
   same problem, rank 0, N = 1 only.
@@ -120,8 +123,9 @@ def main():
     ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1 default)")
     ap.add_argument("--fold", type=int, default=-1, help="last-block dot completion (-1 default)")
     ap.add_argument("--x-defer", type=int, default=-1, help="batched x update (-1 default)")
-    ap.add_argument("--graph", type=int, default=0,
-                    help="1: hipGraph launches, no per-kernel events (roofline from stamps)")
+    ap.add_argument("--event-steps", type=int, default=1,
+                    help="timed steps launched eagerly with hipEvents around every SpMV (the "
+                         "roofline's kernel time); the other timed steps replay hipGraphs")
     args = ap.parse_args()
 
     import torch
@@ -154,7 +158,6 @@ def main():
         M.set_option("fold", args.fold)
     if args.x_defer >= 0:
         M.set_option("x_defer", args.x_defer)
-    M.set_option("event_timing", 0 if args.graph else 1)
     b, x0, _ = M.vectors()
     nrow = n * n * n
     x = torch.zeros(nrow, dtype=torch.float64, device=f"cuda:{local_rank}")
@@ -162,12 +165,13 @@ def main():
     log(f"[rank {rank}] setup {time.time() - t0:.2f}s nnz={info['nnz']} slots={info['slots']} "
         f"variant={info['spmv_variant']}")
 
-    def step():
+    def step(events):
+        M.set_option("event_timing", 1 if events else 0)
         x.zero_()
         return hp.HPCCG(M, b, x, max_iter=args.max_iter, device=True)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i == 0)
 
     def barrier():
         if world > 1:
@@ -179,14 +183,16 @@ def main():
     niters_total = 0
     spmv_ms = spmv_n = upd_ms = upd_n = 0.0
     times_acc = [0.0] * 7
-    for _ in range(args.steps):
-        _, it, nr, times = step()
+    for i in range(args.steps):
+        ev = i < args.event_steps
+        _, it, nr, times = step(ev)
         niters_total += it
-        kt = M.kernel_times()
-        spmv_ms += kt["spmv_ms"]
-        spmv_n += kt["spmv_launches"]
-        upd_ms += kt["update_ms"]
-        upd_n += kt["update_launches"]
+        if ev:
+            kt = M.kernel_times()
+            spmv_ms += kt["spmv_ms"]
+            spmv_n += kt["spmv_launches"]
+            upd_ms += kt["update_ms"]
+            upd_n += kt["update_launches"]
         for i in range(7):
             times_acc[i] += times[i]
     torch.cuda.synchronize()
@@ -205,7 +211,8 @@ def main():
     spmv_bytes = 12.0 * info["nnz"] + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fused_p else 0.0)
     if spmv_n > 0:
         spmv_avg_s = spmv_ms / spmv_n * 1e-3
-        timing_src = "hipEvent pairs around every SpMV launch on the solver stream"
+        timing_src = ("hipEvent pairs around every SpMV launch on the solver stream, %d of the "
+                      "%d timed steps (the others replay hipGraphs)" % (args.event_steps, args.steps))
     else:  # graph mode: device-clock stamps (SPARSEMV class time / calls)
         spmv_avg_s = times_acc[3] / max(1, niters_total + args.steps)
         timing_src = "s_memrealtime stamps (graph mode)"

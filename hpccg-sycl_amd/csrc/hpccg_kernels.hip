@@ -498,15 +498,16 @@ __device__ __forceinline__ void ld_lcols(const unsigned short* __restrict__ p, u
     }
 }
 
-template <int kRpt, bool kNT>
+template <int kRpt, bool kNT, bool kFuse>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool prologue)
 {
     extern __shared__ __attribute__((aligned(16))) double xs[];
     int k = 0;
     if (!prologue) {
         k = a.kst[0];
-        const bool run = cg_run(a, k, false);
+        const bool run = cg_run(a, k, kFuse);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = a.g[kRR];
             if (run)
                 stamp(a, kStampSpmv);
             else
@@ -518,11 +519,23 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     if (s >= a.nslices) return;
     double* __restrict__ p = cur_p(a, k);
     const double* __restrict__ xext = p - a.ghost_lo;
-    // stage the windows
+    // stage the windows; with kFuse the staged value is p_k = r + beta*p_{k-1},
+    // the exact expression k_p_update stores (single rank: ghost_lo = 0)
+    double beta = 0.0;
+    const double* __restrict__ pold = a.r;
+    if constexpr (kFuse) {
+        beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+        pold = (k == 1) ? a.r : cur_p(a, k - 1);
+    }
     const int w0 = a.win_ptr[s], w1 = a.win_ptr[s + 1];
     for (int w = w0; w < w1; w++) {
         const int st0 = a.win_start[w], len = a.win_len[w], off = a.win_off[w];
-        for (int i = threadIdx.x; i < len; i += kSliceRows / kRpt) xs[off + i] = xext[st0 + i];
+        for (int i = threadIdx.x; i < len; i += kSliceRows / kRpt) {
+            if constexpr (kFuse)
+                xs[off + i] = a.r[st0 + i] + beta * pold[st0 + i];
+            else
+                xs[off + i] = xext[st0 + i];
+        }
     }
     __syncthreads();
     const size_t base = (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
@@ -549,7 +562,16 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
     st_rows<kRpt>(a.Ap, row, a.n, o);
     if (prologue) return;
-    const Rows<kRpt> pv = ld<kRpt>(p + row);
+    Rows<kRpt> pv;
+    if constexpr (kFuse) {
+        const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+        const Rows<kRpt> yv = ld<kRpt>(pold + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + beta * yv.v[i];
+        st_rows<kRpt>(p, row, a.n, pv);
+    } else {
+        pv = ld<kRpt>(p + row);
+    }
     double d = 0.0;
 #pragma unroll
     for (int i = 0; i < kRpt; i++)
@@ -873,6 +895,16 @@ void launch_cg_p_update(const CgArgs& a, hipStream_t s)
             hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, false>), dim3(a.grid),                    \
                                dim3(kSliceRows / RPT), 0, s, a, prologue);                          \
     } while (0)
+#define HPCCG_SPMV_LDS(RPT, NT)                                                                    \
+    do {                                                                                           \
+        const size_t smem = (size_t)a.lds_doubles * sizeof(double);                                \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, true>), dim3(a.grid), dim3(kSliceRows / RPT), smem, \
+                               s, a, prologue);                                                    \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, false>), dim3(a.grid), dim3(kSliceRows / RPT), \
+                               smem, s, a, prologue);                                              \
+    } while (0)
 bool spmv_variant_ok(int v)
 {
     switch (v) {
@@ -900,26 +932,15 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 1027: HPCCG_SPMV(2, 27, 1, true); break;
     case 1007: HPCCG_SPMV(2, 7, 1, true); break;
     case 9999: hipLaunchKernelGGL(k_stream_diag<27>, dim3(a.grid), dim3(256), 0, s, a); break;
-    case 2000:
-        hipLaunchKernelGGL((k_spmv_lds<2, true>), dim3(a.grid), dim3(kSliceRows / 2),
-                           a.lds_doubles * sizeof(double), s, a, prologue);
-        break;
-    case 2001:
-        hipLaunchKernelGGL((k_spmv_lds<1, true>), dim3(a.grid), dim3(kSliceRows),
-                           a.lds_doubles * sizeof(double), s, a, prologue);
-        break;
-    case 2002:
-        hipLaunchKernelGGL((k_spmv_lds<4, true>), dim3(a.grid), dim3(kSliceRows / 4),
-                           a.lds_doubles * sizeof(double), s, a, prologue);
-        break;
-    case 2100:
-        hipLaunchKernelGGL((k_spmv_lds<2, false>), dim3(a.grid), dim3(kSliceRows / 2),
-                           a.lds_doubles * sizeof(double), s, a, prologue);
-        break;
+    case 2000: HPCCG_SPMV_LDS(2, true); break;
+    case 2001: HPCCG_SPMV_LDS(1, true); break;
+    case 2002: HPCCG_SPMV_LDS(4, true); break;
+    case 2100: HPCCG_SPMV_LDS(2, false); break;
     default: HPCCG_SPMV(2, 0, 1, false); break;
     }
 }
 #undef HPCCG_SPMV
+#undef HPCCG_SPMV_LDS
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
 {

@@ -154,7 +154,7 @@ struct hpccg_hip_matrix {
     int nslices = 0, grid = 0, width = 0, uniform = 0;
     int spmv_variant = 0;
     int use_graph = 1;
-    int fuse_p = 0;  // p = r + beta p inside the SpMV (single rank; slower: doubles the gather)
+    int fuse_p = -1;  // p = r + beta p inside the SpMV: -1 auto (on for the LDS kernels only)
     int fold = 0;    // dot finalization folded into the producing kernels (slower: see kernels)
     unsigned int* d_slice_base = nullptr;
     int* d_cols = nullptr;
@@ -303,10 +303,14 @@ int choose_variant(const hpccg_hip_matrix* M)
     return big ? 1000 : 0;
 }
 
-// fuse_p is implemented by the SELL-512 kernels (variants < 2000) on one rank.
+// fuse_p (single rank): measured slower in the plain SELL-512 kernels, where it
+// doubles every gather (561 -> 744 us at 200^3), so "auto" enables it only for
+// the SELL-512-L kernels, which compute p_k once per staged window entry.
 bool fuse_p_effective(const hpccg_hip_matrix* M)
 {
-    return M->fuse_p && g_comm.nranks == 1 && M->spmv_variant < 2000;
+    if (g_comm.nranks != 1 || M->spmv_variant == 9999) return false;
+    if (M->fuse_p < 0) return M->spmv_variant >= 2000;
+    return M->fuse_p != 0;
 }
 
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)

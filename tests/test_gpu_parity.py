@@ -96,13 +96,14 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)  # 119 iterations: 7 pending x updates
         assert M.get_option("fuse_p") == fuse
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
-    # and the LDS kernel (same rows per thread) gives the same bits as well
-    M.set_option("spmv_variant", 2000)
-    M.set_option("fuse_p", 1)
-    assert M.get_option("fuse_p") == 0
-    x = prob.x
-    _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
-    results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    # and the LDS kernels (same rows per thread), fused or not, give the same bits
+    for v, fuse in itertools.product((2000, 2100), (0, 1)):
+        M.set_option("spmv_variant", v)
+        M.set_option("fuse_p", fuse)
+        assert M.get_option("fuse_p") == fuse
+        x = prob.x
+        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
+        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     assert all(r == results[0] for r in results)
 
 
