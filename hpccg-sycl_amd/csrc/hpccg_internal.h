@@ -11,7 +11,6 @@ namespace hpccg {
 // the per-slice dot partials of every kernel aligned (deterministic sums).
 constexpr int kSliceRows = 512;
 constexpr int kNumXcd = 8;        // MI355X: 8 XCDs, blocks dealt round-robin
-constexpr int kReduceThreads = 1024;  // shape of every final dot reduction
 
 // Indices into the device scalar block.
 enum Scalar : int { kRR = 0, kPAP = 1 };
@@ -51,9 +50,9 @@ struct CgArgs {
     double* ahist;         // [max_iter + 1]: alpha_k (for the deferred x update)
     int fuse_p;            // 1: p = r + beta p computed inside the SpMV (single rank)
     int fold;              // 1: the last block of each producer reduces the partials
-    unsigned int* tickets; // [2] arrival counters for the folded reductions
+    unsigned int* tickets; // [2 x (ngroups + 1)] arrival counters (fold): groups, top
     double* Ap;
-    double* partial;       // [nslices] per-slice partial dot products
+    double* partial;       // [nslices] slice partials, then 2 x ngroups group sums
     double* g;             // [2] dot results after the all-reduce
     double* loc;           // [2] local dot results
     double* hist;          // [max_iter + 1]: hist[j] = r_j . r_j (global)

@@ -224,85 +224,127 @@ __device__ __forceinline__ void st_rows(double* __restrict__ base, int row, int 
 }
 
 // ---------------------------------------------------------------------------
-// Dot-product completion. Every producing block reduces its slice to one
-// partial (fixed shape). The partials are then summed in slice order by
-// kReduceThreads threads -- either by a separate one-block kernel
-// (k_finalize) or, with a.fold, by the block that arrives last at a ticket
-// counter (Guideline 16 hand-off: plain partial store -> agent release ->
-// s_waitcnt -> relaxed ticket add; the last arriver: agent acquire ->
-// s_waitcnt -> barrier -> plain loads). Both give bitwise the same sum.
-// Measured (r01): with fold every block's agent release (buffer_wbl2) writes
-// back its XCD's dirty L2 lines -- the update kernel went 57 -> 653 us -- so
-// fold is off by default and the separate 1024-thread k_finalize is used.
+// Dot-product completion, fixed two-level shape (bitwise identical whoever
+// runs it): slice partials are summed in groups of kGroup by a 64-lane
+// butterfly (group g = slices [64g, 64g+64)); the group sums are then added by
+// kTopThreads "virtual" threads (virtual thread t adds group sums t, t+256, ...
+// in order), a butterfly per virtual wave, and the 4 wave sums in order.
 // which = kPAP: p.Ap (HPCCG.cpp:381); kRR: r.r (HPCCG.cpp:353, 367), which
 // closes iteration k and advances kst[0].
+//
+// a.fold = 1 (default): completed inside the producing kernel. Every block
+// publishes its partial with a write-through (sc1) store, waits for it
+// (s_waitcnt vmcnt(0)) and takes a relaxed agent-scope ticket on its group;
+// the group's last arriver (told by the ticket value) acquires, reads the
+// group's partials with sc1 loads, publishes the group sum the same way and
+// takes a ticket on the top counter; the last group reducer forms the total.
+// This is the guide's in-launch split-K form (cdna_hip_programming.md 5,
+// "In-launch split-K reduction", sc1 slab stores, no release fence): a
+// per-block agent release (buffer_wbl2) instead measured 57 -> 653 us on the
+// update kernel, and one block reading all 15625 partials took 8.9 us.
+// a.fold = 0: a separate one-block k_finalize computes the same two levels.
 // ---------------------------------------------------------------------------
-template <int kThreads>
-__device__ __forceinline__ void reduce_partials(const CgArgs& a, int which, int kfinal)
+constexpr int kGroup = 64;
+constexpr int kTopThreads = 256;
+
+__device__ __forceinline__ void st_sc1(double* p, double v)
 {
-    // Fixed shape, independent of the block that runs it: kReduceThreads
-    // "virtual" threads; virtual thread t adds the contiguous chunk
-    // partial[t*C, (t+1)*C) (C = ceil(nslices / kReduceThreads)) in order,
-    // loading 8 at a time so the loads are in flight together; virtual waves
-    // are reduced by the shfl_xor butterfly, then added in wave order.
-    constexpr int kVWaves = kReduceThreads / kWave;
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ int ngroups_of(const CgArgs& a) { return (a.nslices + kGroup - 1) / kGroup; }
+
+// group sum by one wave (lane l reads slice partial 64g + l)
+__device__ __forceinline__ double group_sum(const CgArgs& a, int g, int lane)
+{
+    const int i = g * kGroup + lane;
+    const double v = (i < a.nslices) ? ld_sc1(a.partial + i) : 0.0;
+    return wave_sum(v);
+}
+
+// top level over gp[0..ng) with the fixed kTopThreads shape; valid in thread 0
+template <int kThreads>
+__device__ __forceinline__ double top_sum(const double* gp, int ng)
+{
+    constexpr int kVWaves = kTopThreads / kWave;
     constexpr int kRealWaves = kThreads / kWave;
     __shared__ double wsum[kVWaves];
     const int lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
-    const int chunk = (a.nslices + kReduceThreads - 1) / kReduceThreads;
     for (int vw = w; vw < kVWaves; vw += kRealWaves) {
-        const int vt = vw * kWave + lane;
-        const int i0 = vt * chunk;
-        const int i1 = min(i0 + chunk, a.nslices);
         double v = 0.0;
-        for (int i = i0; i < i1; i += 8) {
-            double t[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) t[u] = a.partial[min(i + u, i1 - 1)];
-#pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (i + u < i1) v += t[u];
-        }
+        for (int i = vw * kWave + lane; i < ng; i += kTopThreads) v += ld_sc1(gp + i);
         v = wave_sum(v);
         if (lane == 0) wsum[vw] = v;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double s = 0.0;
+    double s = 0.0;
+    if (threadIdx.x == 0)
 #pragma unroll
         for (int i = 0; i < kVWaves; i++) s += wsum[i];
-        a.loc[which] = s;
-        if (a.nranks == 1) a.g[which] = s;
-        if (which == kRR) a.kst[0] = kfinal;
-    }
+    return s;
+}
+
+__device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which, int kfinal)
+{
+    a.loc[which] = s;
+    if (a.nranks == 1) a.g[which] = s;
+    if (which == kRR) a.kst[0] = kfinal;
 }
 
 template <int kThreads>
 __device__ __forceinline__ void complete_dot(const CgArgs& a, int s, double bs, int which, int kfinal)
 {
+    const int ng = ngroups_of(a);
+    double* gp = a.partial + a.nslices + which * ng;       // group sums of this dot
+    unsigned* gt = a.tickets + which * (ng + 1);          // group tickets, then the top one
     if (!a.fold) {
         if (threadIdx.x == 0) a.partial[s] = bs;
         return;
     }
-    __shared__ int last;
+    __shared__ int role[2];  // [0] group reducer, [1] final reducer (block-uniform)
+    const int g = s / kGroup;
     if (threadIdx.x == 0) {
-        a.partial[s] = bs;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        st_sc1(a.partial + s, bs);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(&a.tickets[which], 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        last = (t == (unsigned)a.nslices - 1u);
-        if (last) {
-            stamp(a, which == kRR ? kStampFinRR : kStampFinPAP);
+        const unsigned glen = (unsigned)min(kGroup, a.nslices - g * kGroup);
+        const unsigned t = __hip_atomic_fetch_add(gt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        role[0] = (t == glen - 1u) ? 1 : 0;
+        role[1] = 0;
+        if (role[0]) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
     }
     __syncthreads();
-    if (!last) return;
-    reduce_partials<kThreads>(a, which, kfinal);
-    if (threadIdx.x == 0) a.tickets[which] = 0u;  // re-armed for the next launch
+    if (role[0] == 0) return;  // block-uniform: the whole block leaves together
+    if (threadIdx.x < kWave) {
+        const double v = group_sum(a, g, threadIdx.x);
+        if (threadIdx.x == 0) {
+            st_sc1(gp + g, v);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(gt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+            const unsigned t = __hip_atomic_fetch_add(gt + ng, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (t == (unsigned)ng - 1u) {
+                role[1] = 1;
+                stamp(a, which == kRR ? kStampFinRR : kStampFinPAP);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+    }
+    __syncthreads();
+    if (role[1] == 0) return;
+    const double tot = top_sum<kThreads>(gp, ng);
+    if (threadIdx.x == 0) {
+        finish_dot(a, tot, which, kfinal);
+        __hip_atomic_store(gt + ng, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -620,8 +662,9 @@ __global__ __launch_bounds__(256) void k_stream_diag(CgArgs a)
     }
 }
 
-// Separate final reduction (a.fold == 0): same shape and order as the folded one.
-__global__ __launch_bounds__(kReduceThreads) void k_finalize(CgArgs a, int which, bool prologue)
+// Separate final reduction (a.fold == 0): the same two levels and order as the
+// folded completion, so fold on/off give the same bits.
+__global__ __launch_bounds__(kTopThreads) void k_finalize(CgArgs a, int which, bool prologue)
 {
     const int k = a.kst[0];
     const bool run = prologue || cg_run(a, k, false);
@@ -632,7 +675,16 @@ __global__ __launch_bounds__(kReduceThreads) void k_finalize(CgArgs a, int which
             mark_end(a);
     }
     if (!run) return;
-    reduce_partials<kReduceThreads>(a, which, prologue ? 1 : k + 1);
+    const int ng = ngroups_of(a);
+    double* gp = a.partial + a.nslices + which * ng;
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int g = threadIdx.x / kWave; g < ng; g += kTopThreads / kWave) {
+        const double v = group_sum(a, g, lane);
+        if (lane == 0) gp[g] = v;
+    }
+    __syncthreads();  // gp written by this block: visible to its own loads after the barrier
+    const double tot = top_sum<kTopThreads>(gp, ng);
+    if (threadIdx.x == 0) finish_dot(a, tot, which, prologue ? 1 : k + 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -944,7 +996,7 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kReduceThreads), 0, s, a, which, prologue);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kTopThreads), 0, s, a, which, prologue);
 }
 
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)

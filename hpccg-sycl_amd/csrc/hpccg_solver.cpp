@@ -155,7 +155,7 @@ struct hpccg_hip_matrix {
     int spmv_variant = 0;
     int use_graph = 1;
     int fuse_p = -1;  // p = r + beta p inside the SpMV: -1 auto (on for the LDS kernels only)
-    int fold = 0;    // dot finalization folded into the producing kernels (slower: see kernels)
+    int fold = 1;    // dot completion inside the producing kernels (two-level, sc1 publish)
     unsigned int* d_slice_base = nullptr;
     int* d_cols = nullptr;
     double* d_vals = nullptr;
@@ -172,6 +172,8 @@ struct hpccg_hip_matrix {
     int x_defer = 1;           // batched x update every kXDefer iterations
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_partial = nullptr;
+    unsigned int* d_tickets = nullptr;
+    int ntickets = 0;
     double* d_scal = nullptr;  // g[2], loc[2], scratch[4]
     int* d_kst = nullptr;
     double* d_hist = nullptr;
@@ -204,6 +206,7 @@ int free_matrix(hpccg_hip_matrix* M)
     if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
     void* ptrs[] = {M->d_slice_base, M->d_cols,    M->d_vals,  M->d_pbuf,  M->d_ahist,  M->d_r,
                     M->d_Ap,         M->d_x,       M->d_b,     M->d_partial,      M->d_scal,
+                    M->d_tickets,
                     M->d_kst,        M->d_hist,    M->d_stamps, M->d_ddot_partial, M->d_gen_b,
                     M->d_gen_x0,     M->d_gen_xexact, M->d_lcols, M->d_win_ptr, M->d_win_start,
                     M->d_win_len,    M->d_win_off};
@@ -260,7 +263,11 @@ int alloc_workspace(hpccg_hip_matrix* M)
         HIP_TRY(hipMalloc(v, sizeof(double) * M->npad));
         HIP_TRY(hipMemset(*v, 0, sizeof(double) * M->npad));
     }
-    HIP_TRY(hipMalloc(&M->d_partial, sizeof(double) * std::max(1, M->nslices)));
+    const int ngroups = (M->nslices + 63) / 64;  // kGroup in hpccg_kernels.hip
+    HIP_TRY(hipMalloc(&M->d_partial, sizeof(double) * (std::max(1, M->nslices) + 2 * ngroups + 8)));
+    M->ntickets = 2 * (ngroups + 1);
+    HIP_TRY(hipMalloc(&M->d_tickets, sizeof(unsigned int) * M->ntickets));
+    HIP_TRY(hipMemset(M->d_tickets, 0, sizeof(unsigned int) * M->ntickets));
     HIP_TRY(hipMalloc(&M->d_scal, sizeof(double) * 8));
     HIP_TRY(hipMemset(M->d_scal, 0, sizeof(double) * 8));
     HIP_TRY(hipMalloc(&M->d_kst, sizeof(int) * 8));  // kst[0..3] + tickets[2] (+pad)
@@ -334,7 +341,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.nring = a.xdefer ? kXDefer : (a.fuse_p ? 2 : 1);
     a.ahist = M->d_ahist;
     a.fold = M->fold ? 1 : 0;
-    a.tickets = reinterpret_cast<unsigned int*>(M->d_kst + 4);
+    a.tickets = M->d_tickets;
     a.Ap = M->d_Ap;
     a.partial = M->d_partial;
     a.g = M->d_scal;
@@ -515,7 +522,8 @@ int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_
     const int iters = std::max(0, max_iter - 1);
     const bool events = M->event_timing != 0;
     if (events) TRY(ensure_events(M, iters + 1));
-    HIP_TRY(hipMemsetAsync(M->d_kst, 0, sizeof(int) * 8, M->stream));  // state + tickets
+    HIP_TRY(hipMemsetAsync(M->d_kst, 0, sizeof(int) * 8, M->stream));  // iteration state
+    HIP_TRY(hipMemsetAsync(M->d_tickets, 0, sizeof(unsigned int) * M->ntickets, M->stream));
     TRY(enqueue_prologue(M, a, events));
     const bool graph = !events && M->use_graph && g_comm.nranks == 1 && iters >= kGraphChunk;
     int done = 0;

@@ -107,6 +107,26 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     assert all(r == results[0] for r in results)
 
 
+def test_folded_dot_completion_stress(hp, gpu):
+    """The in-kernel (fold) dot completion hands partials between workgroups on
+    different XCDs (sc1 publish + tickets). Any stale read would change a sum:
+    repeat many solves and compare every trace bitwise with the separate
+    k_finalize path (data handed over by a kernel boundary)."""
+    prob = hp.generate_matrix(64, 64, 48)  # 384 slices -> 6 groups, partial last group
+    M = hp.Matrix.from_hpc(prob)
+    M.set_option("fold", 0)
+    x = prob.x
+    hp.HPCCG(M, prob.b, x, max_iter=150)
+    ref = (M.last_trace().tobytes(), x.tobytes())
+    M.set_option("fold", 1)
+    for graph in (1, 0):
+        M.set_option("use_graph", graph)
+        for _ in range(20):
+            x = prob.x
+            hp.HPCCG(M, prob.b, x, max_iter=150)
+            assert (M.last_trace().tobytes(), x.tobytes()) == ref
+
+
 def test_waxpby_bitwise_vs_reference(hp, gpu, golden):
     import torch
     k = golden["kernels_20x20x20"]

@@ -31,10 +31,11 @@ def counters(path):
 
 def pick(agg, needle, counter):
     """Average over dispatches of the most-dispatched kernel matching needle
-    (the in-loop SpMV, not the prologue one)."""
+    (a substring or a tuple of substrings; the in-loop SpMV, not the prologue one)."""
+    needles = needle if isinstance(needle, tuple) else (needle,)
     best = None
     for (k, c), v in agg.items():
-        if needle in k and c == counter and (best is None or len(v) > len(best[1])):
+        if any(nd in k for nd in needles) and c == counter and (best is None or len(v) > len(best[1])):
             best = (k, v)
     if best is None:
         raise KeyError(needle)
@@ -61,25 +62,29 @@ def main():
     # SELL-512 uniform width 27 image of the 27-pt problem
     slots = ((nrow + 511) // 512) * 512 * 27
     nnz = (3 * n - 2) ** 3
-    stream_read = 12.0 * slots
+    stream_read = 12.0 * slots  # k_stream_diag reads the 12 B/slot SELL-512 image
     f_stream, _ = pick(fetch, "k_stream_diag", "FETCH_SIZE")
     w_stream, _ = pick(write, "k_stream_diag", "WRITE_SIZE")
     fetch_factor = stream_read / (f_stream * 1024.0)
-    f_spmv, kname = pick(fetch, "k_spmv<", "FETCH_SIZE")
-    w_spmv, _ = pick(write, "k_spmv<", "WRITE_SIZE")
+    SPMV = ("k_spmv<", "k_spmv_lds<")
+    f_spmv, kname = pick(fetch, SPMV, "FETCH_SIZE")
+    w_spmv, _ = pick(write, SPMV, "WRITE_SIZE")
     spmv_read = f_spmv * 1024.0 * fetch_factor
     spmv_write = w_spmv * 1024.0
-    fuse_p = ", true, true>" in kname  # k_spmv<rpt, w, minw, nt, fuse>
+    import re
+    targs = re.search(r"k_spmv\w*<([^>]*)>", kname).group(1).split(",")
+    fuse_p = targs[-1].strip() == "true"  # last template argument = fuse
     algo = 12.0 * nnz + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fuse_p else 0.0)
 
     avg_ns = None
     calls = -1
     for row in csv.DictReader(open(stats)):
-        if "k_spmv<" in row["Name"] and int(row["Calls"]) > calls:
+        if any(nd in row["Name"] for nd in SPMV) and int(row["Calls"]) > calls:
             avg_ns, calls = float(row["AverageNs"]), int(row["Calls"])
     out = {
         "tag": tag,
-        "problem": f"27-pt {n}^3, SELL-512 width 27 ({slots} slots, nnz {nnz})",
+        "problem": f"27-pt {n}^3, SELL-512 width 27 ({slots} slots, nnz {nnz}); "
+                   "k_spmv_lds reads the SELL-512-L image (8 B value + 2 B index per slot)",
         "kernel": kname,
         "fuse_p": fuse_p,
         "bytes_formula": "12 nnz + 20 n + 16 n" + (" + 24 n" if fuse_p else ""),
