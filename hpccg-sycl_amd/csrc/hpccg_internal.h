@@ -49,7 +49,7 @@ struct CgArgs {
     int xdefer;            // 1: x += alpha_j p_j applied every nring iterations
     double* ahist;         // [max_iter + 1]: alpha_k (for the deferred x update)
     int fuse_p;            // 1: p = r + beta p computed inside the SpMV (single rank)
-    int fold;              // 1: the last block of each producer reduces the partials
+    int fold;              // dots completed in the producing kernel: 0 none, 1 both, 2 p.Ap only, 3 r.r only
     unsigned int* tickets; // [2 x (ngroups + 1)] arrival counters (fold): groups, top
     double* Ap;
     double* partial;       // [nslices] slice partials, then 2 x ngroups group sums
@@ -71,6 +71,13 @@ struct CgArgs {
     const int* win_off;    // LDS offset (doubles)
     int lds_doubles;       // dynamic LDS per block (max staged entries over slices)
 };
+
+// Is dot `which` (kRR / kPAP) completed inside its producing kernel?
+inline __host__ __device__ bool fold_of(const CgArgs& a, int which)
+{
+    return a.fold == 1 || (a.fold == 2 && which == kPAP) || (a.fold == 3 && which == kRR);
+}
+
 
 constexpr unsigned short kLdsPad = 0xFFFF;
 constexpr int kLdsMaxDoubles = 8192;  // 64 KiB of LDS per block at most

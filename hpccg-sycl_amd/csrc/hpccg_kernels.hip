@@ -266,26 +266,17 @@ __device__ __forceinline__ double group_sum(const CgArgs& a, int g, int lane)
     return wave_sum(v);
 }
 
-// top level over gp[0..ng) with the fixed kTopThreads shape; valid in thread 0
-template <int kThreads>
-__device__ __forceinline__ double top_sum(const double* gp, int ng)
+// The same fixed shape computed by one wave (virtual waves in order); valid in lane 0.
+__device__ __forceinline__ double top_sum_wave(const double* gp, int ng, int lane)
 {
     constexpr int kVWaves = kTopThreads / kWave;
-    constexpr int kRealWaves = kThreads / kWave;
-    __shared__ double wsum[kVWaves];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int w = threadIdx.x / kWave;
-    for (int vw = w; vw < kVWaves; vw += kRealWaves) {
+    double s = 0.0;
+#pragma unroll
+    for (int vw = 0; vw < kVWaves; vw++) {
         double v = 0.0;
         for (int i = vw * kWave + lane; i < ng; i += kTopThreads) v += ld_sc1(gp + i);
-        v = wave_sum(v);
-        if (lane == 0) wsum[vw] = v;
+        s += wave_sum(v);
     }
-    __syncthreads();
-    double s = 0.0;
-    if (threadIdx.x == 0)
-#pragma unroll
-        for (int i = 0; i < kVWaves; i++) s += wsum[i];
     return s;
 }
 
@@ -296,52 +287,54 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
     if (which == kRR) a.kst[0] = kfinal;
 }
 
+// bs valid in thread 0. Only wave 0 takes part in the hand-off: the other waves
+// of the block return right away (the publish round trip then holds one wave,
+// not the block).
 template <int kThreads>
 __device__ __forceinline__ void complete_dot(const CgArgs& a, int s, double bs, int which, int kfinal)
 {
     const int ng = ngroups_of(a);
     double* gp = a.partial + a.nslices + which * ng;       // group sums of this dot
     unsigned* gt = a.tickets + which * (ng + 1);          // group tickets, then the top one
-    if (!a.fold) {
+    if (!fold_of(a, which)) {
         if (threadIdx.x == 0) a.partial[s] = bs;
         return;
     }
-    __shared__ int role[2];  // [0] group reducer, [1] final reducer (block-uniform)
+    if (threadIdx.x >= kWave) return;
+    const int lane = threadIdx.x;
     const int g = s / kGroup;
-    if (threadIdx.x == 0) {
+    int role = 0;
+    if (lane == 0) {
         st_sc1(a.partial + s, bs);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned glen = (unsigned)min(kGroup, a.nslices - g * kGroup);
         const unsigned t = __hip_atomic_fetch_add(gt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        role[0] = (t == glen - 1u) ? 1 : 0;
-        role[1] = 0;
-        if (role[0]) {
+        role = (t == glen - 1u) ? 1 : 0;
+        if (role) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
     }
-    __syncthreads();
-    if (role[0] == 0) return;  // block-uniform: the whole block leaves together
-    if (threadIdx.x < kWave) {
-        const double v = group_sum(a, g, threadIdx.x);
-        if (threadIdx.x == 0) {
-            st_sc1(gp + g, v);
+    role = __shfl(role, 0, kWave);
+    if (role == 0) return;
+    // group reducer (this wave): sc1 loads of the group's partials
+    const double v = group_sum(a, g, lane);
+    if (lane == 0) {
+        st_sc1(gp + g, v);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(gt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+        const unsigned t = __hip_atomic_fetch_add(gt + ng, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        role = (t == (unsigned)ng - 1u) ? 2 : 0;
+        if (role == 2) {
+            stamp(a, which == kRR ? kStampFinRR : kStampFinPAP);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(gt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-            const unsigned t = __hip_atomic_fetch_add(gt + ng, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-            if (t == (unsigned)ng - 1u) {
-                role[1] = 1;
-                stamp(a, which == kRR ? kStampFinRR : kStampFinPAP);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
         }
     }
-    __syncthreads();
-    if (role[1] == 0) return;
-    const double tot = top_sum<kThreads>(gp, ng);
-    if (threadIdx.x == 0) {
+    role = __shfl(role, 0, kWave);
+    if (role != 2) return;
+    const double tot = top_sum_wave(gp, ng, lane);
+    if (lane == 0) {
         finish_dot(a, tot, which, kfinal);
         __hip_atomic_store(gt + ng, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
     }
@@ -664,7 +657,9 @@ __global__ __launch_bounds__(256) void k_stream_diag(CgArgs a)
 
 // Separate final reduction (a.fold == 0): the same two levels and order as the
 // folded completion, so fold on/off give the same bits.
-__global__ __launch_bounds__(kTopThreads) void k_finalize(CgArgs a, int which, bool prologue)
+constexpr int kFinalizeThreads = 1024;
+
+__global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int which, bool prologue)
 {
     const int k = a.kst[0];
     const bool run = prologue || cg_run(a, k, false);
@@ -678,13 +673,26 @@ __global__ __launch_bounds__(kTopThreads) void k_finalize(CgArgs a, int which, b
     const int ng = ngroups_of(a);
     double* gp = a.partial + a.nslices + which * ng;
     const int lane = threadIdx.x & (kWave - 1);
-    for (int g = threadIdx.x / kWave; g < ng; g += kTopThreads / kWave) {
-        const double v = group_sum(a, g, lane);
-        if (lane == 0) gp[g] = v;
+    constexpr int kWaves = kFinalizeThreads / kWave;
+    constexpr int kBatch = 8;  // groups per wave per round, loads in flight together
+    for (int g0 = threadIdx.x / kWave; g0 < ng; g0 += kWaves * kBatch) {
+        double v[kBatch];
+#pragma unroll
+        for (int b = 0; b < kBatch; b++) {
+            const int i = (g0 + b * kWaves) * kGroup + lane;
+            v[b] = (g0 + b * kWaves < ng && i < a.nslices) ? a.partial[i] : 0.0;
+        }
+#pragma unroll
+        for (int b = 0; b < kBatch; b++) {
+            const double w = wave_sum(v[b]);
+            if (lane == 0 && g0 + b * kWaves < ng) gp[g0 + b * kWaves] = w;
+        }
     }
     __syncthreads();  // gp written by this block: visible to its own loads after the barrier
-    const double tot = top_sum<kTopThreads>(gp, ng);
-    if (threadIdx.x == 0) finish_dot(a, tot, which, prologue ? 1 : k + 1);
+    if (threadIdx.x < kWave) {
+        const double tot = top_sum_wave(gp, ng, lane);
+        if (lane == 0) finish_dot(a, tot, which, prologue ? 1 : k + 1);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -996,7 +1004,7 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kTopThreads), 0, s, a, which, prologue);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kFinalizeThreads), 0, s, a, which, prologue);
 }
 
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)

@@ -155,7 +155,7 @@ struct hpccg_hip_matrix {
     int spmv_variant = 0;
     int use_graph = 1;
     int fuse_p = -1;  // p = r + beta p inside the SpMV: -1 auto (on for the LDS kernels only)
-    int fold = 1;    // dot completion inside the producing kernels (two-level, sc1 publish)
+    int fold = 2;    // dots completed inside their producing kernel (two-level, sc1 publish): p.Ap only
     unsigned int* d_slice_base = nullptr;
     int* d_cols = nullptr;
     double* d_vals = nullptr;
@@ -340,7 +340,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.xdefer = M->x_defer ? 1 : 0;
     a.nring = a.xdefer ? kXDefer : (a.fuse_p ? 2 : 1);
     a.ahist = M->d_ahist;
-    a.fold = M->fold ? 1 : 0;
+    a.fold = (M->fold >= 0 && M->fold <= 3) ? M->fold : 0;
     a.tickets = M->d_tickets;
     a.Ap = M->d_Ap;
     a.partial = M->d_partial;
@@ -418,7 +418,7 @@ int enqueue_iteration(hpccg_hip_matrix* M, const CgArgs& a, int slot = -1, int k
     if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], s));
     launch_cg_spmv(a, M->spmv_variant, false, s);
     if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], s));
-    if (!a.fold) launch_cg_finalize(a, kPAP, false, s);
+    if (!fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, s);
     if (g_comm.nranks > 1) {
         launch_cg_stamp(a, kStampArPAP, false, s);
         TRY(enqueue_allreduce(M, a, kPAP));
@@ -426,7 +426,7 @@ int enqueue_iteration(hpccg_hip_matrix* M, const CgArgs& a, int slot = -1, int k
     if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], s));
     launch_cg_update(a, false, s);
     if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 3], s));
-    if (!a.fold) launch_cg_finalize(a, kRR, false, s);
+    if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, false, s);
     if (g_comm.nranks > 1) {
         launch_cg_stamp(a, kStampArRR, false, s);
         TRY(enqueue_allreduce(M, a, kRR));
@@ -449,7 +449,7 @@ int enqueue_prologue(hpccg_hip_matrix* M, const CgArgs& a, bool events)
     if (events) HIP_TRY(hipEventRecord(M->ev[2], s));
     launch_cg_update(a, true, s);                  // r = b - Ap (+ r.r partials)
     if (events) HIP_TRY(hipEventRecord(M->ev[3], s));
-    if (!a.fold) launch_cg_finalize(a, kRR, true, s);  // rtrans, k = 1
+    if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, true, s);  // rtrans, k = 1
     if (g_comm.nranks > 1) {
         launch_cg_stamp(a, kStampArRR, true, s);
         TRY(enqueue_allreduce(M, a, kRR));

@@ -96,6 +96,12 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)  # 119 iterations: 7 pending x updates
         assert M.get_option("fuse_p") == fuse
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    # one dot folded, the other finalized by its own kernel
+    for fold in (2, 3):
+        M.set_option("fold", fold)
+        x = prob.x
+        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
+        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # and the LDS kernels (same rows per thread), fused or not, give the same bits
     for v, fuse in itertools.product((2000, 2100), (0, 1)):
         M.set_option("spmv_variant", v)

@@ -15,7 +15,7 @@ step() {  # step <name> <seconds> <cmd...>
     return 0
 }
 step pytest_gpu 900 python -m pytest tests -m gpu -q
-step sweep 300 python tools/spmv_sweep.py
+[ -n "${SKIP_SWEEP:-}" ] || step sweep 300 python tools/spmv_sweep.py
 step bench_events 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline
 step bench_nofold 300 python bench.py --steps 5 --warmup 1 --fold 0 --no-cpu-baseline
 step bench_nofuse 300 python bench.py --steps 5 --warmup 1 --fuse-p 0 --no-cpu-baseline
@@ -23,6 +23,11 @@ step bench_7pt 300 python bench.py --n 256 --stencil 7 --steps 3 --warmup 1 --no
 step bench_7pt_nodefer 300 python bench.py --n 256 --stencil 7 --steps 3 --warmup 1 --x-defer 0 --no-cpu-baseline
 step bench_100 300 python bench.py --n 100 --steps 5 --warmup 1 --no-cpu-baseline
 step bench_100_nofold 300 python bench.py --n 100 --steps 5 --warmup 1 --fold 0 --no-cpu-baseline
+step bench_100_fold2 300 python bench.py --n 100 --steps 5 --warmup 1 --fold 2 --no-cpu-baseline
+step bench_100_fold3 300 python bench.py --n 100 --steps 5 --warmup 1 --fold 3 --no-cpu-baseline
+step bench_fold2 300 python bench.py --steps 5 --warmup 1 --fold 2 --no-cpu-baseline
+step bench_fold3 300 python bench.py --steps 5 --warmup 1 --fold 3 --no-cpu-baseline
+step bench_7pt_nofold 300 python bench.py --n 256 --stencil 7 --steps 3 --warmup 1 --fold 0 --no-cpu-baseline
 step cli_100 120 hpccg-sycl_amd/bin/test_HPCCG 100 100 100
 HPCCG_DEVICE_GENERATE=1 step cli_200dev 120 hpccg-sycl_amd/bin/test_HPCCG 200 200 200
 step cli_10 60 hpccg-sycl_amd/bin/test_HPCCG 10 10 10
