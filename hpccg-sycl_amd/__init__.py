@@ -102,6 +102,11 @@ def lib() -> C.CDLL:
         "hpccg_sell_build": (lp, [ip, lp, lp, vp, vp, vp, vp, vp, vp]),
         "hpccg_halo_plan": (ip, [ip, ip, ip, vp, vp, PI]),
         "hpccg_slab_plan": (ip, [ip, ip, PI, PI]),
+        "hpccg_hip_group_generate": (ip, [ip, ip, ip, ip, ip, PI, C.POINTER(vp)]),
+        "hpccg_hip_group_create_csr": (ip, [ip, PI, PI, PI, ip, C.POINTER(vp), C.POINTER(vp),
+                                            C.POINTER(vp), C.POINTER(vp)]),
+        "hpccg_hip_group_solve": (ip, [C.POINTER(vp), ip, C.POINTER(vp), C.POINTER(vp), ip, dp, PI,
+                                       PD, PD]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -298,6 +303,57 @@ def HPCCG(M: Matrix, b, x, max_iter: int = 500, tolerance: float = 0.0, print_re
         rc = L.hpccg_hip_solve(M.h, bb.ctypes.data, x.ctypes.data, max_iter, tolerance,
                                C.byref(it), C.byref(nr), tp, int(print_residuals))
     _check(rc, "HPCCG")
+    return rc, it.value, nr.value, times
+
+
+# ---------------------------------------------------------------------------
+# in-process rank group: the z-slab ranks of one job driven by one thread
+# ---------------------------------------------------------------------------
+def _ints(v):
+    return None if v is None else (C.c_int * len(v))(*[int(d) for d in v])
+
+
+def group_generate(nx, ny, nz, nranks, use_7pt=False, devices=None) -> list:
+    """Rank r of an nranks z-slab job (generate_matrix.cpp:225-229) for every r,
+    generated on devices[r] (default: the current device for all)."""
+    out = (C.c_void_p * nranks)()
+    _check(lib().hpccg_hip_group_generate(nx, ny, nz, int(use_7pt), nranks, _ints(devices), out),
+           "group_generate")
+    return [Matrix(C.c_void_p(out[r])) for r in range(nranks)]
+
+
+def group_from_csr(parts, total_nrow, devices=None) -> list:
+    """parts[r] = (row_ptr, cols, vals, start_row) of rank r (global columns)."""
+    P = len(parts)
+    keep = []
+    rps, cls, vls = (C.c_void_p * P)(), (C.c_void_p * P)(), (C.c_void_p * P)()
+    for r, (rp, cols, vals, _) in enumerate(parts):
+        rp = np.ascontiguousarray(rp, np.int64)
+        cols = np.ascontiguousarray(cols, np.int32)
+        vals = np.ascontiguousarray(vals, np.float64)
+        keep += [rp, cols, vals]
+        rps[r], cls[r], vls[r] = rp.ctypes.data, cols.ctypes.data, vals.ctypes.data
+    nrow = _ints([len(p[0]) - 1 for p in parts])
+    start = _ints([p[3] for p in parts])
+    out = (C.c_void_p * P)()
+    _check(lib().hpccg_hip_group_create_csr(P, _ints(devices), nrow, start, total_nrow, rps, cls, vls,
+                                            out), "group_from_csr")
+    return [Matrix(C.c_void_p(out[r])) for r in range(P)]
+
+
+def group_HPCCG(Ms: list, bs, xs, max_iter: int = 500, tolerance: float = 0.0):
+    """HPCCG() over an in-process group; bs[r], xs[r]: rank r's device vectors
+    (xs updated in place). Returns (ierr, niters, normr, times)."""
+    P = len(Ms)
+    hs = (C.c_void_p * P)(*[M.h for M in Ms])
+    bp = (C.c_void_p * P)(*[_ptr(b) for b in bs])
+    xp = (C.c_void_p * P)(*[_ptr(x) for x in xs])
+    it = C.c_int(0)
+    nr = C.c_double(0.0)
+    times = np.zeros(7, np.float64)
+    rc = lib().hpccg_hip_group_solve(hs, P, bp, xp, max_iter, tolerance, C.byref(it), C.byref(nr),
+                                     times.ctypes.data_as(C.POINTER(C.c_double)))
+    _check(rc, "group_HPCCG")
     return rc, it.value, nr.value, times
 
 

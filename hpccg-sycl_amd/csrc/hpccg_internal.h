@@ -96,6 +96,17 @@ void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);
 void launch_cg_end(const CgArgs& a, hipStream_t s);
 void launch_cg_xflush(const CgArgs& a, hipStream_t s);  // pending deferred x updates
 
+// In-process rank group all-reduce of one CG scalar: g[which] of every rank =
+// sum of loc[which] over ranks, in rank order.
+constexpr int kMaxGroupRanks = 16;
+struct GroupSum {
+    int nranks;
+    int which;
+    const double* loc[kMaxGroupRanks];
+    double* g[kMaxGroupRanks];
+};
+void launch_group_sum(const GroupSum& gs, hipStream_t s);
+
 // Kernel-level ops on arbitrary device pointers.
 void launch_waxpby(int n, double alpha, const double* x, double beta, const double* y, double* w,
                    hipStream_t s);

@@ -1025,6 +1025,18 @@ void launch_cg_end(const CgArgs& a, hipStream_t s)
     hipLaunchKernelGGL(k_end, dim3(1), dim3(64), 0, s, a);
 }
 
+__global__ void k_group_sum(GroupSum gs)
+{
+    double v = 0.0;
+    for (int r = 0; r < gs.nranks; r++) v += gs.loc[r][gs.which];
+    for (int r = 0; r < gs.nranks; r++) gs.g[r][gs.which] = v;
+}
+
+void launch_group_sum(const GroupSum& gs, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(1), 0, s, gs);
+}
+
 void launch_cg_xflush(const CgArgs& a, hipStream_t s)
 {
     if (a.xdefer) hipLaunchKernelGGL(k_xflush<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);

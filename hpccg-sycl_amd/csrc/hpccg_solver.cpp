@@ -76,6 +76,16 @@ struct Comm {
 };
 Comm g_comm;
 
+// In-process rank group (hpccg_hip_group_*): while a group member is being
+// created on this thread, rank/size come from here instead of the RCCL
+// communicator, and the halo plan is made by hpccg_hip_group_* afterwards.
+struct GroupCtx {
+    int active = 0, nranks = 1, rank = 0;
+};
+thread_local GroupCtx g_group_ctx;
+int comm_nranks() { return g_group_ctx.active ? g_group_ctx.nranks : g_comm.nranks; }
+int comm_rank() { return g_group_ctx.active ? g_group_ctx.rank : g_comm.rank; }
+
 // ---------------------------------------------------------------------------
 // SELL-512 build from any row accessor. Entry order per row is preserved.
 // ---------------------------------------------------------------------------
@@ -145,6 +155,8 @@ long long sell_build_impl(int nrow, long long col_base, long long ncol_ext, RowL
 // ---------------------------------------------------------------------------
 struct hpccg_hip_matrix {
     int device = 0;
+    int rank = 0, nranks = 1;  // z-slab rank of this matrix (RCCL communicator or in-process group)
+    int in_group = 0;          // 1: halo / all-reduce by hpccg_hip_group_solve, not RCCL
     int nrow = 0, start_row = 0, total_nrow = 0;
     int ghost_lo = 0, ghost_hi = 0;
     // what neighbours need from us (filled by the collective plan exchange)
@@ -224,6 +236,12 @@ int free_matrix(hpccg_hip_matrix* M)
 int exchange_plan(hpccg_hip_matrix* M)
 {
     M->send_lo = M->send_hi = 0;
+    M->rank = comm_rank();
+    M->nranks = comm_nranks();
+    if (g_group_ctx.active) {  // in-process group: planned when every member exists
+        M->in_group = 1;
+        return 0;
+    }
     if (g_comm.nranks == 1) {
         if (M->ghost_lo || M->ghost_hi)
             return set_err(HPCCG_HIP_EPLAN, "columns outside the local rows on a single rank");
@@ -315,7 +333,7 @@ int choose_variant(const hpccg_hip_matrix* M)
 // the SELL-512-L kernels, which compute p_k once per staged window entry.
 bool fuse_p_effective(const hpccg_hip_matrix* M)
 {
-    if (g_comm.nranks != 1 || M->spmv_variant == 9999) return false;
+    if (M->nranks != 1 || M->spmv_variant == 9999) return false;
     if (M->fuse_p < 0) return M->spmv_variant >= 2000;
     return M->fuse_p != 0;
 }
@@ -329,7 +347,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.grid = M->grid;
     a.max_iter = max_iter;
     a.tol = tol;
-    a.nranks = g_comm.nranks;
+    a.nranks = M->nranks;
     a.ghost_lo = M->ghost_lo;
     a.b = b;
     a.x = x;
@@ -401,59 +419,158 @@ int ensure_events(hpccg_hip_matrix* M, int slots)
 }
 
 // p_k's ring buffer (local rows), as the kernels' cur_p computes it.
+// p_k's ring buffer (local rows), as the kernels' cur_p computes it.
 double* ring_p(const CgArgs& a, int k) { return a.p + (size_t)(k % a.nring) * (size_t)a.pstride; }
 
-// One CG iteration k (HPCCG.cpp:358-386), fully device resident. slot >= 0:
-// bracket the SpMV and the fused update with that slot's hipEvents. k_host is
-// the iteration the host enqueues (used only to address the halo buffer on
-// multi-rank runs, which launch eagerly).
-int enqueue_iteration(hpccg_hip_matrix* M, const CgArgs& a, int slot = -1, int k_host = 1)
+// The ranks one host thread enqueues: one matrix (a process of an RCCL job, or
+// a single GPU), or every member of an in-process group (hpccg_hip_group_*).
+struct Ranks {
+    hpccg_hip_matrix* const* M;
+    const CgArgs* a;
+    int P;
+    hipEvent_t* ev;  // group: P "ready" events + 1 "reduced" event
+};
+
+int use_device(const Ranks& R, int r)
 {
-    hipStream_t s = M->stream;
-    if (!a.fuse_p) launch_cg_p_update(a, s);
-    if (g_comm.nranks > 1) {
-        launch_cg_stamp(a, kStampHalo, false, s);
-        TRY(enqueue_halo(M, ring_p(a, k_host)));
+    if (R.P > 1) HIP_TRY(hipSetDevice(R.M[r]->device));
+    return 0;
+}
+
+// In-process halo: rank r's ghost planes are copied from its neighbours' p_k
+// rows once their streams have produced them (the same rows enqueue_halo moves
+// with RCCL). Rank r-1 cannot overwrite p_k's ring slot before the copy: its
+// next write there comes after at least one all-reduce, which waits for rank
+// r's update kernel, which follows rank r's SpMV on the same stream.
+int group_halo(const Ranks& R, int k_host, bool prologue)
+{
+    for (int r = 0; r < R.P; r++) {
+        TRY(use_device(R, r));
+        HIP_TRY(hipEventRecord(R.ev[r], R.M[r]->stream));
     }
-    if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], s));
-    launch_cg_spmv(a, M->spmv_variant, false, s);
-    if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], s));
-    if (!fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, s);
-    if (g_comm.nranks > 1) {
-        launch_cg_stamp(a, kStampArPAP, false, s);
-        TRY(enqueue_allreduce(M, a, kPAP));
+    auto p_of = [&](int r) { return prologue ? R.a[r].p : ring_p(R.a[r], k_host); };
+    for (int r = 0; r < R.P; r++) {
+        hpccg_hip_matrix* M = R.M[r];
+        TRY(use_device(R, r));
+        if (r > 0 && M->ghost_lo) {
+            const hpccg_hip_matrix* L = R.M[r - 1];
+            HIP_TRY(hipStreamWaitEvent(M->stream, R.ev[r - 1], 0));
+            HIP_TRY(hipMemcpyPeerAsync(p_of(r) - M->ghost_lo, M->device, p_of(r - 1) + L->nrow - M->ghost_lo,
+                                       L->device, sizeof(double) * M->ghost_lo, M->stream));
+        }
+        if (r < R.P - 1 && M->ghost_hi) {
+            const hpccg_hip_matrix* U = R.M[r + 1];
+            HIP_TRY(hipStreamWaitEvent(M->stream, R.ev[r + 1], 0));
+            HIP_TRY(hipMemcpyPeerAsync(p_of(r) + M->nrow, M->device, p_of(r + 1), U->device,
+                                       sizeof(double) * M->ghost_hi, M->stream));
+        }
     }
-    if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], s));
-    launch_cg_update(a, false, s);
-    if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 3], s));
-    if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, false, s);
-    if (g_comm.nranks > 1) {
-        launch_cg_stamp(a, kStampArRR, false, s);
-        TRY(enqueue_allreduce(M, a, kRR));
+    return 0;
+}
+
+// In-process all-reduce of loc[which]: one lane on rank 0's stream adds the
+// ranks' values in rank order and writes g[which] of every rank.
+int group_allreduce(const Ranks& R, int which)
+{
+    GroupSum gs;
+    std::memset(&gs, 0, sizeof gs);
+    gs.nranks = R.P;
+    gs.which = which;
+    for (int r = 0; r < R.P; r++) {
+        gs.loc[r] = R.a[r].loc;
+        gs.g[r] = R.a[r].g;
+        TRY(use_device(R, r));
+        HIP_TRY(hipEventRecord(R.ev[r], R.M[r]->stream));
     }
+    TRY(use_device(R, 0));
+    for (int r = 1; r < R.P; r++) HIP_TRY(hipStreamWaitEvent(R.M[0]->stream, R.ev[r], 0));
+    launch_group_sum(gs, R.M[0]->stream);
+    HIP_TRY(hipEventRecord(R.ev[R.P], R.M[0]->stream));
+    for (int r = 1; r < R.P; r++) {
+        TRY(use_device(R, r));
+        HIP_TRY(hipStreamWaitEvent(R.M[r]->stream, R.ev[R.P], 0));
+    }
+    return 0;
+}
+
+int exch_halo(const Ranks& R, int k_host, bool prologue)
+{
+    for (int r = 0; r < R.P; r++) {
+        TRY(use_device(R, r));
+        launch_cg_stamp(R.a[r], kStampHalo, prologue, R.M[r]->stream);
+    }
+    if (R.P > 1) return group_halo(R, k_host, prologue);
+    return enqueue_halo(R.M[0], prologue ? R.a[0].p : ring_p(R.a[0], k_host));
+}
+
+int exch_allreduce(const Ranks& R, int which, bool prologue)
+{
+    for (int r = 0; r < R.P; r++) {
+        TRY(use_device(R, r));
+        launch_cg_stamp(R.a[r], which == kRR ? kStampArRR : kStampArPAP, prologue, R.M[r]->stream);
+    }
+    if (R.P > 1) return group_allreduce(R, which);
+    return enqueue_allreduce(R.M[0], R.a[0], which);
+}
+
+// One CG iteration k (HPCCG.cpp:358-386), fully device resident, for every
+// rank of R. slot >= 0 (single matrix): bracket the SpMV and the fused update
+// with that slot's hipEvents. k_host is the iteration being enqueued: it
+// addresses p_k's ring slot for the halo.
+int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
+{
+    const bool multi = R.a[0].nranks > 1;
+    for (int r = 0; r < R.P; r++) {
+        TRY(use_device(R, r));
+        if (!R.a[r].fuse_p) launch_cg_p_update(R.a[r], R.M[r]->stream);
+    }
+    if (multi) TRY(exch_halo(R, k_host, false));
+    for (int r = 0; r < R.P; r++) {
+        hpccg_hip_matrix* M = R.M[r];
+        const CgArgs& a = R.a[r];
+        TRY(use_device(R, r));
+        if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
+        launch_cg_spmv(a, M->spmv_variant, false, M->stream);
+        if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
+        if (!fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
+    }
+    if (multi) TRY(exch_allreduce(R, kPAP, false));
+    for (int r = 0; r < R.P; r++) {
+        hpccg_hip_matrix* M = R.M[r];
+        const CgArgs& a = R.a[r];
+        TRY(use_device(R, r));
+        if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], M->stream));
+        launch_cg_update(a, false, M->stream);
+        if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 3], M->stream));
+        if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, false, M->stream);
+    }
+    if (multi) TRY(exch_allreduce(R, kRR, false));
     HIP_TRY(hipGetLastError());
     return 0;
 }
 
-int enqueue_prologue(hpccg_hip_matrix* M, const CgArgs& a, bool events)
+int enqueue_prologue(const Ranks& R, bool events)
 {
-    hipStream_t s = M->stream;
-    launch_cg_prologue_copy(a, s);  // p = x
-    if (g_comm.nranks > 1) {
-        launch_cg_stamp(a, kStampHalo, true, s);
-        TRY(enqueue_halo(M, a.p));
+    const bool multi = R.a[0].nranks > 1;
+    for (int r = 0; r < R.P; r++) {
+        TRY(use_device(R, r));
+        launch_cg_prologue_copy(R.a[r], R.M[r]->stream);  // p = x
     }
-    if (events) HIP_TRY(hipEventRecord(M->ev[0], s));
-    launch_cg_spmv(a, M->spmv_variant, true, s);  // Ap = A p
-    if (events) HIP_TRY(hipEventRecord(M->ev[1], s));
-    if (events) HIP_TRY(hipEventRecord(M->ev[2], s));
-    launch_cg_update(a, true, s);                  // r = b - Ap (+ r.r partials)
-    if (events) HIP_TRY(hipEventRecord(M->ev[3], s));
-    if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, true, s);  // rtrans, k = 1
-    if (g_comm.nranks > 1) {
-        launch_cg_stamp(a, kStampArRR, true, s);
-        TRY(enqueue_allreduce(M, a, kRR));
+    if (multi) TRY(exch_halo(R, 0, true));
+    for (int r = 0; r < R.P; r++) {
+        hpccg_hip_matrix* M = R.M[r];
+        const CgArgs& a = R.a[r];
+        hipStream_t s = M->stream;
+        TRY(use_device(R, r));
+        if (events) HIP_TRY(hipEventRecord(M->ev[0], s));
+        launch_cg_spmv(a, M->spmv_variant, true, s);  // Ap = A p
+        if (events) HIP_TRY(hipEventRecord(M->ev[1], s));
+        if (events) HIP_TRY(hipEventRecord(M->ev[2], s));
+        launch_cg_update(a, true, s);                  // r = b - Ap (+ r.r partials)
+        if (events) HIP_TRY(hipEventRecord(M->ev[3], s));
+        if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, true, s);  // rtrans, k = 1
     }
+    if (multi) TRY(exch_allreduce(R, kRR, true));
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -470,7 +587,8 @@ int build_graph(hpccg_hip_matrix* M, const CgArgs& a)
     hipGraph_t g = nullptr;
     HIP_TRY(hipStreamBeginCapture(M->stream, hipStreamCaptureModeThreadLocal));
     int rc = 0;
-    for (int i = 0; i < kGraphChunk && rc == 0; i++) rc = enqueue_iteration(M, a);
+    const Ranks R{&M, &a, 1, nullptr};
+    for (int i = 0; i < kGraphChunk && rc == 0; i++) rc = enqueue_iteration(R, -1, i + 1);
     hipError_t e = hipStreamEndCapture(M->stream, &g);
     if (rc) return rc;
     if (e != hipSuccess) return set_err(HPCCG_HIP_EHIP, "graph capture failed: %s", hipGetErrorString(e));
@@ -512,20 +630,44 @@ void stamps_to_times(const std::vector<unsigned long long>& st, int count, doubl
     times[5] = t5;
 }
 
-int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_iter, double tol,
-               int* niters_out, double* normr_out, double* times, int print)
+// Solve on the ranks Ms[0..P) (P > 1: an in-process group; P == 1: this
+// process's matrix, exchanging through RCCL when the communicator has peers).
+int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, double* const* x_dev,
+                int max_iter, double tol, int* niters_out, double* normr_out, double* times, int print)
 {
-    HIP_TRY(hipSetDevice(M->device));
-    TRY(ensure_hist(M, max_iter));
-    const auto t_begin = std::chrono::steady_clock::now();
-    CgArgs a = make_args(M, b_dev, x_dev, max_iter, tol);
+    hpccg_hip_matrix* M = Ms[0];
+    std::vector<CgArgs> av(P);
+    std::vector<hipEvent_t> gev;
+    struct EvFree {
+        std::vector<hipEvent_t>& v;
+        ~EvFree() { for (hipEvent_t e : v) (void)hipEventDestroy(e); }
+    } ev_free{gev};
     const int iters = std::max(0, max_iter - 1);
-    const bool events = M->event_timing != 0;
+    const bool events = P == 1 && M->event_timing != 0;
+    for (int r = 0; r < P; r++) {
+        HIP_TRY(hipSetDevice(Ms[r]->device));
+        TRY(ensure_hist(Ms[r], max_iter));
+    }
+    if (P > 1) {
+        gev.resize(P + 1);
+        for (int r = 0; r <= P; r++) {
+            HIP_TRY(hipSetDevice(Ms[r < P ? r : 0]->device));
+            HIP_TRY(hipEventCreateWithFlags(&gev[r], hipEventDisableTiming));
+        }
+    }
+    HIP_TRY(hipSetDevice(M->device));
+    const auto t_begin = std::chrono::steady_clock::now();
+    for (int r = 0; r < P; r++) {
+        HIP_TRY(hipSetDevice(Ms[r]->device));
+        av[r] = make_args(Ms[r], b_dev[r], x_dev[r], max_iter, tol);
+        HIP_TRY(hipMemsetAsync(Ms[r]->d_kst, 0, sizeof(int) * 8, Ms[r]->stream));  // iteration state
+        HIP_TRY(hipMemsetAsync(Ms[r]->d_tickets, 0, sizeof(unsigned int) * Ms[r]->ntickets, Ms[r]->stream));
+    }
+    const CgArgs& a = av[0];
+    const Ranks R{Ms, av.data(), P, gev.data()};
     if (events) TRY(ensure_events(M, iters + 1));
-    HIP_TRY(hipMemsetAsync(M->d_kst, 0, sizeof(int) * 8, M->stream));  // iteration state
-    HIP_TRY(hipMemsetAsync(M->d_tickets, 0, sizeof(unsigned int) * M->ntickets, M->stream));
-    TRY(enqueue_prologue(M, a, events));
-    const bool graph = !events && M->use_graph && g_comm.nranks == 1 && iters >= kGraphChunk;
+    TRY(enqueue_prologue(R, events));
+    const bool graph = P == 1 && !events && M->use_graph && M->nranks == 1 && iters >= kGraphChunk;
     int done = 0;
     if (graph) {
         // kernel arguments are baked into the graph: rebuild only when they change
@@ -538,10 +680,14 @@ int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_
         for (; done + kGraphChunk <= iters; done += kGraphChunk)
             HIP_TRY(hipGraphLaunch(M->graph_exec, M->stream));
     }
-    for (; done < iters; done++) TRY(enqueue_iteration(M, a, events ? done + 1 : -1, done + 1));
-    launch_cg_end(a, M->stream);
-    launch_cg_xflush(a, M->stream);  // x += alpha_j p_j still pending (x_defer)
-    HIP_TRY(hipGetLastError());
+    for (; done < iters; done++) TRY(enqueue_iteration(R, events ? done + 1 : -1, done + 1));
+    for (int r = P - 1; r >= 0; r--) {
+        TRY(use_device(R, r));
+        launch_cg_end(av[r], Ms[r]->stream);
+        launch_cg_xflush(av[r], Ms[r]->stream);  // x += alpha_j p_j still pending (x_defer)
+        HIP_TRY(hipGetLastError());
+        if (r > 0) HIP_TRY(hipStreamSynchronize(Ms[r]->stream));
+    }
     // results
     int kst[4];
     HIP_TRY(hipMemcpyAsync(kst, M->d_kst, sizeof kst, hipMemcpyDeviceToHost, M->stream));
@@ -563,6 +709,10 @@ int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_
     M->trace[0] = std::sqrt(niters > 0 ? hist[0] : scal[kRR]);
     for (int k = 1; k <= niters; k++) M->trace[k] = std::sqrt(hist[k - 1]);
     M->last_niters = niters;
+    for (int r = 1; r < P; r++) {  // every group member reports the same solve
+        Ms[r]->trace = M->trace;
+        Ms[r]->last_niters = niters;
+    }
     const double normr = M->trace[niters];
     if (events) {
         double sp = 0, up = 0;
@@ -578,7 +728,7 @@ int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_
         M->ktimes[2] = up;
         M->ktimes[3] = niters + 1;
     }
-    if (print && g_comm.rank == 0) {
+    if (print && M->rank == 0) {
         int pf = max_iter / 10;
         if (pf > 50) pf = 50;
         if (pf < 1) pf = 1;
@@ -594,6 +744,14 @@ int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_
     *niters_out = niters;
     *normr_out = normr;
     return 0;
+}
+
+int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_iter, double tol,
+               int* niters_out, double* normr_out, double* times, int print)
+{
+    HIP_TRY(hipSetDevice(M->device));
+    if (M->in_group) return set_err(HPCCG_HIP_EINVAL, "group member: solve with hpccg_hip_group_solve");
+    return solve_ranks(&M, 1, &b_dev, &x_dev, max_iter, tol, niters_out, normr_out, times, print);
 }
 
 // ---------------------------------------------------------------------------
@@ -847,6 +1005,76 @@ std::map<const void*, hpccg_hip_matrix*> g_dropin_cache;
 
 }  // namespace
 
+// ---- in-process rank group -------------------------------------------------
+namespace {
+
+template <class Make>
+int group_make(int nranks, const int* devices, hpccg_hip_matrix** out, Make make)
+{
+    if (!out) return set_err(HPCCG_HIP_EINVAL, "out is NULL");
+    if (nranks < 1 || nranks > kMaxGroupRanks)
+        return set_err(HPCCG_HIP_EINVAL, "group size must be 1..%d", kMaxGroupRanks);
+    if (g_comm.nranks > 1) return set_err(HPCCG_HIP_EINVAL, "in-process group inside an RCCL job");
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    for (int r = 0; r < nranks; r++) out[r] = nullptr;
+    int rc = 0;
+    for (int r = 0; r < nranks && rc == 0; r++) {
+        const int dev = devices ? devices[r] : cur;
+        if (hipSetDevice(dev) != hipSuccess) {
+            rc = set_err(HPCCG_HIP_EHIP, "hipSetDevice(%d) failed", dev);
+            break;
+        }
+        g_group_ctx = GroupCtx{1, nranks, r};
+        rc = make(r, &out[r]);
+        g_group_ctx = GroupCtx();
+    }
+    // halo plan from every member's {nrow, ghost_lo, ghost_hi, start_row}
+    std::vector<int> info(4 * nranks);
+    for (int r = 0; r < nranks && rc == 0; r++) {
+        const hpccg_hip_matrix* M = out[r];
+        int mine[4] = {M->nrow, M->ghost_lo, M->ghost_hi, M->start_row};
+        std::memcpy(&info[4 * r], mine, sizeof mine);
+    }
+    for (int r = 0; r < nranks && rc == 0; r++) {
+        int sends[2];
+        rc = hpccg_slab_plan(nranks, r, info.data(), sends);
+        if (rc == 0) {
+            out[r]->send_lo = sends[0];
+            out[r]->send_hi = sends[1];
+        }
+    }
+    // peer access between the members' distinct devices
+    for (int r = 0; r < nranks && rc == 0; r++)
+        for (int q = 0; q < nranks; q++) {
+            if (out[r]->device == out[q]->device) continue;
+            int can = 0;
+            (void)hipDeviceCanAccessPeer(&can, out[r]->device, out[q]->device);
+            if (!can) {
+                rc = set_err(HPCCG_HIP_EHIP, "device %d cannot access device %d", out[r]->device,
+                             out[q]->device);
+                break;
+            }
+            (void)hipSetDevice(out[r]->device);
+            const hipError_t e = hipDeviceEnablePeerAccess(out[q]->device, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+                rc = set_err(HPCCG_HIP_EHIP, "hipDeviceEnablePeerAccess: %s", hipGetErrorString(e));
+                break;
+            }
+            (void)hipGetLastError();
+        }
+    (void)hipSetDevice(cur);
+    if (rc) {
+        for (int r = 0; r < nranks; r++) {
+            free_matrix(out[r]);
+            out[r] = nullptr;
+        }
+    }
+    return rc;
+}
+
+}  // namespace
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -969,8 +1197,8 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
 {
     if (nx < 1 || ny < 1 || nz < 1) return set_err(HPCCG_HIP_EINVAL, "nx, ny, nz must be >= 1");
     const long long n64 = (long long)nx * ny * nz;
-    if (n64 * g_comm.nranks >= (1LL << 31)) return set_err(HPCCG_HIP_EINVAL, "global rows exceed int32");
-    const int n = (int)n64, rank = g_comm.rank, size = g_comm.nranks;
+    if (n64 * comm_nranks() >= (1LL << 31)) return set_err(HPCCG_HIP_EINVAL, "global rows exceed int32");
+    const int n = (int)n64, rank = comm_rank(), size = comm_nranks();
     auto* M = new hpccg_hip_matrix();
     HIP_TRY(hipGetDevice(&M->device));
     M->nrow = n;
@@ -1057,6 +1285,43 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     }
     *out = M;
     return 0;
+}
+
+
+int hpccg_hip_group_generate(int nx, int ny, int nz, int use_7pt, int nranks, const int* devices,
+                             hpccg_hip_matrix** out)
+{
+    return group_make(nranks, devices, out, [&](int, hpccg_hip_matrix** m) {
+        return hpccg_hip_matrix_generate(nx, ny, nz, use_7pt, m);
+    });
+}
+
+int hpccg_hip_group_create_csr(int nranks, const int* devices, const int* nrow, const int* start_row,
+                               int total_nrow, const long long* const* row_ptr, const int* const* cols,
+                               const double* const* vals, hpccg_hip_matrix** out)
+{
+    if (!nrow || !start_row || !row_ptr || !cols || !vals) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    return group_make(nranks, devices, out, [&](int r, hpccg_hip_matrix** m) {
+        return hpccg_hip_matrix_create_csr(nrow[r], start_row[r], total_nrow, row_ptr[r], cols[r], vals[r], m);
+    });
+}
+
+int hpccg_hip_group_solve(hpccg_hip_matrix* const* Ms, int nranks, const double* const* b_dev,
+                          double* const* x_dev, int max_iter, double tolerance, int* niters, double* normr,
+                          double* times)
+{
+    if (!Ms || !b_dev || !x_dev || !niters || !normr || nranks < 1 || nranks > kMaxGroupRanks)
+        return set_err(HPCCG_HIP_EINVAL, "bad argument");
+    for (int r = 0; r < nranks; r++) {
+        if (!Ms[r] || !b_dev[r] || !x_dev[r]) return set_err(HPCCG_HIP_EINVAL, "NULL member %d", r);
+        if (Ms[r]->nranks != nranks || Ms[r]->rank != r || (nranks > 1 && !Ms[r]->in_group))
+            return set_err(HPCCG_HIP_EINVAL, "member %d is not rank %d of a %d-rank group", r, r, nranks);
+    }
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    const int rc = solve_ranks(Ms, nranks, b_dev, x_dev, max_iter, tolerance, niters, normr, times, 0);
+    (void)hipSetDevice(cur);
+    return rc;
 }
 
 int hpccg_hip_matrix_destroy(hpccg_hip_matrix* M) { return free_matrix(M); }

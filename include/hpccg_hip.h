@@ -106,8 +106,10 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  * on for nranks == 1), "spmv_variant" (SpMV kernel, see hpccg_kernels.hip),
  * "event_timing" (1 = bracket every SpMV and fused-update launch with
  * hipEvents on the solver stream; eager launches), "fuse_p" (1 = compute
- * p = r + beta*p inside the SpMV; single rank only), "fold" (1 = the last
- * block of each producing kernel completes the dot product). None of them
+ * p = r + beta*p inside the SpMV; single rank only), "fold" (the last
+ * block of the producing kernel completes a dot product: 0 neither, 1 both,
+ * 2 p.Ap only (default), 3 r.r only), "x_defer" (1 = x += alpha p batched
+ * every 8 iterations, default). None of them
  * changes a computed value: fuse_p/fold on and off are bitwise equal. */
 int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value);
 int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* value);
@@ -118,6 +120,29 @@ int hpccg_hip_kernel_times(const hpccg_hip_matrix* M, double out[4]);
 /* Diagnostic: average duration (hipEvents, solver stream) of `reps`
  * back-to-back launches of SpMV variant `variant` on the resident p. */
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_us);
+
+/* ---- in-process rank group --------------------------------------------------
+ * The z-slab decomposition of one process's RCCL job (make_local_matrix.cpp
+ * :58-610 + exchange_externals.cpp:51-131 + the MPI_Allreduce in ddot.cpp),
+ * driven from ONE host thread: member r is rank r of nranks (devices[r], or
+ * the current device for all when devices is NULL; several ranks may share a
+ * device). Halo planes move by peer copies between the members' streams and
+ * the two CG scalars are summed in rank order by one lane on rank 0's
+ * device. The kernels are the multi-rank ones an RCCL job runs; only the
+ * transport differs. nranks <= 16. Not inside an RCCL job (nranks > 1 there). */
+int hpccg_hip_group_generate(int nx, int ny, int nz, int use_7pt, int nranks, const int* devices,
+                             hpccg_hip_matrix** out);
+/* Member r from CSR rows [start_row[r], start_row[r] + nrow[r]) of the global
+ * matrix (global columns, z-slab halo only; HPCCG_HIP_EPLAN otherwise). */
+int hpccg_hip_group_create_csr(int nranks, const int* devices, const int* nrow, const int* start_row,
+                               int total_nrow, const long long* const* row_ptr, const int* const* cols,
+                               const double* const* vals, hpccg_hip_matrix** out);
+/* HPCCG() over the group: b_dev[r], x_dev[r] are rank r's local rows on its
+ * device (x in/out). niters, normr and times (rank 0's stamps) as
+ * hpccg_hip_solve_device; every member's hpccg_hip_last_trace is set. */
+int hpccg_hip_group_solve(hpccg_hip_matrix* const* Ms, int nranks, const double* const* b_dev,
+                          double* const* x_dev, int max_iter, double tolerance, int* niters, double* normr,
+                          double* times);
 
 /* ---- kernel level, device pointers, synchronous ----------------------------
  * hpccg_hip_sparsemv: HPC_sparsemv.cpp:68-89. x_dev has the local rows (the

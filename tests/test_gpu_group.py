@@ -1,0 +1,115 @@
+"""Multi-rank kernels on the GPU: the in-process rank group.
+
+RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so a 1-GPU box
+cannot run the RCCL job itself. hpccg_hip_group_* drives the same z-slab
+ranks from one thread instead: every member is built and solved by the
+multi-rank code path (ghost-localised columns, LDS windows over the ghost
+planes, the allreduced scalars in g, cg_run on all-reduced values), and only
+the transport differs (peer copies of the ghost planes, a rank-ordered sum for
+the two scalars). The oracle is the serial reference run of the z-stacked
+global problem (SURVEY 4 "Multi-GPU oracle"; golden cases *_xNranks,
+generate_matrix.cpp:225-229), tolerance RTRANS_RTOL_MULTI."""
+import numpy as np
+import pytest
+
+from conftest import RTRANS_RTOL_MULTI, check_final, check_trace, solve_case, unhex
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve_group(hp, Ms, max_iter=500, tol=0.0, bs=None):
+    import torch
+    xs = [torch.zeros(M.info()["nrow"], dtype=torch.float64, device="cuda:0") for M in Ms]
+    if bs is None:
+        bs = [M.vectors()[0] for M in Ms]
+    ierr, niters, normr, times = hp.group_HPCCG(Ms, bs, xs, max_iter=max_iter, tolerance=tol)
+    return niters, normr, [x.cpu().numpy() for x in xs], times
+
+
+@pytest.mark.parametrize("name", ["27pt_16x16x16_x8ranks", "27pt_8x8x8_x2ranks",
+                                  "7pt_12x10x8_x2ranks"])
+def test_group_matches_global_reference(hp, gpu, golden, name):
+    c = solve_case(golden, name)
+    P = c["ranks"]
+    Ms = hp.group_generate(c["nx"], c["ny"], c["nz"], P, use_7pt=c["use_7pt"])
+    nxy = c["nx"] * c["ny"]
+    for r, M in enumerate(Ms):
+        inf = M.info()
+        assert inf["ghost_lo"] == (nxy if r > 0 else 0)
+        assert inf["ghost_hi"] == (nxy if r < P - 1 else 0)
+    niters, normr, xs, times = _solve_group(hp, Ms)
+    ref_tr = [unhex(t) for t in c["trace_normr"]]
+    rr = c["runs"]["500"]
+    tr = Ms[0].last_trace()
+    for M in Ms[1:]:
+        assert np.array_equal(M.last_trace(), tr)  # one set of all-reduced scalars
+    assert tr[0] == ref_tr[0]
+    assert check_trace(tr, ref_tr, RTRANS_RTOL_MULTI) >= 5
+    check_final(niters, normr, tr, rr["niters"], unhex(rr["normr"]), ref_tr, 500)
+    assert max(np.max(np.abs(x - 1.0)) for x in xs) <= 1e-12
+    assert times[5] > 0.0 and times[4] > 0.0  # halo and all-reduce classes were stamped
+
+
+def test_group_kernel_variants_bitwise(hp, gpu):
+    """Multi-rank SpMV kernels (plain SELL-512, NT, LDS-staged windows that
+    include the ghost planes) and the dot completion modes give the same bits."""
+    Ms = hp.group_generate(24, 20, 9, 3)
+    ref = None
+    for v in (1000, 0, 2000, 2100):
+        for fold in (0, 1, 2):
+            for M in Ms:
+                M.set_option("spmv_variant", v)
+                M.set_option("fold", fold)
+            niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
+            got = (niters, normr, Ms[0].last_trace().tobytes(), b"".join(x.tobytes() for x in xs))
+            if ref is None:
+                ref = got
+            assert got == ref, (v, fold)
+    assert Ms[0].get_option("lds_doubles") > 0
+
+
+def test_group_from_host_csr_equals_device_generator(hp, gpu):
+    """Host generate_matrix per rank (global columns) -> group_from_csr: same
+    SELL image, same solve bits as the device generator."""
+    nx, ny, nz, P = 10, 9, 7, 3
+    parts = []
+    for r in range(P):
+        prob = hp.generate_matrix(nx, ny, nz, rank=r, size=P)
+        rp, cols, vals = prob.to_csr()
+        parts.append((rp, cols, vals, r * nx * ny * nz))
+    Mh = hp.group_from_csr(parts, P * nx * ny * nz)
+    Md = hp.group_generate(nx, ny, nz, P)
+    for a, b in zip(Mh, Md):
+        assert a.info() == b.info()
+    bs = [M.vectors()[0] for M in Md]  # device generator's b == generate_matrix's b
+    r1 = _solve_group(hp, Mh, max_iter=100, bs=bs)
+    r2 = _solve_group(hp, Md, max_iter=100)
+    assert r1[0] == r2[0] and r1[1] == r2[1]
+    assert Mh[0].last_trace().tobytes() == Md[0].last_trace().tobytes()
+    assert all(np.array_equal(a, b) for a, b in zip(r1[2], r2[2]))
+
+
+def test_group_of_one_equals_single_rank(hp, gpu):
+    (Mg,) = hp.group_generate(12, 11, 10, 1)
+    niters, normr, xs, _ = _solve_group(hp, [Mg], max_iter=120)
+    M = hp.Matrix.generate(12, 11, 10)
+    import torch
+    b, _, _ = M.vectors()
+    x = torch.zeros(12 * 11 * 10, dtype=torch.float64, device="cuda:0")
+    _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=120, device=True)
+    assert (it, nr) == (niters, normr)
+    assert M.last_trace().tobytes() == Mg.last_trace().tobytes()
+    assert np.array_equal(x.cpu().numpy(), xs[0])
+
+
+def test_group_errors(hp, gpu):
+    Ms = hp.group_generate(6, 6, 4, 2)
+    import torch
+    b, _, _ = Ms[0].vectors()
+    x = torch.zeros(144, dtype=torch.float64, device="cuda:0")
+    with pytest.raises(hp.HPCCGError, match="group"):
+        hp.HPCCG(Ms[0], b, x, max_iter=10, device=True)  # a member alone
+    with pytest.raises(hp.HPCCGError):
+        hp.group_HPCCG(Ms[::-1], [b, b], [x, x], max_iter=10)  # wrong rank order
+    with pytest.raises(hp.HPCCGError):
+        hp.group_generate(6, 6, 4, 17)  # more than 16 ranks
