@@ -386,6 +386,23 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_p_update(CgArgs a)
     st_rows<kRpt>(cur_p(a, k), row, a.n, o);
 }
 
+// Multi-rank with the p update fused into the SpMV: the rows the neighbours
+// need (the first nlo and last nhi local rows) are updated first, by this
+// kernel, so the halo can move p_k before the SpMV computes the rest. Same
+// expression as k_p_update; the SpMV later stores the same bits there again.
+__global__ __launch_bounds__(256) void k_p_boundary(CgArgs a, int nlo, int nhi)
+{
+    const int k = a.kst[0];
+    if (!cg_run(a, k, true)) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nlo + nhi) return;
+    const int row = i < nlo ? i : a.n - nhi + (i - nlo);
+    const double beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+    const double rv = a.r[row];
+    const double yv = (k == 1) ? rv : cur_p(a, k - 1)[row];
+    cur_p(a, k)[row] = rv + beta * yv;
+}
+
 // ---------------------------------------------------------------------------
 // SpMV over SELL-512 (HPC_sparsemv.cpp:68-89) + fused p.Ap slice partial
 // (ddot.cpp:60-73), optionally + the p update (waxpby, HPCCG.cpp:362/369).
@@ -554,8 +571,8 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     if (s >= a.nslices) return;
     double* __restrict__ p = cur_p(a, k);
     const double* __restrict__ xext = p - a.ghost_lo;
-    // stage the windows; with kFuse the staged value is p_k = r + beta*p_{k-1},
-    // the exact expression k_p_update stores (single rank: ghost_lo = 0)
+    // stage the windows; with kFuse the staged value of an own row is
+    // p_k = r + beta*p_{k-1}, the exact expression k_p_update stores
     double beta = 0.0;
     const double* __restrict__ pold = a.r;
     if constexpr (kFuse) {
@@ -566,10 +583,13 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     for (int w = w0; w < w1; w++) {
         const int st0 = a.win_start[w], len = a.win_len[w], off = a.win_off[w];
         for (int i = threadIdx.x; i < len; i += kSliceRows / kRpt) {
-            if constexpr (kFuse)
-                xs[off + i] = a.r[st0 + i] + beta * pold[st0 + i];
-            else
+            if constexpr (kFuse) {
+                // own rows: p_k computed here; ghost planes: p_k from the halo
+                const int l = st0 + i - a.ghost_lo;
+                xs[off + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + beta * pold[l] : xext[st0 + i];
+            } else {
                 xs[off + i] = xext[st0 + i];
+            }
         }
     }
     __syncthreads();
@@ -932,6 +952,12 @@ void launch_cg_prologue_copy(const CgArgs& a, hipStream_t s)
 void launch_cg_p_update(const CgArgs& a, hipStream_t s)
 {
     hipLaunchKernelGGL(k_p_update<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
+}
+
+void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
+{
+    if (nlo + nhi <= 0) return;
+    hipLaunchKernelGGL(k_p_boundary, dim3((nlo + nhi + 255) / 256), dim3(256), 0, s, a, nlo, nhi);
 }
 
 // SpMV variants. All compute every row bitwise identically; the p.Ap

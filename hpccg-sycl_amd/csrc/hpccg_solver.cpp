@@ -331,9 +331,12 @@ int choose_variant(const hpccg_hip_matrix* M)
 // fuse_p (single rank): measured slower in the plain SELL-512 kernels, where it
 // doubles every gather (561 -> 744 us at 200^3), so "auto" enables it only for
 // the SELL-512-L kernels, which compute p_k once per staged window entry.
+// Multi-rank: only the SELL-512-L kernels, which stage ghost planes from the
+// halo and compute own rows (the halo rows first, by k_p_boundary).
 bool fuse_p_effective(const hpccg_hip_matrix* M)
 {
-    if (M->nranks != 1 || M->spmv_variant == 9999) return false;
+    if (M->spmv_variant == 9999) return false;
+    if (M->nranks != 1 && M->spmv_variant < 2000) return false;
     if (M->fuse_p < 0) return M->spmv_variant >= 2000;
     return M->fuse_p != 0;
 }
@@ -522,7 +525,10 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
     const bool multi = R.a[0].nranks > 1;
     for (int r = 0; r < R.P; r++) {
         TRY(use_device(R, r));
-        if (!R.a[r].fuse_p) launch_cg_p_update(R.a[r], R.M[r]->stream);
+        if (!R.a[r].fuse_p)
+            launch_cg_p_update(R.a[r], R.M[r]->stream);
+        else if (multi)
+            launch_cg_p_boundary(R.a[r], R.M[r]->send_lo, R.M[r]->send_hi, R.M[r]->stream);
     }
     if (multi) TRY(exch_halo(R, k_host, false));
     for (int r = 0; r < R.P; r++) {

@@ -106,7 +106,8 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  * on for nranks == 1), "spmv_variant" (SpMV kernel, see hpccg_kernels.hip),
  * "event_timing" (1 = bracket every SpMV and fused-update launch with
  * hipEvents on the solver stream; eager launches), "fuse_p" (1 = compute
- * p = r + beta*p inside the SpMV; single rank only), "fold" (the last
+ * p = r + beta*p inside the SpMV; default on for the SELL-512-L kernels,
+ * multi-rank only with those: the halo rows are updated first), "fold" (the last
  * block of the producing kernel completes a dot product: 0 neither, 1 both,
  * 2 p.Ap only (default), 3 r.r only), "x_defer" (1 = x += alpha p batched
  * every 8 iterations, default). None of them

@@ -52,19 +52,25 @@ def test_group_matches_global_reference(hp, gpu, golden, name):
 
 def test_group_kernel_variants_bitwise(hp, gpu):
     """Multi-rank SpMV kernels (plain SELL-512, NT, LDS-staged windows that
-    include the ghost planes) and the dot completion modes give the same bits."""
+    include the ghost planes), the p update fused into the LDS SpMV (halo rows
+    by k_p_boundary first), the dot completion modes and the deferred x update
+    give the same bits."""
     Ms = hp.group_generate(24, 20, 9, 3)
     ref = None
-    for v in (1000, 0, 2000, 2100):
-        for fold in (0, 1, 2):
-            for M in Ms:
-                M.set_option("spmv_variant", v)
-                M.set_option("fold", fold)
-            niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
-            got = (niters, normr, Ms[0].last_trace().tobytes(), b"".join(x.tobytes() for x in xs))
-            if ref is None:
-                ref = got
-            assert got == ref, (v, fold)
+    import itertools
+    for v, fold, fuse, defer in itertools.product((1000, 0, 2000, 2100), (0, 1, 2), (0, 1), (0, 1)):
+        for M in Ms:
+            M.set_option("spmv_variant", v)
+            M.set_option("fold", fold)
+            M.set_option("fuse_p", fuse)
+            M.set_option("x_defer", defer)
+        # p = r + beta p inside the SpMV: LDS kernels only on multiple ranks
+        assert Ms[1].get_option("fuse_p") == (fuse if v >= 2000 else 0)
+        niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
+        got = (niters, normr, Ms[0].last_trace().tobytes(), b"".join(x.tobytes() for x in xs))
+        if ref is None:
+            ref = got
+        assert got == ref, (v, fold, fuse, defer)
     assert Ms[0].get_option("lds_doubles") > 0
 
 
