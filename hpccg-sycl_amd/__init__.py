@@ -393,6 +393,15 @@ def comm_init(uid: bytes, nranks: int, rank: int) -> None:
     _check(lib().hpccg_hip_comm_init(uid, nranks, rank), "comm_init")
 
 
+def comm_allreduce_host(vals, op: str = "sum") -> np.ndarray:
+    """All-reduce a few host doubles over the RCCL communicator (sum/min/max)."""
+    a = np.ascontiguousarray(vals, np.float64).copy()
+    _check(lib().hpccg_hip_comm_allreduce_host(a.ctypes.data_as(C.POINTER(C.c_double)), len(a),
+                                               {"sum": 0, "min": 1, "max": 2}[op]),
+           "comm_allreduce_host")
+    return a
+
+
 def comm_destroy() -> None:
     lib().hpccg_hip_comm_destroy()
 

@@ -1121,7 +1121,8 @@ int hpccg_hip_comm_init(const unsigned char id[128], int nranks, int rank)
         ncclCommDestroy(g_comm.comm);
         g_comm = Comm();
     }
-    if (nranks == 1) return 0;
+    // a 1-rank communicator is created too (bootstrap + RCCL check on one GPU);
+    // the solver still takes its single-rank path when nranks == 1
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
     NCCL_TRY(ncclCommInitRank(&g_comm.comm, nranks, uid, rank));
@@ -1147,7 +1148,7 @@ int hpccg_hip_comm_size(int* nranks, int* rank)
 int hpccg_hip_comm_allreduce_host(double* vals, int n, int op)
 {
     if (!vals || n < 0 || op < 0 || op > 2) return set_err(HPCCG_HIP_EINVAL, "bad argument");
-    if (g_comm.nranks == 1 || n == 0) return 0;
+    if (!g_comm.comm || n == 0) return 0;
     double* d = nullptr;
     hipStream_t s = nullptr;
     HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamDefault));
