@@ -34,10 +34,37 @@ __device__ __forceinline__ int xcd_slice(int grid)
     return (b % kNumXcd) * per + (b / kNumXcd);
 }
 
+// Lane l < off receives lane l + off (gfx950 lane moves, no LDS traffic):
+// permlane32/16_swap for the cross-row steps, DPP row_shl inside a row.
+template <int kOff>
+__device__ __forceinline__ double from_lane_plus(double v)
+{
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    int rlo, rhi;
+    if constexpr (kOff == 32) {
+        rlo = __builtin_amdgcn_permlane32_swap(lo, lo, false, false)[1];
+        rhi = __builtin_amdgcn_permlane32_swap(hi, hi, false, false)[1];
+    } else if constexpr (kOff == 16) {
+        rlo = __builtin_amdgcn_permlane16_swap(lo, lo, false, false)[1];
+        rhi = __builtin_amdgcn_permlane16_swap(hi, hi, false, false)[1];
+    } else {
+        static_assert(kOff >= 1 && kOff <= 8, "row_shl range");
+        rlo = __builtin_amdgcn_update_dpp(0, lo, 0x100 + kOff, 0xF, 0xF, false);
+        rhi = __builtin_amdgcn_update_dpp(0, hi, 0x100 + kOff, 0xF, 0xF, false);
+    }
+    return __hiloint2double(rhi, rlo);
+}
+
+// Wave sum, result valid in LANE 0 only. Fixed tree: the butterfly's lane 0,
+// v_l += v_{l+off} for off = 32, 16, 8, 4, 2, 1 (lanes >= off are don't-care).
 __device__ __forceinline__ double wave_sum(double v)
 {
-#pragma unroll
-    for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    v += from_lane_plus<32>(v);
+    v += from_lane_plus<16>(v);
+    v += from_lane_plus<8>(v);
+    v += from_lane_plus<4>(v);
+    v += from_lane_plus<2>(v);
+    v += from_lane_plus<1>(v);
     return v;
 }
 
@@ -266,17 +293,29 @@ __device__ __forceinline__ double group_sum(const CgArgs& a, int g, int lane)
     return wave_sum(v);
 }
 
-// The same fixed shape computed by one wave (virtual waves in order); valid in lane 0.
-__device__ __forceinline__ double top_sum_wave(const double* gp, int ng, int lane)
+// The same fixed shape computed by one wave (virtual waves in order); valid in
+// lane 0. ld(i) reads group sum i. All loads are issued before the sums.
+template <class Ld>
+__device__ __forceinline__ double top_sum_wave(Ld ld, int ng, int lane)
 {
     constexpr int kVWaves = kTopThreads / kWave;
+    double v[kVWaves];
+#pragma unroll
+    for (int vw = 0; vw < kVWaves; vw++) v[vw] = 0.0;
+    for (int i0 = 0; i0 < ng; i0 += kTopThreads) {
+        double t[kVWaves];
+#pragma unroll
+        for (int vw = 0; vw < kVWaves; vw++) {
+            const int i = i0 + vw * kWave + lane;
+            t[vw] = i < ng ? ld(i) : 0.0;
+        }
+#pragma unroll
+        for (int vw = 0; vw < kVWaves; vw++)
+            if (i0 + vw * kWave < ng) v[vw] += t[vw];
+    }
     double s = 0.0;
 #pragma unroll
-    for (int vw = 0; vw < kVWaves; vw++) {
-        double v = 0.0;
-        for (int i = vw * kWave + lane; i < ng; i += kTopThreads) v += ld_sc1(gp + i);
-        s += wave_sum(v);
-    }
+    for (int vw = 0; vw < kVWaves; vw++) s += wave_sum(v[vw]);
     return s;
 }
 
@@ -333,7 +372,7 @@ __device__ __forceinline__ void complete_dot(const CgArgs& a, int s, double bs, 
     }
     role = __shfl(role, 0, kWave);
     if (role != 2) return;
-    const double tot = top_sum_wave(gp, ng, lane);
+    const double tot = top_sum_wave([gp](int i) { return ld_sc1(gp + i); }, ng, lane);
     if (lane == 0) {
         finish_dot(a, tot, which, kfinal);
         __hip_atomic_store(gt + ng, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
@@ -678,9 +717,11 @@ __global__ __launch_bounds__(256) void k_stream_diag(CgArgs a)
 // Separate final reduction (a.fold == 0): the same two levels and order as the
 // folded completion, so fold on/off give the same bits.
 constexpr int kFinalizeThreads = 1024;
+constexpr int kFinLdsGroups = 4096;  // group sums kept in LDS up to 2M slices
 
 __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int which, bool prologue)
 {
+    __shared__ double gs[kFinLdsGroups];
     const int k = a.kst[0];
     const bool run = prologue || cg_run(a, k, false);
     if (threadIdx.x == 0) {
@@ -691,10 +732,11 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
     }
     if (!run) return;
     const int ng = ngroups_of(a);
+    const bool in_lds = ng <= kFinLdsGroups;
     double* gp = a.partial + a.nslices + which * ng;
     const int lane = threadIdx.x & (kWave - 1);
     constexpr int kWaves = kFinalizeThreads / kWave;
-    constexpr int kBatch = 8;  // groups per wave per round, loads in flight together
+    constexpr int kBatch = 16;  // groups per wave per round, loads in flight together
     for (int g0 = threadIdx.x / kWave; g0 < ng; g0 += kWaves * kBatch) {
         double v[kBatch];
 #pragma unroll
@@ -705,12 +747,19 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
 #pragma unroll
         for (int b = 0; b < kBatch; b++) {
             const double w = wave_sum(v[b]);
-            if (lane == 0 && g0 + b * kWaves < ng) gp[g0 + b * kWaves] = w;
+            const int g = g0 + b * kWaves;
+            if (lane == 0 && g < ng) {
+                if (in_lds)
+                    gs[g] = w;
+                else
+                    gp[g] = w;
+            }
         }
     }
-    __syncthreads();  // gp written by this block: visible to its own loads after the barrier
+    __syncthreads();  // group sums written by this block
     if (threadIdx.x < kWave) {
-        const double tot = top_sum_wave(gp, ng, lane);
+        const double tot = in_lds ? top_sum_wave([&](int i) { return gs[i]; }, ng, lane)
+                                  : top_sum_wave([gp](int i) { return gp[i]; }, ng, lane);
         if (lane == 0) finish_dot(a, tot, which, prologue ? 1 : k + 1);
     }
 }

@@ -5,7 +5,8 @@
 # calibrate them. Stops at the first crash/timeout; no retries.
 set -u
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+N=${N:-200}
+OUT=gpurun_out/prof_$N
 mkdir -p $OUT
 step() {
     local name=$1 secs=$2; shift 2
@@ -15,7 +16,7 @@ step() {
     case $rc in 124|134|137|139) echo "fatal in $name, stopping"; exit $rc;; esac
     return 0
 }
-N=${N:-200}
+
 step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --steps 2 --warmup 1 --no-cpu-baseline
 step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python tools/pmc_workload.py --n $N
 step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python tools/pmc_workload.py --n $N

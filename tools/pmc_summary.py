@@ -101,6 +101,17 @@ def main():
         "rocprof_avg_spmv_ns": avg_ns,
         "rocprof_spmv_GBs": algo / avg_ns if avg_ns else None,
     }
+    # every kernel of the pmc workload: corrected HBM bytes per launch
+    per_kernel = {}
+    for (k, c), v in fetch.items():
+        if c != "FETCH_SIZE":
+            continue
+        short = re.sub(r"^void |hpccg::\(anonymous namespace\)::|\(.*$", "", k)
+        wv = write.get((k, "WRITE_SIZE"), [0.0])
+        per_kernel[short] = {"launches": len(v),
+                             "read_bytes": round(sum(v) / len(v) * 1024.0 * fetch_factor),
+                             "write_bytes": round(sum(wv) / len(wv) * 1024.0)}
+    out["per_kernel_hbm_bytes_per_launch"] = per_kernel
     if bench_log and os.path.exists(bench_log):
         lines = [l for l in open(bench_log) if l.startswith("{")]
         if lines:
