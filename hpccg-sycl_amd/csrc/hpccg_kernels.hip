@@ -589,7 +589,9 @@ __device__ __forceinline__ void ld_lcols(const unsigned short* __restrict__ p, u
     }
 }
 
-template <int kRpt, bool kNT, bool kFuse>
+// kPre > 0: the first kPre slots of the matrix stream are loaded before the
+// window staging and its barrier, so the block's HBM stream starts at once.
+template <int kRpt, bool kNT, bool kFuse, int kPre>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool prologue)
 {
     extern __shared__ __attribute__((aligned(16))) double xs[];
@@ -610,6 +612,20 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     if (s >= a.nslices) return;
     double* __restrict__ p = cur_p(a, k);
     const double* __restrict__ xext = p - a.ghost_lo;
+    const size_t base = (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
+    const int wdt = (int)(a.slice_base[s + 1] - a.slice_base[s]);
+    const double* __restrict__ vp = a.vals + base;
+    const unsigned short* __restrict__ cp = a.lcols + base;
+    constexpr int kP = kPre > 0 ? kPre : 1;
+    unsigned cpre[kP][kRpt];
+    Rows<kRpt> vpre[kP];
+#pragma unroll
+    for (int j = 0; j < kPre; j++) {
+        if (j < wdt) {
+            ld_lcols<kRpt, kNT>(cp + (size_t)j * kSliceRows, cpre[j]);
+            vpre[j] = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+        }
+    }
     // stage the windows; with kFuse the staged value of an own row is
     // p_k = r + beta*p_{k-1}, the exact expression k_p_update stores
     double beta = 0.0;
@@ -632,15 +648,21 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
         }
     }
     __syncthreads();
-    const size_t base = (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
-    const int wdt = (int)(a.slice_base[s + 1] - a.slice_base[s]);
-    const double* __restrict__ vp = a.vals + base;
-    const unsigned short* __restrict__ cp = a.lcols + base;
     double sum[kRpt];
 #pragma unroll
     for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < kPre; j++) {
+        if (j < wdt) {
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) {
+                const double xv = (cpre[j][i] != kLdsPad) ? xs[cpre[j][i]] : 0.0;
+                sum[i] = sum[i] + vpre[j].v[i] * xv;
+            }
+        }
+    }
 #pragma unroll 3
-    for (int j = 0; j < wdt; j++) {
+    for (int j = kPre; j < wdt; j++) {
         unsigned c[kRpt];
         ld_lcols<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
         const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
@@ -1030,14 +1052,14 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
             hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, false>), dim3(a.grid),                    \
                                dim3(kSliceRows / RPT), 0, s, a, prologue);                          \
     } while (0)
-#define HPCCG_SPMV_LDS(RPT, NT)                                                                    \
+#define HPCCG_SPMV_LDS(RPT, NT, PRE)                                                               \
     do {                                                                                           \
         const size_t smem = (size_t)a.lds_doubles * sizeof(double);                                \
         if (a.fuse_p && !prologue)                                                                 \
-            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, true>), dim3(a.grid), dim3(kSliceRows / RPT), smem, \
-                               s, a, prologue);                                                    \
+            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, true, PRE>), dim3(a.grid), dim3(kSliceRows / RPT), \
+                               smem, s, a, prologue);                                              \
         else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, false>), dim3(a.grid), dim3(kSliceRows / RPT), \
+            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, false, PRE>), dim3(a.grid), dim3(kSliceRows / RPT), \
                                smem, s, a, prologue);                                              \
     } while (0)
 bool spmv_variant_ok(int v)
@@ -1045,7 +1067,7 @@ bool spmv_variant_ok(int v)
     switch (v) {
     case 0: case 1: case 2: case 27: case 7: case 327: case 427:
     case 1000: case 1001: case 1002: case 1027: case 1007: case 9999:
-    case 2000: case 2001: case 2002: case 2100:
+    case 2000: case 2001: case 2002: case 2100: case 2200: case 2208: case 2300: case 2308:
         return true;
     default:
         return false;
@@ -1067,10 +1089,14 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 1027: HPCCG_SPMV(2, 27, 1, true); break;
     case 1007: HPCCG_SPMV(2, 7, 1, true); break;
     case 9999: hipLaunchKernelGGL(k_stream_diag<27>, dim3(a.grid), dim3(256), 0, s, a); break;
-    case 2000: HPCCG_SPMV_LDS(2, true); break;
-    case 2001: HPCCG_SPMV_LDS(1, true); break;
-    case 2002: HPCCG_SPMV_LDS(4, true); break;
-    case 2100: HPCCG_SPMV_LDS(2, false); break;
+    case 2000: HPCCG_SPMV_LDS(2, true, 0); break;
+    case 2001: HPCCG_SPMV_LDS(1, true, 0); break;
+    case 2002: HPCCG_SPMV_LDS(4, true, 0); break;
+    case 2100: HPCCG_SPMV_LDS(2, false, 0); break;
+    case 2200: HPCCG_SPMV_LDS(2, true, 4); break;
+    case 2208: HPCCG_SPMV_LDS(2, true, 8); break;
+    case 2300: HPCCG_SPMV_LDS(2, false, 4); break;
+    case 2308: HPCCG_SPMV_LDS(2, false, 8); break;
     default: HPCCG_SPMV(2, 0, 1, false); break;
     }
 }

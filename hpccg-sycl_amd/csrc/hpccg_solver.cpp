@@ -167,7 +167,7 @@ struct hpccg_hip_matrix {
     int spmv_variant = 0;
     int use_graph = 1;
     int fuse_p = -1;  // p = r + beta p inside the SpMV: -1 auto (on for the LDS kernels only)
-    int fold = 2;    // dots completed inside their producing kernel (two-level, sc1 publish): p.Ap only
+    int fold = -1;   // dots completed inside their producing kernel (two-level, sc1 publish); -1 auto
     unsigned int* d_slice_base = nullptr;
     int* d_cols = nullptr;
     double* d_vals = nullptr;
@@ -317,14 +317,15 @@ int ensure_hist(hpccg_hip_matrix* M, int max_iter)
 // 5.4 staged doubles vs 26.7 entries per row -> 1.33x faster; 7-pt: 6 vs 7 ->
 // 1.14x slower), non-temporal matrix loads once the image outgrows the 256 MB
 // Infinity Cache (>= 128^3: nt 5-12 % faster; <= 100^3: default policy 2-20 %
-// faster).
+// faster). The LDS kernels prefetch 4 matrix slots ahead of the window staging
+// barrier (2200/2300; in-CG 200^3: 409-415 vs 420-441 us per SpMV, 100^3 even).
 int choose_variant(const hpccg_hip_matrix* M)
 {
     const double rows = std::max(1, M->nrow);
     const bool lds = M->has_lds && (double)M->nnz / rows >= 2.5 * M->lds_doubles / (double)kSliceRows;
     const double image = (double)M->nslots * (lds ? 10.0 : 12.0);
     const bool big = image > 300e6;
-    if (lds) return big ? 2000 : 2100;
+    if (lds) return big ? 2200 : 2300;
     return big ? 1000 : 0;
 }
 
@@ -339,6 +340,17 @@ bool fuse_p_effective(const hpccg_hip_matrix* M)
     if (M->nranks != 1 && M->spmv_variant < 2000) return false;
     if (M->fuse_p < 0) return M->spmv_variant >= 2000;
     return M->fuse_p != 0;
+}
+
+// fold auto (measured, profiles/r01_final_*): completing p.Ap inside the SpMV
+// saves the k_finalize launch (~7 us incl. its boundary) but holds each
+// block's LDS for the publish round trip. 100^3 (1954 slices): 13062 vs 12475
+// it/s; 200^3 (15625 slices): 1943 vs 1954. r.r in the update kernel: slower
+// at both (every block of a short kernel waits for its ticket).
+int fold_effective(const hpccg_hip_matrix* M)
+{
+    if (M->fold >= 0 && M->fold <= 3) return M->fold;
+    return M->nslices <= 8192 ? 2 : 0;
 }
 
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
@@ -361,7 +373,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.xdefer = M->x_defer ? 1 : 0;
     a.nring = a.xdefer ? kXDefer : (a.fuse_p ? 2 : 1);
     a.ahist = M->d_ahist;
-    a.fold = (M->fold >= 0 && M->fold <= 3) ? M->fold : 0;
+    a.fold = fold_effective(M);
     a.tickets = M->d_tickets;
     a.Ap = M->d_Ap;
     a.partial = M->d_partial;
@@ -1458,7 +1470,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "spmv_variant")) *value = M->spmv_variant;
     else if (!std::strcmp(key, "event_timing")) *value = M->event_timing;
     else if (!std::strcmp(key, "fuse_p")) *value = fuse_p_effective(M) ? 1 : 0;
-    else if (!std::strcmp(key, "fold")) *value = M->fold;
+    else if (!std::strcmp(key, "fold")) *value = fold_effective(M);
     else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_lds ? M->lds_doubles : 0;
     else if (!std::strcmp(key, "windows")) *value = M->nwin;

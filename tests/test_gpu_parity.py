@@ -53,7 +53,7 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 1000, 1001, 1002, 1027, 2000, 2001,
-                                     2002, 2100])
+                                     2002, 2100, 2200, 2208, 2300, 2308])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
@@ -103,7 +103,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # and the LDS kernels (same rows per thread), fused or not, give the same bits
-    for v, fuse in itertools.product((2000, 2100), (0, 1)):
+    for v, fuse in itertools.product((2000, 2100, 2200, 2308), (0, 1)):
         M.set_option("spmv_variant", v)
         M.set_option("fuse_p", fuse)
         assert M.get_option("fuse_p") == fuse

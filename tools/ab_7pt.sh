@@ -1,0 +1,6 @@
+export TMPDIR=/tmp; mkdir -p gpurun_out; : > gpurun_out/pre.jsonl
+run() { timeout -k 10 300 python bench.py "$@" --no-cpu-baseline > gpurun_out/pre_one.log 2>&1 || exit $?; echo "$* $(tail -n1 gpurun_out/pre_one.log)" >> gpurun_out/pre.jsonl; }
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pt.log 2>&1 || exit $?
+for v in 1000 2000 2200 1000 2200; do run --n 256 --stencil 7 --steps 3 --variant $v; done
+run --n 256 --stencil 7 --steps 3 --variant 1000 --fuse-p 1
+run --n 256 --stencil 7 --steps 3 --variant 2200 --fuse-p 0
