@@ -34,6 +34,16 @@ __device__ __forceinline__ int xcd_slice(int grid)
     return (b % kNumXcd) * per + (b / kNumXcd);
 }
 
+// Same XCD ownership, each XCD's slices in reverse order: a kernel that follows
+// a forward sweep starts on the rows its predecessor wrote last (still in the
+// XCD's L2 / the Infinity Cache).
+__device__ __forceinline__ int xcd_slice_rev(int grid)
+{
+    const int b = blockIdx.x;
+    const int per = grid / kNumXcd;
+    return (b % kNumXcd) * per + (per - 1 - b / kNumXcd);
+}
+
 // Lane l < off receives lane l + off (gfx950 lane moves, no LDS traffic):
 // permlane32/16_swap for the cross-row steps, DPP row_shl inside a row.
 template <int kOff>
@@ -808,7 +818,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
         }
         if (!run) return;
     }
-    const int s = xcd_slice(a.grid);
+    const int s = a.rev ? xcd_slice_rev(a.grid) : xcd_slice(a.grid);
     if (s >= a.nslices) return;
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     const Rows<kRpt> apv = ld<kRpt>(a.Ap + row);

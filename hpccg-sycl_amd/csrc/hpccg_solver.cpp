@@ -182,6 +182,7 @@ struct hpccg_hip_matrix {
     long long pstride = 0;     // doubles between ring buffers
     double* d_ahist = nullptr;
     int x_defer = 1;           // batched x update every kXDefer iterations
+    int rev_update = 1;        // update kernel walks slices backwards (reads the SpMV's latest writes first)
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_partial = nullptr;
     unsigned int* d_tickets = nullptr;
@@ -371,6 +372,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.pstride = M->pstride;
     a.fuse_p = fuse_p_effective(M) ? 1 : 0;
     a.xdefer = M->x_defer ? 1 : 0;
+    a.rev = M->rev_update ? 1 : 0;
     a.nring = a.xdefer ? kXDefer : (a.fuse_p ? 2 : 1);
     a.ahist = M->d_ahist;
     a.fold = fold_effective(M);
@@ -1379,6 +1381,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->fuse_p = (int)value;
     } else if (!std::strcmp(key, "x_defer")) {
         M->x_defer = (int)value;
+    } else if (!std::strcmp(key, "rev_update")) {
+        M->rev_update = (int)value;
     } else if (!std::strcmp(key, "fold")) {
         M->fold = (int)value;
     } else if (!std::strcmp(key, "spmv_variant")) {
@@ -1472,6 +1476,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "fuse_p")) *value = fuse_p_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "fold")) *value = fold_effective(M);
     else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
+    else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_lds ? M->lds_doubles : 0;
     else if (!std::strcmp(key, "windows")) *value = M->nwin;
     else return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);

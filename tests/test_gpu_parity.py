@@ -92,6 +92,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         M.set_option("fold", fold)
         M.set_option("use_graph", graph)
         M.set_option("x_defer", defer)
+        M.set_option("rev_update", (fuse + fold + defer) % 2)  # slice order: no value changes
         x = prob.x
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)  # 119 iterations: 7 pending x updates
         assert M.get_option("fuse_p") == fuse
