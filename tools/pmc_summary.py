@@ -73,7 +73,8 @@ def main():
     spmv_write = w_spmv * 1024.0
     import re
     targs = re.search(r"k_spmv\w*<([^>]*)>", kname).group(1).split(",")
-    fuse_p = targs[-1].strip() == "true"  # last template argument = fuse
+    # k_spmv<kRpt, kW, kMinW, kNT, kFuse>, k_spmv_lds<kRpt, kNT, kFuse, kPre>
+    fuse_p = (targs[2] if "k_spmv_lds" in kname else targs[-1]).strip() == "true"
     algo = 12.0 * nnz + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fuse_p else 0.0)
 
     avg_ns = None
