@@ -103,6 +103,9 @@ def lib() -> C.CDLL:
         "hpccg_halo_plan": (ip, [ip, ip, ip, vp, vp, PI]),
         "hpccg_slab_plan": (ip, [ip, ip, PI, PI]),
         "hpccg_hip_group_generate": (ip, [ip, ip, ip, ip, ip, PI, C.POINTER(vp)]),
+        "hpccg_hip_set_halo_mode": (ip, [ip]),
+        "hpccg_read_HPC_row": (ip, [C.c_char_p, ip, ip, C.POINTER(C.POINTER(_HPCMatrix)),
+                                    C.POINTER(PD), C.POINTER(PD), C.POINTER(PD)]),
         "hpccg_hip_group_create_csr": (ip, [ip, PI, PI, PI, ip, C.POINTER(vp), C.POINTER(vp),
                                             C.POINTER(vp), C.POINTER(vp)]),
         "hpccg_hip_group_solve": (ip, [C.POINTER(vp), ip, C.POINTER(vp), C.POINTER(vp), ip, dp, PI,
@@ -199,6 +202,26 @@ def generate_matrix(nx, ny, nz, rank=0, size=1, use_7pt=False) -> Problem:
     _check(L.hpccg_generate_matrix(nx, ny, nz, rank, size, int(use_7pt), C.byref(A), C.byref(x),
                                    C.byref(b), C.byref(xe)), "generate_matrix")
     return Problem(A, x, b, xe, nx * ny * nz)
+
+
+def read_HPC_row(data_file: str, rank=0, size=1) -> Problem:
+    """read_HPC_row.cpp:217-373 (Mode 2): rank's block of rows of the system in
+    data_file (global columns), with x0, b, xexact from the file."""
+    L = lib()
+    A = C.POINTER(_HPCMatrix)()
+    x, b, xe = C.POINTER(C.c_double)(), C.POINTER(C.c_double)(), C.POINTER(C.c_double)()
+    _check(L.hpccg_read_HPC_row(os.fsencode(data_file), rank, size, C.byref(A), C.byref(x), C.byref(b),
+                                C.byref(xe)), "read_HPC_row")
+    p = Problem(A, x, b, xe, A.contents.local_nrow)
+    p.start_row = A.contents.start_row
+    p.total_nrow = A.contents.total_nrow
+    p.total_nnz = A.contents.total_nnz
+    return p
+
+
+def set_halo_mode(mode: int) -> None:
+    """0 auto, 1 z-slab only, 2 gather plan (matrices created afterwards)."""
+    _check(lib().hpccg_hip_set_halo_mode(mode), "set_halo_mode")
 
 
 # ---------------------------------------------------------------------------

@@ -90,6 +90,8 @@ constexpr int kXDefer = 8;  // p ring length = x-update deferral depth
 void launch_cg_prologue_copy(const CgArgs& a, hipStream_t s);   // p = x + 0*x
 void launch_cg_p_update(const CgArgs& a, hipStream_t s);        // p = r + beta p
 void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s);  // same, halo rows only
+// gather plan: buf[i] = p_k[idx[i]] (computed when fused; prologue: p = x)
+void launch_cg_pack(const CgArgs& a, const int* idx, int cnt, double* buf, bool prologue, hipStream_t s);
 void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s);
 bool spmv_variant_ok(int variant);
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s);

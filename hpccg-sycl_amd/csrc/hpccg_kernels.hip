@@ -452,6 +452,35 @@ __global__ __launch_bounds__(256) void k_p_boundary(CgArgs a, int nlo, int nhi)
     cur_p(a, k)[row] = rv + beta * yv;
 }
 
+// Gather halo plan: pack p_k at the rows the requesting ranks need
+// (exchange_externals.cpp:100-118 fills send_buffer the same way). With the p
+// update fused into the SpMV, p_k is computed here with k_p_update's exact
+// expression (the SpMV stores the same bits at those rows later).
+__global__ __launch_bounds__(256) void k_pack(CgArgs a, const int* __restrict__ idx, int cnt,
+                                              double* __restrict__ buf, bool prologue)
+{
+    int k = 0;
+    if (!prologue) {
+        k = a.kst[0];
+        if (!cg_run(a, k, true)) return;
+    }
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= cnt) return;
+    const int e = idx[i];
+    double v;
+    if (prologue) {
+        v = a.p[e];
+    } else if (a.fuse_p) {
+        const double beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+        const double rv = a.r[e];
+        const double yv = (k == 1) ? rv : cur_p(a, k - 1)[e];
+        v = rv + beta * yv;
+    } else {
+        v = cur_p(a, k)[e];
+    }
+    buf[i] = v;
+}
+
 // ---------------------------------------------------------------------------
 // SpMV over SELL-512 (HPC_sparsemv.cpp:68-89) + fused p.Ap slice partial
 // (ddot.cpp:60-73), optionally + the p update (waxpby, HPCCG.cpp:362/369).
@@ -1033,6 +1062,12 @@ void launch_cg_prologue_copy(const CgArgs& a, hipStream_t s)
 void launch_cg_p_update(const CgArgs& a, hipStream_t s)
 {
     hipLaunchKernelGGL(k_p_update<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
+}
+
+void launch_cg_pack(const CgArgs& a, const int* idx, int cnt, double* buf, bool prologue, hipStream_t s)
+{
+    if (cnt <= 0) return;
+    hipLaunchKernelGGL(k_pack, dim3((cnt + 255) / 256), dim3(256), 0, s, a, idx, cnt, buf, prologue);
 }
 
 void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)

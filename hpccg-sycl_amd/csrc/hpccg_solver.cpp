@@ -15,6 +15,7 @@
 #include <cstring>
 #include <iostream>
 #include <map>
+#include <unordered_map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -43,6 +44,15 @@ int set_err(int code, const char* fmt, ...)
     g_err = buf;
     return code;
 }
+
+}  // namespace
+
+namespace hpccg {
+// error channel for the other host translation units (read_hpc_row.cpp)
+int set_error_message(int code, const char* msg) { return set_err(code, "%s", msg); }
+}  // namespace hpccg
+
+namespace {
 
 #define HIP_TRY(expr)                                                                              \
     do {                                                                                           \
@@ -79,20 +89,46 @@ Comm g_comm;
 // In-process rank group (hpccg_hip_group_*): while a group member is being
 // created on this thread, rank/size come from here instead of the RCCL
 // communicator, and the halo plan is made by hpccg_hip_group_* afterwards.
+// Gather halo plan (make_local_matrix.cpp:58-610, exchange_externals.cpp:51-131)
+// for partitions the z-slab plan cannot serve: the external columns get local
+// indices n, n+1, ... grouped by owning rank, groups in order of first
+// appearance and first appearance inside a group, exactly as
+// make_local_matrix.cpp:96-200 numbers them.
+struct GatherPlan {
+    std::vector<long long> ext_global;              // external j <-> local column n + j
+    std::unordered_map<long long, int> ext_of;      // global column -> j
+    std::vector<int> recv_rank, recv_off, recv_cnt; // externals owned by recv_rank[i]: [off, off + cnt)
+    std::vector<std::vector<int>> req;              // per owner: the global columns we need, our order
+    std::vector<int> send_rank, send_off, send_cnt; // per requester: a run of send_idx
+    std::vector<int> send_idx;                      // local rows packed for the requesters
+};
+
 struct GroupCtx {
     int active = 0, nranks = 1, rank = 0;
+    const int* info = nullptr;        // every member's {nrow, ghost_lo, ghost_hi, start_row}, or null
+    const GatherPlan* plan = nullptr; // this member's gather plan (gather mode), or null
 };
 thread_local GroupCtx g_group_ctx;
+int g_halo_mode = 0;  // 0 auto (slab when it serves every rank), 1 slab only, 2 gather
 int comm_nranks() { return g_group_ctx.active ? g_group_ctx.nranks : g_comm.nranks; }
 int comm_rank() { return g_group_ctx.active ? g_group_ctx.rank : g_comm.rank; }
 
 // ---------------------------------------------------------------------------
 // SELL-512 build from any row accessor. Entry order per row is preserved.
 // ---------------------------------------------------------------------------
-template <class RowLen, class RowAt>
-long long sell_build_impl(int nrow, long long col_base, long long ncol_ext, RowLen row_len,
-                          RowAt row_at, unsigned int* slice_base, int* sell_cols, double* sell_vals,
-                          int uniform_width, int* err)
+// Column map of the slab plan: global column -> index into [ghost_lo | n | ghost_hi].
+struct SlabCols {
+    long long col_base, ncol_ext;
+    long long operator()(long long c) const
+    {
+        const long long lc = c - col_base;
+        return (lc < 0 || lc >= ncol_ext) ? -1 : lc;
+    }
+};
+
+template <class RowLen, class RowAt, class ColMap>
+long long sell_build_impl(int nrow, ColMap colmap, RowLen row_len, RowAt row_at, unsigned int* slice_base,
+                          int* sell_cols, double* sell_vals, int uniform_width, int* err)
 {
     const int nslices = (nrow + kSliceRows - 1) / kSliceRows;
     // widths
@@ -128,8 +164,8 @@ long long sell_build_impl(int nrow, long long col_base, long long ncol_ext, RowL
                         double v;
                         long long c;
                         row_at(i, j, &c, &v);
-                        const long long lc = c - col_base;
-                        if (lc < 0 || lc >= ncol_ext) bad.store(1);
+                        const long long lc = colmap(c);
+                        if (lc < 0) bad.store(1);
                         sell_cols[e] = (int)lc;
                         sell_vals[e] = v;
                     } else {
@@ -162,6 +198,13 @@ struct hpccg_hip_matrix {
     // what neighbours need from us (filled by the collective plan exchange)
     int send_lo = 0;  // rows to send to rank-1 (its ghost_hi)
     int send_hi = 0;  // rows to send to rank+1 (its ghost_lo)
+    // gather plan (partitions the slab plan cannot serve): externals after the
+    // local rows (ghost_lo = 0, ghost_hi = number of externals)
+    int general = 0;
+    std::vector<int> recv_rank, recv_off, recv_cnt, send_rank, send_off, send_cnt;
+    int nsend = 0;
+    int* d_send_idx = nullptr;
+    double* d_send_buf = nullptr;
     long long nnz = 0, nslots = 0;
     int nslices = 0, grid = 0, width = 0, uniform = 0;
     int spmv_variant = 0;
@@ -222,7 +265,7 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_tickets,
                     M->d_kst,        M->d_hist,    M->d_stamps, M->d_ddot_partial, M->d_gen_b,
                     M->d_gen_x0,     M->d_gen_xexact, M->d_lcols, M->d_win_ptr, M->d_win_start,
-                    M->d_win_len,    M->d_win_off};
+                    M->d_win_len,    M->d_win_off, M->d_send_idx, M->d_send_buf};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -231,16 +274,187 @@ int free_matrix(hpccg_hip_matrix* M)
     return 0;
 }
 
-// Plan exchange: every rank learns what its neighbours need (make_local_matrix
-// .cpp:286-587 does this with MPI handshakes; for z-slabs it is one
-// all-gather of {nrow, ghost_lo, ghost_hi}).
-int exchange_plan(hpccg_hip_matrix* M)
+// Can the z-slab plan serve rank r? (ghosts from rank+-1 only, contiguous,
+// the planes those ranks own; the condition hpccg_slab_plan enforces)
+bool slab_serves(const int* info, int P, int r)
+{
+    const int* me = info + 4 * r;
+    const int glo = me[1], ghi = me[2];
+    if (glo > 0 && (r == 0 || glo > info[4 * (r - 1)])) return false;
+    if (ghi > 0 && (r == P - 1 || ghi > info[4 * (r + 1)])) return false;
+    if (r > 0 && info[4 * (r - 1) + 3] + info[4 * (r - 1)] != me[3]) return false;
+    return true;
+}
+
+// 1 = slab plan for every rank, 2 = gather plan for every rank (all ranks decide
+// the same from the same all-gathered info).
+int choose_halo_mode(const int* info, int P)
+{
+    if (g_halo_mode == 2) return 2;
+    for (int r = 0; r < P; r++)
+        if (!slab_serves(info, P, r)) return g_halo_mode == 1 ? -1 : 2;
+    return 1;
+}
+
+int owner_of(long long c, const int* info, int P)  // make_local_matrix.cpp:165-173
+{
+    int lo = 0, hi = P - 1;
+    while (lo < hi) {  // last rank whose start_row <= c
+        const int mid = (lo + hi + 1) / 2;
+        if (info[4 * mid + 3] <= c) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+template <class RowLen, class RowAt>
+void gather_externals(int nrow, long long start, const int* info, int P, RowLen row_len, RowAt row_at,
+                      GatherPlan& g)
+{
+    std::vector<long long> first;  // externals in order of first appearance
+    std::unordered_map<long long, int> seen;
+    for (int i = 0; i < nrow; i++) {
+        const int len = row_len(i);
+        for (int j = 0; j < len; j++) {
+            long long c;
+            double v;
+            row_at(i, j, &c, &v);
+            if (c >= start && c < start + nrow) continue;
+            if (seen.emplace(c, (int)first.size()).second) first.push_back(c);
+        }
+    }
+    std::vector<std::vector<int>> by_owner(P);
+    std::vector<int> order;
+    for (int i = 0; i < (int)first.size(); i++) {
+        const int q = owner_of(first[i], info, P);
+        if (by_owner[q].empty()) order.push_back(q);
+        by_owner[q].push_back(i);
+    }
+    g.ext_global.assign(first.size(), 0);
+    g.req.assign(P, {});
+    int count = 0;
+    for (int q : order) {
+        g.recv_rank.push_back(q);
+        g.recv_off.push_back(count);
+        g.recv_cnt.push_back((int)by_owner[q].size());
+        for (int i : by_owner[q]) {
+            g.ext_global[count] = first[i];
+            g.ext_of[first[i]] = count;
+            g.req[q].push_back((int)first[i]);
+            count++;
+        }
+    }
+}
+
+// What rank r packs for its requesters, from every rank's requests
+// (reqs_to_me[q] = the global columns rank q needs from r, q's order).
+void gather_sends(long long start, const std::vector<std::vector<int>>& reqs_to_me, GatherPlan& g)
+{
+    g.send_rank.clear();
+    g.send_off.clear();
+    g.send_cnt.clear();
+    g.send_idx.clear();
+    for (int q = 0; q < (int)reqs_to_me.size(); q++) {
+        if (reqs_to_me[q].empty()) continue;
+        g.send_rank.push_back(q);
+        g.send_off.push_back((int)g.send_idx.size());
+        g.send_cnt.push_back((int)reqs_to_me[q].size());
+        for (int c : reqs_to_me[q]) g.send_idx.push_back((int)(c - start));
+    }
+}
+
+// RCCL: requests travel to their owners (the handshake of make_local_matrix
+// .cpp:286-587): an all-gather of the P x P count matrix, then grouped
+// send/recv of the int32 column lists.
+int rccl_requests(hpccg_hip_matrix* M, GatherPlan& g)
+{
+    const int P = g_comm.nranks, r = g_comm.rank;
+    std::vector<int> mine(P);
+    for (int q = 0; q < P; q++) mine[q] = (int)g.req[q].size();
+    int* d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof(int) * (size_t)P * (P + 1)));
+    HIP_TRY(hipMemcpy(d, mine.data(), sizeof(int) * P, hipMemcpyHostToDevice));
+    NCCL_TRY(ncclAllGather(d, d + P, P, ncclInt32, g_comm.comm, M->stream));
+    std::vector<int> cnt((size_t)P * P);
+    HIP_TRY(hipMemcpyAsync(cnt.data(), d + P, sizeof(int) * P * P, hipMemcpyDeviceToHost, M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    (void)hipFree(d);
+    long long nout = 0, nin = 0;
+    for (int q = 0; q < P; q++) {
+        nout += cnt[(size_t)r * P + q];
+        nin += cnt[(size_t)q * P + r];
+    }
+    int* dout = nullptr;
+    int* din = nullptr;
+    HIP_TRY(hipMalloc(&dout, sizeof(int) * std::max(1LL, nout)));
+    HIP_TRY(hipMalloc(&din, sizeof(int) * std::max(1LL, nin)));
+    std::vector<int> flat;
+    for (int q = 0; q < P; q++) flat.insert(flat.end(), g.req[q].begin(), g.req[q].end());
+    if (nout) HIP_TRY(hipMemcpy(dout, flat.data(), sizeof(int) * nout, hipMemcpyHostToDevice));
+    NCCL_TRY(ncclGroupStart());
+    long long oo = 0, oi = 0;
+    for (int q = 0; q < P; q++) {
+        const int co = cnt[(size_t)r * P + q], ci = cnt[(size_t)q * P + r];
+        if (co) NCCL_TRY(ncclSend(dout + oo, co, ncclInt32, q, g_comm.comm, M->stream));
+        if (ci) NCCL_TRY(ncclRecv(din + oi, ci, ncclInt32, q, g_comm.comm, M->stream));
+        oo += co;
+        oi += ci;
+    }
+    NCCL_TRY(ncclGroupEnd());
+    std::vector<int> got(std::max(1LL, nin));
+    HIP_TRY(hipMemcpyAsync(got.data(), din, sizeof(int) * std::max(1LL, nin), hipMemcpyDeviceToHost, M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    (void)hipFree(dout);
+    (void)hipFree(din);
+    std::vector<std::vector<int>> to_me(P);
+    oi = 0;
+    for (int q = 0; q < P; q++) {
+        const int ci = cnt[(size_t)q * P + r];
+        to_me[q].assign(got.begin() + oi, got.begin() + oi + ci);
+        oi += ci;
+    }
+    gather_sends(M->start_row, to_me, g);
+    return 0;
+}
+
+// Install a gather plan on M (host tables + device send list/buffer).
+int install_gather(hpccg_hip_matrix* M, const GatherPlan& g)
+{
+    M->general = 1;
+    M->ghost_lo = 0;
+    M->ghost_hi = (int)g.ext_global.size();
+    M->recv_rank = g.recv_rank;
+    M->recv_off = g.recv_off;
+    M->recv_cnt = g.recv_cnt;
+    M->send_rank = g.send_rank;
+    M->send_off = g.send_off;
+    M->send_cnt = g.send_cnt;
+    M->nsend = (int)g.send_idx.size();
+    HIP_TRY(hipMalloc(&M->d_send_idx, sizeof(int) * std::max(1, M->nsend)));
+    HIP_TRY(hipMalloc(&M->d_send_buf, sizeof(double) * std::max(1, M->nsend)));
+    if (M->nsend)
+        HIP_TRY(hipMemcpy(M->d_send_idx, g.send_idx.data(), sizeof(int) * M->nsend, hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Plan exchange: every rank learns what its neighbours need. For z-slabs it is
+// one all-gather of {nrow, ghost_lo, ghost_hi, start_row}; when the slab plan
+// cannot serve every rank, *mode is set to 2 and the caller builds the gather
+// plan (the general make_local_matrix.cpp:58-610 handshake).
+int exchange_plan(hpccg_hip_matrix* M, int* mode = nullptr, std::vector<int>* all_out = nullptr)
 {
     M->send_lo = M->send_hi = 0;
     M->rank = comm_rank();
     M->nranks = comm_nranks();
-    if (g_group_ctx.active) {  // in-process group: planned when every member exists
+    if (mode) *mode = 1;
+    if (g_group_ctx.active) {  // in-process group: planned by the group functions
         M->in_group = 1;
+        if (g_group_ctx.info) {
+            const int P = g_group_ctx.nranks;
+            const int md = P == 1 ? 1 : choose_halo_mode(g_group_ctx.info, P);
+            if (md < 0) return set_err(HPCCG_HIP_EPLAN, "the z-slab halo plan cannot serve this partition");
+            if (mode) *mode = md;
+            if (all_out) all_out->assign(g_group_ctx.info, g_group_ctx.info + 4 * P);
+        }
         return 0;
     }
     if (g_comm.nranks == 1) {
@@ -258,6 +472,14 @@ int exchange_plan(hpccg_hip_matrix* M)
                            M->stream));
     HIP_TRY(hipStreamSynchronize(M->stream));
     (void)hipFree(d);
+    const int md = choose_halo_mode(all.data(), g_comm.nranks);
+    if (md < 0) return set_err(HPCCG_HIP_EPLAN, "the z-slab halo plan cannot serve this partition");
+    if (all_out) *all_out = all;
+    if (md == 2) {
+        if (!mode) return set_err(HPCCG_HIP_EPLAN, "gather halo plan needs the matrix rows");
+        *mode = 2;
+        return 0;
+    }
     int sends[2];
     TRY(hpccg_slab_plan(g_comm.nranks, g_comm.rank, all.data(), sends));
     M->send_lo = sends[0];
@@ -418,6 +640,24 @@ int enqueue_halo(hpccg_hip_matrix* M, double* p)
     return 0;
 }
 
+// Gather plan over RCCL (exchange_externals.cpp:51-131): pack what each
+// requester needs, then one grouped send/recv per neighbour; the externals
+// arrive contiguously after the local rows.
+int enqueue_halo_gather(hpccg_hip_matrix* M, const CgArgs& a, double* p, bool prologue)
+{
+    if (g_comm.nranks == 1) return 0;
+    launch_cg_pack(a, M->d_send_idx, M->nsend, M->d_send_buf, prologue, M->stream);
+    NCCL_TRY(ncclGroupStart());
+    for (size_t i = 0; i < M->recv_rank.size(); i++)
+        NCCL_TRY(ncclRecv(p + M->nrow + M->recv_off[i], M->recv_cnt[i], ncclFloat64, M->recv_rank[i],
+                          g_comm.comm, M->stream));
+    for (size_t i = 0; i < M->send_rank.size(); i++)
+        NCCL_TRY(ncclSend(M->d_send_buf + M->send_off[i], M->send_cnt[i], ncclFloat64, M->send_rank[i],
+                          g_comm.comm, M->stream));
+    NCCL_TRY(ncclGroupEnd());
+    return 0;
+}
+
 int enqueue_allreduce(hpccg_hip_matrix* M, const CgArgs& a, int which)
 {
     if (g_comm.nranks == 1) return 0;
@@ -485,6 +725,37 @@ int group_halo(const Ranks& R, int k_host, bool prologue)
     return 0;
 }
 
+// In-process gather halo: every member packs for its requesters; each
+// receiver copies its runs out of the owners' send buffers. An owner's next
+// pack (next iteration) follows an all-reduce that waits for the receiver's
+// SpMV, which follows the copy.
+int group_halo_gather(const Ranks& R, int k_host, bool prologue)
+{
+    for (int r = 0; r < R.P; r++) {
+        hpccg_hip_matrix* M = R.M[r];
+        TRY(use_device(R, r));
+        launch_cg_pack(R.a[r], M->d_send_idx, M->nsend, M->d_send_buf, prologue, M->stream);
+        HIP_TRY(hipEventRecord(R.ev[r], M->stream));
+    }
+    for (int r = 0; r < R.P; r++) {
+        hpccg_hip_matrix* M = R.M[r];
+        double* p = prologue ? R.a[r].p : ring_p(R.a[r], k_host);
+        TRY(use_device(R, r));
+        for (size_t i = 0; i < M->recv_rank.size(); i++) {
+            const int q = M->recv_rank[i];
+            const hpccg_hip_matrix* Q = R.M[q];
+            size_t j = 0;
+            while (j < Q->send_rank.size() && Q->send_rank[j] != r) j++;
+            if (j == Q->send_rank.size() || Q->send_cnt[j] != M->recv_cnt[i])
+                return set_err(HPCCG_HIP_EPLAN, "rank %d: no matching send run on rank %d", r, q);
+            HIP_TRY(hipStreamWaitEvent(M->stream, R.ev[q], 0));
+            HIP_TRY(hipMemcpyPeerAsync(p + M->nrow + M->recv_off[i], M->device, Q->d_send_buf + Q->send_off[j],
+                                       Q->device, sizeof(double) * M->recv_cnt[i], M->stream));
+        }
+    }
+    return 0;
+}
+
 // In-process all-reduce of loc[which]: one lane on rank 0's stream adds the
 // ranks' values in rank order and writes g[which] of every rank.
 int group_allreduce(const Ranks& R, int which)
@@ -516,6 +787,10 @@ int exch_halo(const Ranks& R, int k_host, bool prologue)
         TRY(use_device(R, r));
         launch_cg_stamp(R.a[r], kStampHalo, prologue, R.M[r]->stream);
     }
+    if (R.M[0]->general) {
+        if (R.P > 1) return group_halo_gather(R, k_host, prologue);
+        return enqueue_halo_gather(R.M[0], R.a[0], prologue ? R.a[0].p : ring_p(R.a[0], k_host), prologue);
+    }
     if (R.P > 1) return group_halo(R, k_host, prologue);
     return enqueue_halo(R.M[0], prologue ? R.a[0].p : ring_p(R.a[0], k_host));
 }
@@ -541,7 +816,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
         TRY(use_device(R, r));
         if (!R.a[r].fuse_p)
             launch_cg_p_update(R.a[r], R.M[r]->stream);
-        else if (multi)
+        else if (multi && !R.M[r]->general)  // gather plan: k_pack computes the halo rows
             launch_cg_p_boundary(R.a[r], R.M[r]->send_lo, R.M[r]->send_hi, R.M[r]->stream);
     }
     if (multi) TRY(exch_halo(R, k_host, false));
@@ -937,8 +1212,33 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
     M->nnz = nnz;
     M->ghost_lo = (int)std::max(0LL, (long long)start_row - mn);
     M->ghost_hi = (int)std::max(0LL, mx - ((long long)start_row + nrow - 1));
+    if (mn < 0 || mx >= total_nrow) {
+        delete M;
+        return set_err(HPCCG_HIP_EPLAN, "column outside [0, total_nrow)");
+    }
     HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamDefault));
-    int rc = exchange_plan(M);
+    int mode = 1;
+    std::vector<int> all;
+    GatherPlan gp_local;
+    const GatherPlan* gp = nullptr;
+    int rc = exchange_plan(M, &mode, &all);
+    if (rc == 0 && mode == 2) {
+        // gather plan: externals after the local rows (make_local_matrix.cpp:58-610)
+        if (g_group_ctx.active) {
+            gp = g_group_ctx.plan;
+            if (!gp) rc = set_err(HPCCG_HIP_EPLAN, "group member without a gather plan");
+        } else {
+            gather_externals(nrow, start_row, all.data(), M->nranks, row_len, row_at, gp_local);
+            rc = rccl_requests(M, gp_local);
+            gp = &gp_local;
+        }
+        if (rc == 0) rc = install_gather(M, *gp);
+    } else if (rc == 0 && g_group_ctx.active && g_group_ctx.info && M->nranks > 1) {
+        int sends[2];
+        rc = hpccg_slab_plan(M->nranks, M->rank, g_group_ctx.info, sends);
+        M->send_lo = sends[0];
+        M->send_hi = sends[1];
+    }
     if (rc) {
         free_matrix(M);
         return rc;
@@ -949,19 +1249,34 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
     const long long ncol_ext = (long long)M->ghost_lo + nrow + M->ghost_hi;
     // uniform width when padding to the max costs < 4 % (stencils)
     std::vector<unsigned int> sb(M->nslices + 1);
-    const long long slots_var =
-        sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, sb.data(), nullptr, nullptr, 0, nullptr);
-    const long long slots_uni =
-        sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, sb.data(), nullptr, nullptr, 1, nullptr);
-    M->uniform = (slots_uni <= slots_var + slots_var / 25) ? 1 : 0;
-    M->nslots = sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, sb.data(), nullptr, nullptr,
-                                M->uniform, nullptr);
-    M->width = M->nslices ? (int)(M->nslots / kSliceRows / M->nslices) : 0;
-    std::vector<int> hc((size_t)std::max(1LL, M->nslots));
-    std::vector<double> hv((size_t)std::max(1LL, M->nslots));
+    std::vector<int> hc;
+    std::vector<double> hv;
     int bad = 0;
-    sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, sb.data(), hc.data(), hv.data(), M->uniform,
-                    &bad);
+    auto build = [&](auto colmap) {
+        const long long slots_var = sell_build_impl(nrow, colmap, row_len, row_at, sb.data(), nullptr, nullptr, 0,
+                                                    nullptr);
+        const long long slots_uni = sell_build_impl(nrow, colmap, row_len, row_at, sb.data(), nullptr, nullptr, 1,
+                                                    nullptr);
+        M->uniform = (slots_uni <= slots_var + slots_var / 25) ? 1 : 0;
+        M->nslots = sell_build_impl(nrow, colmap, row_len, row_at, sb.data(), nullptr, nullptr, M->uniform,
+                                    nullptr);
+        M->width = M->nslices ? (int)(M->nslots / kSliceRows / M->nslices) : 0;
+        hc.assign((size_t)std::max(1LL, M->nslots), 0);
+        hv.assign((size_t)std::max(1LL, M->nslots), 0.0);
+        sell_build_impl(nrow, colmap, row_len, row_at, sb.data(), hc.data(), hv.data(), M->uniform, &bad);
+    };
+    if (M->general) {
+        // own columns -> c - start_row; externals -> n + j (ghost_lo = 0)
+        const std::unordered_map<long long, int>& ext = gp->ext_of;
+        const long long s0 = start_row, n0 = nrow;
+        build([&ext, s0, n0](long long c) -> long long {
+            if (c >= s0 && c < s0 + n0) return c - s0;
+            const auto it = ext.find(c);
+            return it == ext.end() ? -1 : n0 + it->second;
+        });
+    } else {
+        build(SlabCols{col_base, ncol_ext});
+    }
     if (bad) {
         free_matrix(M);
         return set_err(HPCCG_HIP_EPLAN, "column index outside the halo plan");
@@ -1029,7 +1344,8 @@ std::map<const void*, hpccg_hip_matrix*> g_dropin_cache;
 namespace {
 
 template <class Make>
-int group_make(int nranks, const int* devices, hpccg_hip_matrix** out, Make make)
+int group_make(int nranks, const int* devices, hpccg_hip_matrix** out, Make make, const int* info = nullptr,
+               const std::vector<GatherPlan>* plans = nullptr)
 {
     if (!out) return set_err(HPCCG_HIP_EINVAL, "out is NULL");
     if (nranks < 1 || nranks > kMaxGroupRanks)
@@ -1045,20 +1361,20 @@ int group_make(int nranks, const int* devices, hpccg_hip_matrix** out, Make make
             rc = set_err(HPCCG_HIP_EHIP, "hipSetDevice(%d) failed", dev);
             break;
         }
-        g_group_ctx = GroupCtx{1, nranks, r};
+        g_group_ctx = GroupCtx{1, nranks, r, info, plans ? &(*plans)[r] : nullptr};
         rc = make(r, &out[r]);
         g_group_ctx = GroupCtx();
     }
-    // halo plan from every member's {nrow, ghost_lo, ghost_hi, start_row}
-    std::vector<int> info(4 * nranks);
+    // slab plan from every member's {nrow, ghost_lo, ghost_hi, start_row}
+    std::vector<int> minfo(4 * nranks);
     for (int r = 0; r < nranks && rc == 0; r++) {
         const hpccg_hip_matrix* M = out[r];
         int mine[4] = {M->nrow, M->ghost_lo, M->ghost_hi, M->start_row};
-        std::memcpy(&info[4 * r], mine, sizeof mine);
+        std::memcpy(&minfo[4 * r], mine, sizeof mine);
     }
-    for (int r = 0; r < nranks && rc == 0; r++) {
+    for (int r = 0; r < nranks && rc == 0 && !out[0]->general; r++) {
         int sends[2];
-        rc = hpccg_slab_plan(nranks, r, info.data(), sends);
+        rc = hpccg_slab_plan(nranks, r, minfo.data(), sends);
         if (rc == 0) {
             out[r]->send_lo = sends[0];
             out[r]->send_hi = sends[1];
@@ -1322,9 +1638,53 @@ int hpccg_hip_group_create_csr(int nranks, const int* devices, const int* nrow, 
                                const double* const* vals, hpccg_hip_matrix** out)
 {
     if (!nrow || !start_row || !row_ptr || !cols || !vals) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
-    return group_make(nranks, devices, out, [&](int r, hpccg_hip_matrix** m) {
-        return hpccg_hip_matrix_create_csr(nrow[r], start_row[r], total_nrow, row_ptr[r], cols[r], vals[r], m);
-    });
+    if (nranks < 1 || nranks > kMaxGroupRanks)
+        return set_err(HPCCG_HIP_EINVAL, "group size must be 1..%d", kMaxGroupRanks);
+    // what the all-gather of exchange_plan would give every member
+    std::vector<int> info(4 * nranks);
+    for (int r = 0; r < nranks; r++) {
+        if (nrow[r] < 0 || (nrow[r] > 0 && (!row_ptr[r] || !cols[r] || !vals[r])))
+            return set_err(HPCCG_HIP_EINVAL, "member %d: bad CSR", r);
+        long long mn = start_row[r], mx = (long long)start_row[r] + nrow[r] - 1;
+        for (long long e = 0; e < (nrow[r] > 0 ? row_ptr[r][nrow[r]] : 0); e++) {
+            mn = std::min<long long>(mn, cols[r][e]);
+            mx = std::max<long long>(mx, cols[r][e]);
+        }
+        if (mn < 0 || mx >= total_nrow) return set_err(HPCCG_HIP_EPLAN, "member %d: column outside [0, total_nrow)", r);
+        info[4 * r] = nrow[r];
+        info[4 * r + 1] = (int)std::max(0LL, (long long)start_row[r] - mn);
+        info[4 * r + 2] = (int)std::max(0LL, mx - ((long long)start_row[r] + nrow[r] - 1));
+        info[4 * r + 3] = start_row[r];
+    }
+    const int mode = nranks == 1 ? 1 : choose_halo_mode(info.data(), nranks);
+    if (mode < 0) return set_err(HPCCG_HIP_EPLAN, "the z-slab halo plan cannot serve this partition");
+    std::vector<GatherPlan> plans;
+    if (mode == 2) {  // the requests every member would send its owners, then the send runs
+        plans.resize(nranks);
+        for (int r = 0; r < nranks; r++) {
+            const long long* rp = row_ptr[r];
+            const int* cl = cols[r];
+            const double* vl = vals[r];
+            gather_externals(nrow[r], start_row[r], info.data(), nranks,
+                             [rp](int i) { return (int)(rp[i + 1] - rp[i]); },
+                             [rp, cl, vl](int i, int j, long long* c, double* v) {
+                                 *c = cl[rp[i] + j];
+                                 *v = vl[rp[i] + j];
+                             },
+                             plans[r]);
+        }
+        for (int r = 0; r < nranks; r++) {
+            std::vector<std::vector<int>> to_me(nranks);
+            for (int q = 0; q < nranks; q++) to_me[q] = plans[q].req[r];
+            gather_sends(start_row[r], to_me, plans[r]);
+        }
+    }
+    return group_make(
+        nranks, devices, out,
+        [&](int r, hpccg_hip_matrix** m) {
+            return hpccg_hip_matrix_create_csr(nrow[r], start_row[r], total_nrow, row_ptr[r], cols[r], vals[r], m);
+        },
+        info.data(), mode == 2 ? &plans : nullptr);
 }
 
 int hpccg_hip_group_solve(hpccg_hip_matrix* const* Ms, int nranks, const double* const* b_dev,
@@ -1343,6 +1703,13 @@ int hpccg_hip_group_solve(hpccg_hip_matrix* const* Ms, int nranks, const double*
     const int rc = solve_ranks(Ms, nranks, b_dev, x_dev, max_iter, tolerance, niters, normr, times, 0);
     (void)hipSetDevice(cur);
     return rc;
+}
+
+int hpccg_hip_set_halo_mode(int mode)
+{
+    if (mode < 0 || mode > 2) return set_err(HPCCG_HIP_EINVAL, "halo mode must be 0, 1 or 2");
+    g_halo_mode = mode;
+    return 0;
 }
 
 int hpccg_hip_matrix_destroy(hpccg_hip_matrix* M) { return free_matrix(M); }
@@ -1477,6 +1844,8 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "fold")) *value = fold_effective(M);
     else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
+    else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
+    else if (!std::strcmp(key, "num_external")) *value = M->general ? M->ghost_hi : M->ghost_lo + M->ghost_hi;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_lds ? M->lds_doubles : 0;
     else if (!std::strcmp(key, "windows")) *value = M->nwin;
     else return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
@@ -1503,9 +1872,14 @@ int hpccg_hip_sparsemv(hpccg_hip_matrix* M, const double* x_dev, double* y_dev)
     if (!M || !x_dev || !y_dev) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
     HIP_TRY(hipSetDevice(M->device));
     // stage x into p (the halo-carrying buffer), exchange, multiply
+    if (M->in_group && M->nranks > 1)
+        return set_err(HPCCG_HIP_EINVAL, "group member: the halo needs hpccg_hip_group_solve");
     HIP_TRY(hipMemcpyAsync(M->d_p, x_dev, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
-    TRY(enqueue_halo(M, M->d_p));
     CgArgs a = make_args(M, nullptr, nullptr, 0, 0.0);
+    if (M->general)
+        TRY(enqueue_halo_gather(M, a, M->d_p, true));
+    else
+        TRY(enqueue_halo(M, M->d_p));
     launch_sparsemv(a, M->d_p - M->ghost_lo, y_dev, 0, M->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(M->stream));
@@ -1575,13 +1949,13 @@ long long hpccg_sell_build(int nrow, long long col_base, long long ncol_ext, con
         tmp.resize((nrow + kSliceRows - 1) / kSliceRows + 1);
         slice_base = tmp.data();
     }
-    const long long var = sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, slice_base, nullptr,
+    const long long var = sell_build_impl(nrow, SlabCols{col_base, ncol_ext}, row_len, row_at, slice_base, nullptr,
                                           nullptr, 0, nullptr);
-    const long long uni = sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, slice_base, nullptr,
+    const long long uni = sell_build_impl(nrow, SlabCols{col_base, ncol_ext}, row_len, row_at, slice_base, nullptr,
                                           nullptr, 1, nullptr);
     const int uniform = (uni <= var + var / 25) ? 1 : 0;
     int bad = 0;
-    const long long r = sell_build_impl(nrow, col_base, ncol_ext, row_len, row_at, slice_base, sell_cols,
+    const long long r = sell_build_impl(nrow, SlabCols{col_base, ncol_ext}, row_len, row_at, slice_base, sell_cols,
                                         sell_vals, uniform, &bad);
     return bad ? HPCCG_HIP_EPLAN : r;
 }

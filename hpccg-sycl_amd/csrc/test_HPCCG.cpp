@@ -1,7 +1,8 @@
 // test_HPCCG.cpp -- the reference command line, MI355X edition.
 //
 //   test_HPCCG nx ny nz          (Mode 1, main.cpp:146-159)
-//   test_HPCCG HPC_data_file     (Mode 2, deprecated in the reference; not built here)
+//   test_HPCCG HPC_data_file     (Mode 2, main.cpp:160-168: read_HPC_row.cpp format; rows
+//                                 block-distributed over the ranks, halo plan chosen by the library)
 //
 // Same stdout as the reference (main.cpp:136-305): residual lines, "Elapsed
 // time: X s", then the YAML report (also written to ./hpccg-1.0_<stamp>.yaml).
@@ -95,15 +96,13 @@ int main(int argc, char* argv[])
                       << std::endl;
         std::exit(1);
     }
-    if (argc == 2) {
-        std::cerr << "Mode 2 (HPC_data_file) is not available in this build; use: " << argv[0]
-                  << " nx ny nz" << std::endl;
-        std::exit(1);
-    }
-    const int nx = std::atoi(argv[1]), ny = std::atoi(argv[2]), nz = std::atoi(argv[3]);
+    const bool file_mode = argc == 2;
+    // Mode 2 leaves nx, ny, nz unset in the reference (main.cpp:110, 160-168); reported as 0
+    const int nx = file_mode ? 0 : std::atoi(argv[1]), ny = file_mode ? 0 : std::atoi(argv[2]),
+              nz = file_mode ? 0 : std::atoi(argv[3]);
     const int max_iter = env_int("HPCCG_MAX_ITER", 500);
     const int use_7pt = env_int("HPCCG_7PT", 0);
-    const bool dev_gen = env_int("HPCCG_DEVICE_GENERATE", 0) != 0;
+    const bool dev_gen = !file_mode && env_int("HPCCG_DEVICE_GENERATE", 0) != 0;
     const double tolerance = 0.0;  // main.cpp:188
 
     int ndev = 0;
@@ -116,7 +115,15 @@ int main(int argc, char* argv[])
     double *x = nullptr, *b = nullptr, *xexact = nullptr;
     hpccg_hip_matrix* M = nullptr;
     const auto ts = std::chrono::steady_clock::now();
-    if (dev_gen) {
+    if (file_mode) {
+        std::printf("Reading matrix info from %s...\n", argv[1]);  // read_HPC_row.cpp:239
+        std::fflush(stdout);
+        if (hpccg_read_HPC_row(argv[1], rank, size, &A, &x, &b, &xexact)) {
+            std::printf("%s\n", hpccg_hip_last_error());
+            std::exit(1);
+        }
+        if (hpccg_hip_matrix_create(A, &M)) die("matrix upload");
+    } else if (dev_gen) {
         if (hpccg_hip_matrix_generate(nx, ny, nz, use_7pt, &M)) die("device generate");
     } else {
         if (hpccg_generate_matrix(nx, ny, nz, rank, size, use_7pt, &A, &x, &b, &xexact))
@@ -127,7 +134,7 @@ int main(int argc, char* argv[])
 
     int niters = 0;
     double normr = 0.0;
-    const long long n = (long long)nx * ny * nz;
+    const long long n = file_mode ? (long long)A->local_nrow : (long long)nx * ny * nz;
     std::vector<double> xv;
     int ierr;
     const auto start = std::chrono::high_resolution_clock::now();
@@ -155,7 +162,7 @@ int main(int argc, char* argv[])
     double resid = 0.0;
     {
         const double* xs = dev_gen ? xv.data() : x;
-        for (long long i = 0; i < n; i++) resid = std::max(resid, std::fabs(xs[i] - 1.0));
+        for (long long i = 0; i < n; i++) resid = std::max(resid, std::fabs(xs[i] - (xexact ? xexact[i] : 1.0)));
         if (std::isnan(resid)) resid = NAN;
     }
     double t4 = times[4], t4min = t4, t4max = t4, t4avg = t4;
@@ -171,8 +178,10 @@ int main(int argc, char* argv[])
         long long info[8];
         hpccg_hip_matrix_info(M, info);
         const double fniters = niters;
-        const double fnrow = (double)n * size;
-        const double fnnz = 27.0 * fnrow;  // total_nnz as the reference stores it (main.cpp:222)
+        // total_nrow and total_nnz as the reference's matrix carries them (main.cpp:218-222):
+        // generate_matrix stores 27 * total_nrow, read_HPC_row the file header's count
+        const double fnrow = file_mode ? (double)A->total_nrow : (double)n * size;
+        const double fnnz = file_mode ? (double)A->total_nnz : 27.0 * fnrow;
         const double fnops_ddot = fniters * 4 * fnrow;
         const double fnops_waxpby = fniters * 6 * fnrow;
         const double fnops_sparsemv = fniters * 2 * fnnz;

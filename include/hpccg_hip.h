@@ -61,6 +61,14 @@ int hpccg_hip_device_name(char* buf, int cap, int* compute_units);
 int hpccg_generate_matrix(int nx, int ny, int nz, int rank, int size, int use_7pt,
                           struct HPC_Sparse_Matrix_STRUCT** A, double** x, double** b,
                           double** xexact);
+/* read_HPC_row (read_HPC_row.cpp:217-373, Mode 2 input): the rows of rank
+ * `rank` of `size` (the reference's block partition, remainder spread over the
+ * first ranks) of the system in data_file, global columns; x (initial guess),
+ * b and xexact from the file. Free with hpccg_free_problem. Returns
+ * HPCCG_HIP_EINVAL with a message on a missing or malformed file (the
+ * reference prints "Error: Cannot open file" and exits). Host only. */
+int hpccg_read_HPC_row(const char* data_file, int rank, int size, struct HPC_Sparse_Matrix_STRUCT** A,
+                       double** x, double** b, double** xexact);
 void hpccg_free_problem(struct HPC_Sparse_Matrix_STRUCT* A, double* x, double* b,
                         double* xexact);
 
@@ -80,6 +88,15 @@ int hpccg_hip_matrix_create_csr(int nrow, int start_row, int total_nrow, const l
  * xexact on the device. Rank/size from the communicator. */
 int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_matrix** out);
 int hpccg_hip_matrix_destroy(hpccg_hip_matrix* M);
+/* Halo plan for matrices created after this call (process-wide): 0 auto (the
+ * z-slab plan when it serves every rank -- contiguous ghost planes from rank+-1
+ * only -- else the gather plan), 1 slab only (HPCCG_HIP_EPLAN otherwise), 2
+ * gather always. The gather plan is make_local_matrix.cpp:58-610: external
+ * columns numbered after the local rows, grouped by owning rank in the
+ * reference's order, send lists learned from the owners' requests, and each
+ * halo exchange packs p at the requested rows (exchange_externals.cpp:51-131).
+ * The device generator always builds slab plans. */
+int hpccg_hip_set_halo_mode(int mode);
 /* nrow, ncol (incl. ghosts), stored nnz, SELL slots (incl. padding). */
 int hpccg_hip_matrix_info(const hpccg_hip_matrix* M, long long info_out[8]);
 /* Device pointers owned by M: b, x0 (zeros) and xexact of a generated matrix. */

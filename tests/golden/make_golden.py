@@ -67,22 +67,22 @@ def test_vector(n: int) -> np.ndarray:
     return (((i * 7919 + 13) % 1000) - 500).astype(np.float64) / 37.0
 
 
-def sweep_trace(M, b, m_max):
+def sweep_trace(M, b, m_max, x0=None):
     """normr_trace[k] for k = 0..m_max-1 via max_iter = k+1 runs of HPCCG()."""
     tr = []
     with quiet_stdout():
         for m in range(1, m_max + 1):
-            tr.append(oracle.ref_hpccg(M, b, max_iter=m)["normr"])
+            tr.append(oracle.ref_hpccg(M, b, max_iter=m, x=x0)["normr"])
     return tr
 
 
-def solve_case(name, M, b, n, max_iters, sweep, store_x=False, extra=None):
+def solve_case(name, M, b, n, max_iters, sweep, store_x=False, extra=None, x0=None):
     case = {"name": name, "nrow": n, "runs": {}}
     if extra:
         case.update(extra)
     for mi in max_iters:
         with quiet_stdout():
-            res = oracle.ref_hpccg(M, b, max_iter=mi)
+            res = oracle.ref_hpccg(M, b, max_iter=mi, x=x0)
         x = res["x"]
         run = {
             "max_iter": mi,
@@ -96,7 +96,7 @@ def solve_case(name, M, b, n, max_iters, sweep, store_x=False, extra=None):
             run["x_b64"] = b64(x)
         case["runs"][str(mi)] = run
     if sweep:
-        case["trace_normr"] = [v.hex() for v in sweep_trace(M, b, sweep)]
+        case["trace_normr"] = [v.hex() for v in sweep_trace(M, b, sweep, x0)]
     return case
 
 
@@ -160,6 +160,15 @@ def main():
                                 extra={"nx": nx, "ny": ny, "nz": nz, "ranks": P, "use_7pt": s7,
                                        "matrix_from": "oracle generator (global nz*ranks)"}))
         RM.close()
+    # Mode 2 (read_HPC_row.cpp) system: built by tests/golden/filemode.py (no RNG),
+    # solved by the reference HPCCG() from the file's initial guess.
+    sys.path.insert(0, OUT)
+    import filemode
+    rp, cl, vl, fx0, fb, fxe = filemode.general_system(600)
+    RM = oracle.ref_from_csr(oracle.CSR(rp, cl, vl, fx0, fb, fxe))
+    cases.append(solve_case("file_general_600", RM, fb, 600, [150, 500], sweep=120, x0=fx0,
+                            extra={"ranks": 1, "matrix_from": "tests/golden/filemode.py general_system(600)"}))
+    RM.close()
     golden["solves"] = cases
 
     # D. Reference CLI stdout (timings vary; tests compare structure and the
@@ -171,6 +180,14 @@ def main():
                              cwd=tmp, capture_output=True, text=True, check=True).stdout
         with open(os.path.join(OUT, "ref_cli_%dx%dx%d.txt" % dims), "w") as f:
             f.write(out)
+
+    # Mode 2 through the reference CLI (its own read_HPC_row.cpp)
+    fpath = os.path.join(tmp, "general_600.dat")
+    filemode.write(fpath, rp, cl, vl, fx0, fb, fxe)
+    out = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "test_HPCCG"), fpath],
+                         cwd=tmp, capture_output=True, text=True, check=True).stdout
+    with open(os.path.join(OUT, "ref_cli_file_general_600.txt"), "w") as f:
+        f.write(out.replace(fpath, "<DATA_FILE>"))
 
     with open(os.path.join(OUT, "golden.json"), "w") as f:
         json.dump(golden, f, separators=(",", ":"))
