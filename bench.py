@@ -123,6 +123,8 @@ def main():
     ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1 default)")
     ap.add_argument("--fold", type=int, default=-1, help="last-block dot completion (-1 default)")
     ap.add_argument("--x-defer", type=int, default=-1, help="batched x update (-1 default)")
+    ap.add_argument("--resident-mb", type=int, default=-1,
+                    help="MB of the matrix image streamed with default-policy loads (-1 default)")
     ap.add_argument("--rev-update", type=int, default=-1,
                     help="update kernel walks slices backwards (-1 default)")
     ap.add_argument("--event-steps", type=int, default=1,
@@ -162,6 +164,8 @@ def main():
         M.set_option("x_defer", args.x_defer)
     if args.rev_update >= 0:
         M.set_option("rev_update", args.rev_update)
+    if args.resident_mb >= 0:
+        M.set_option("resident_mb", args.resident_mb)
     b, x0, _ = M.vectors()
     nrow = n * n * n
     x = torch.zeros(nrow, dtype=torch.float64, device=f"cuda:{local_rank}")

@@ -48,6 +48,7 @@ struct CgArgs {
     int nring;             // p_k lives in ring buffer k % nring (1 = in place)
     int xdefer;            // 1: x += alpha_j p_j applied every nring iterations
     int rev;               // 1: the update kernel walks each XCD's slices backwards
+    int nt_split;          // NT matrix kernels: per XCD, this many leading slices use default-policy loads
     double* ahist;         // [max_iter + 1]: alpha_k (for the deferred x update)
     int fuse_p;            // 1: p = r + beta p computed inside the SpMV (single rank)
     int fold;              // dots completed in the producing kernel: 0 none, 1 both, 2 p.Ap only, 3 r.r only

@@ -628,6 +628,36 @@ __device__ __forceinline__ void ld_lcols(const unsigned short* __restrict__ p, u
     }
 }
 
+template <int kRpt, bool kNT, int kPre, int kP>
+__device__ __forceinline__ void lds_prefetch(const double* __restrict__ vp, const unsigned short* __restrict__ cp,
+                                             int wdt, Rows<kRpt> (&vpre)[kP], unsigned (&cpre)[kP][kRpt])
+{
+#pragma unroll
+    for (int j = 0; j < kPre; j++) {
+        if (j < wdt) {
+            ld_lcols<kRpt, kNT>(cp + (size_t)j * kSliceRows, cpre[j]);
+            vpre[j] = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+        }
+    }
+}
+
+template <int kRpt, bool kNT>
+__device__ __forceinline__ void lds_stream(const double* __restrict__ vp, const unsigned short* __restrict__ cp,
+                                           int j0, int wdt, const double* xs, double (&sum)[kRpt])
+{
+#pragma unroll 3
+    for (int j = j0; j < wdt; j++) {
+        unsigned c[kRpt];
+        ld_lcols<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
+        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            const double xv = (c[i] != kLdsPad) ? xs[c[i]] : 0.0;
+            sum[i] = sum[i] + v.v[i] * xv;
+        }
+    }
+}
+
 // kPre > 0: the first kPre slots of the matrix stream are loaded before the
 // window staging and its barrier, so the block's HBM stream starts at once.
 template <int kRpt, bool kNT, bool kFuse, int kPre>
@@ -658,13 +688,14 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     constexpr int kP = kPre > 0 ? kPre : 1;
     unsigned cpre[kP][kRpt];
     Rows<kRpt> vpre[kP];
-#pragma unroll
-    for (int j = 0; j < kPre; j++) {
-        if (j < wdt) {
-            ld_lcols<kRpt, kNT>(cp + (size_t)j * kSliceRows, cpre[j]);
-            vpre[j] = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
-        }
-    }
+    // the first nt_split slices of every XCD's eighth stream with the default
+    // policy (they may stay resident in the Infinity Cache between iterations,
+    // spread evenly over the XCDs), the rest non-temporal
+    const bool nt = kNT && (s % (a.grid / kNumXcd)) >= a.nt_split;
+    if (nt)
+        lds_prefetch<kRpt, true, kPre>(vp, cp, wdt, vpre, cpre);
+    else
+        lds_prefetch<kRpt, false, kPre>(vp, cp, wdt, vpre, cpre);
     // stage the windows; with kFuse the staged value of an own row is
     // p_k = r + beta*p_{k-1}, the exact expression k_p_update stores
     double beta = 0.0;
@@ -700,17 +731,10 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
             }
         }
     }
-#pragma unroll 3
-    for (int j = kPre; j < wdt; j++) {
-        unsigned c[kRpt];
-        ld_lcols<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
-        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
-#pragma unroll
-        for (int i = 0; i < kRpt; i++) {
-            const double xv = (c[i] != kLdsPad) ? xs[c[i]] : 0.0;
-            sum[i] = sum[i] + v.v[i] * xv;
-        }
-    }
+    if (nt)
+        lds_stream<kRpt, true>(vp, cp, kPre, wdt, xs, sum);
+    else
+        lds_stream<kRpt, false>(vp, cp, kPre, wdt, xs, sum);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     Rows<kRpt> o;
 #pragma unroll

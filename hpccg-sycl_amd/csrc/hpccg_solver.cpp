@@ -226,6 +226,7 @@ struct hpccg_hip_matrix {
     double* d_ahist = nullptr;
     int x_defer = 1;           // batched x update every kXDefer iterations
     int rev_update = 1;        // update kernel walks slices backwards (reads the SpMV's latest writes first)
+    long long resident_mb = -1; // NT kernels: MB of leading slices on default-policy loads (-1 auto)
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_partial = nullptr;
     unsigned int* d_tickets = nullptr;
@@ -547,9 +548,20 @@ int choose_variant(const hpccg_hip_matrix* M)
     const double rows = std::max(1, M->nrow);
     const bool lds = M->has_lds && (double)M->nnz / rows >= 2.5 * M->lds_doubles / (double)kSliceRows;
     const double image = (double)M->nslots * (lds ? 10.0 : 12.0);
-    const bool big = image > 300e6;
+    const bool big = image > 180e6;
     if (lds) return big ? 2200 : 2300;
     return big ? 1000 : 0;
+}
+
+// resident_mb auto: an NT image not far above the 256 MB Infinity Cache keeps
+// 128 MB of itself on default-policy loads, which then survive to the next
+// iteration (100^3, 270 MB: SpMV 59.6 vs 62.3 us); a multi-GB stream evicts
+// everything, and default-policy loads only cost there (200^3: 449 vs 432 us).
+long long resident_mb_effective(const hpccg_hip_matrix* M)
+{
+    if (M->resident_mb >= 0) return M->resident_mb;
+    const double image = (double)M->nslots * (M->has_lds ? 10.0 : 12.0);
+    return image <= 400e6 ? 128 : 0;
 }
 
 // fuse_p (single rank): measured slower in the plain SELL-512 kernels, where it
@@ -595,6 +607,11 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.fuse_p = fuse_p_effective(M) ? 1 : 0;
     a.xdefer = M->x_defer ? 1 : 0;
     a.rev = M->rev_update ? 1 : 0;
+    {
+        const double per_slice = (double)M->nslots / std::max(1, M->nslices) * (M->has_lds ? 10.0 : 12.0);
+        const double sl = (double)resident_mb_effective(M) * 1e6 / std::max(1.0, per_slice);
+        a.nt_split = (int)std::min<double>(M->grid / kNumXcd, sl / kNumXcd);
+    }
     a.nring = a.xdefer ? kXDefer : (a.fuse_p ? 2 : 1);
     a.ahist = M->d_ahist;
     a.fold = fold_effective(M);
@@ -1750,6 +1767,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->x_defer = (int)value;
     } else if (!std::strcmp(key, "rev_update")) {
         M->rev_update = (int)value;
+    } else if (!std::strcmp(key, "resident_mb")) {
+        M->resident_mb = value < 0 ? -1 : value;
     } else if (!std::strcmp(key, "fold")) {
         M->fold = (int)value;
     } else if (!std::strcmp(key, "spmv_variant")) {
@@ -1844,6 +1863,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "fold")) *value = fold_effective(M);
     else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
+    else if (!std::strcmp(key, "resident_mb")) *value = resident_mb_effective(M);
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
     else if (!std::strcmp(key, "num_external")) *value = M->general ? M->ghost_hi : M->ghost_lo + M->ghost_hi;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_lds ? M->lds_doubles : 0;

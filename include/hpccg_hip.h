@@ -128,7 +128,10 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  * block of the producing kernel completes a dot product: 0 neither, 1 both,
  * 2 p.Ap only, 3 r.r only; -1 auto (default): 2 up to 8192 slices, else 0), "x_defer" (1 = x += alpha p batched
  * every 8 iterations, default), "rev_update" (1 = the update kernel walks each
- * XCD's slices backwards, default). None of them
+ * XCD's slices backwards, default), "resident_mb" (non-temporal SpMV kernels:
+ * this many MB of leading slices per XCD use default-policy loads so they can
+ * stay in the Infinity Cache; -1 auto = 128 for images up to 400 MB, else 0).
+ * None of them
  * changes a computed value: fuse_p/fold on and off are bitwise equal. */
 int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value);
 int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* value);

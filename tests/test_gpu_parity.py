@@ -107,6 +107,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     for v, fuse in itertools.product((2000, 2100, 2200, 2308), (0, 1)):
         M.set_option("spmv_variant", v)
         M.set_option("fuse_p", fuse)
+        M.set_option("resident_mb", fuse)  # 1 MB on default-policy loads: no value changes
         assert M.get_option("fuse_p") == fuse
         x = prob.x
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
