@@ -67,6 +67,9 @@ struct CgArgs {
     const double* vals;
     // SELL-512-L: per-slice x windows staged in LDS + slice-local indices
     const unsigned short* lcols;  // LDS index of the column, kLdsPad = padding
+    const unsigned char* ccodes;  // SELL-512-C: per entry, code of its (column - row) offset
+    const int* cdict;             // SELL-512-C: per slice, kCodes offsets
+    const int* ldsc;              // SELL-512-C: per slice, LDS position of lane 0's column per code
     const int* win_ptr;    // [nslices + 1] into the window arrays
     const int* win_start;  // first local column of the window
     const int* win_len;    // entries
@@ -121,6 +124,14 @@ int ddot_nparts(int n);
 void launch_sparsemv(const CgArgs& a, const double* xext, double* y, int variant, hipStream_t s);
 
 // Device generator: writes the SELL-512 image, b, xexact.
+// SELL-512-C from the SELL-512 cols on the device (windows optional). ok[0]
+// = 0 if a slice has more than 255 distinct offsets, ok[1] = 0 if a code's
+// entries fall in different windows (no LDS form).
+constexpr int kCodes = 256;
+constexpr unsigned kCodePad = 255;
+void launch_build_c(const unsigned int* slice_base, int nslices, const int* cols, const int* win_ptr,
+                    const int* win_start, const int* win_off, const int* win_len, unsigned char* codes,
+                    int* cdict, int* ldsc, int* ok, hipStream_t s);
 // With win_* non-null it also writes the SELL-512-L index image (lcols).
 void launch_generate(int nx, int ny, int nz, int rank, int size, int use_7pt, long long col_base,
                      const unsigned int* slice_base, int* cols, double* vals, double* b,

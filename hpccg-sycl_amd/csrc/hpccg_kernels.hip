@@ -9,6 +9,9 @@
 // FMA); dot products use a fixed-shape two-stage tree (per-slice partials,
 // then one 1024-thread block in fixed order), so they are reproducible run to
 // run and differ from the reference's sequential sum only by rounding.
+#include <climits>
+#include <type_traits>
+
 #include "hpccg_internal.h"
 
 #pragma clang fp contract(off)
@@ -546,6 +549,192 @@ __device__ __forceinline__ void spmv_rows(const CgArgs& a, const G& gat, int s, 
 // Padding slots add v*x = 0*0 = +0: a sum that starts at +0.0 is never -0 under
 // round-to-nearest, so +0 leaves every row sum bit-identical to skipping it.
 
+// SELL-512-C: per slice a dictionary of the distinct (column - row) offsets
+// (at most 255; stencils have 7 or 27), and per stored entry a 1-byte code
+// (kCodePad = padding). The stream is 8 B value + 1 B code per slot. The plain
+// kernel gathers x[row + dict[code]]; the LDS kernel reads its staged window
+// at lane + ldsc[code], a per-slice constant for every code (checked at
+// build). Same products in the same order as SELL-512.
+template <int kRpt, bool kNT>
+__device__ __forceinline__ void ld_codes(const unsigned char* __restrict__ p, unsigned (&c)[kRpt])
+{
+    if constexpr (kRpt == 1) {
+        c[0] = kNT ? __builtin_nontemporal_load(p) : p[0];
+    } else if constexpr (kRpt == 2) {
+        const unsigned short t = kNT ? __builtin_nontemporal_load(reinterpret_cast<const unsigned short*>(p))
+                                     : *reinterpret_cast<const unsigned short*>(p);
+        c[0] = t & 0xFFu;
+        c[1] = t >> 8;
+    } else {
+#pragma unroll
+        for (int i = 0; i < kRpt; i += 4) {
+            const unsigned t = kNT ? __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p + i))
+                                   : *reinterpret_cast<const unsigned*>(p + i);
+#pragma unroll
+            for (int q = 0; q < 4; q++) c[i + q] = (t >> (8 * q)) & 0xFFu;
+        }
+    }
+}
+
+template <int kRpt, bool kNT, bool kFuse>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool prologue)
+{
+    __shared__ int sdict[kCodes];
+    int k = 0;
+    if (!prologue) {
+        k = a.kst[0];
+        const bool run = cg_run(a, k, kFuse);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = a.g[kRR];
+            if (run)
+                stamp(a, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    for (int i = threadIdx.x; i < kCodes; i += kSliceRows / kRpt) sdict[i] = a.cdict[(size_t)s * kCodes + i];
+    __syncthreads();
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    double* __restrict__ p = cur_p(a, k);
+    const size_t b0 = (size_t)a.slice_base[s];
+    const int w = (int)(a.slice_base[s + 1] - b0);
+    const size_t base = b0 * kSliceRows + (size_t)threadIdx.x * kRpt;
+    const double* __restrict__ vp = a.vals + base;
+    const unsigned char* __restrict__ cp = a.ccodes + base;
+    double beta = 0.0;
+    const double* pold = a.r;
+    if constexpr (kFuse) {
+        beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+        pold = (k == 1) ? a.r : cur_p(a, k - 1);
+    }
+    const double* __restrict__ xext = p - a.ghost_lo;
+    double sum[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+#pragma unroll 3
+    for (int j = 0; j < w; j++) {
+        unsigned c[kRpt];
+        ld_codes<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
+        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            double xv = 0.0;
+            if (c[i] != kCodePad) {
+                const int col = row + i + sdict[c[i]];
+                if constexpr (kFuse) xv = a.r[col - a.ghost_lo] + beta * pold[col - a.ghost_lo];
+                else xv = xext[col];
+            }
+            sum[i] = sum[i] + v.v[i] * xv;
+        }
+    }
+    Rows<kRpt> pv;
+    if constexpr (kFuse) {
+        const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+        const Rows<kRpt> yv = ld<kRpt>(pold + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + beta * yv.v[i];
+        st_rows<kRpt>(p, row, a.n, pv);
+    } else {
+        pv = ld<kRpt>(p + row);
+    }
+    Rows<kRpt> o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+    st_rows<kRpt>(a.Ap, row, a.n, o);
+    if (prologue) return;
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += pv.v[i] * o.v[i];
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
+}
+
+// SELL-512-C build: one block per slice. An LDS hash of the slice's distinct
+// (column - row) offsets gives the codes; with windows, ldsc[code] is the LDS
+// position of row 0's column for that offset, and every entry must agree.
+__global__ __launch_bounds__(256) void k_build_c(const unsigned int* __restrict__ slice_base, int nslices,
+                                                 const int* __restrict__ cols, const int* __restrict__ win_ptr,
+                                                 const int* __restrict__ win_start, const int* __restrict__ win_off,
+                                                 const int* __restrict__ win_len,
+                                                 unsigned char* __restrict__ codes, int* __restrict__ cdict,
+                                                 int* __restrict__ ldsc, int* ok)
+{
+    constexpr int kH = 1024;
+    constexpr int kEmpty = INT_MIN;
+    __shared__ int keys[kH];
+    __shared__ int code_of[kH];
+    __shared__ int sldsc[kCodes];
+    __shared__ int cnt;
+    const int s = blockIdx.x;
+    if (s >= nslices) return;
+    for (int h = threadIdx.x; h < kH; h += 256) keys[h] = kEmpty;
+    if (threadIdx.x == 0) cnt = 0;
+    for (int i = threadIdx.x; i < kCodes; i += 256) {
+        cdict[(size_t)s * kCodes + i] = 0;
+        sldsc[i] = kEmpty;
+    }
+    __syncthreads();
+    const int row0 = s * kSliceRows;
+    const size_t e0 = (size_t)slice_base[s] * kSliceRows, e1 = (size_t)slice_base[s + 1] * kSliceRows;
+    auto slot_of = [](int d) { return (int)(((unsigned)d * 2654435761u) >> 22); };  // 10 bits
+    for (size_t e = e0 + threadIdx.x; e < e1; e += 256) {
+        const int c = cols[e];
+        if (c < 0) continue;
+        const int d = c - (row0 + (int)((e - e0) % kSliceRows));
+        int h = slot_of(d);
+        for (int probe = 0; probe < kH; probe++) {
+            const int old = atomicCAS(&keys[h], kEmpty, d);
+            if (old == kEmpty || old == d) break;
+            h = (h + 1) & (kH - 1);
+        }
+    }
+    __syncthreads();
+    for (int h = threadIdx.x; h < kH; h += 256) {
+        if (keys[h] == kEmpty) continue;
+        const int code = atomicAdd(&cnt, 1);
+        code_of[h] = code;
+        if (code < kCodePad) cdict[(size_t)s * kCodes + code] = keys[h];
+    }
+    __syncthreads();
+    if (cnt > kCodePad) {
+        if (threadIdx.x == 0) ok[0] = 0;
+        return;
+    }
+    const int w0 = win_ptr ? win_ptr[s] : 0, w1 = win_ptr ? win_ptr[s + 1] : 0;
+    for (size_t e = e0 + threadIdx.x; e < e1; e += 256) {
+        const int c = cols[e];
+        if (c < 0) {
+            codes[e] = (unsigned char)kCodePad;
+            continue;
+        }
+        const int lane = (int)((e - e0) % kSliceRows);
+        const int d = c - (row0 + lane);
+        int h = slot_of(d);
+        while (keys[h] != d) h = (h + 1) & (kH - 1);
+        const int code = code_of[h];
+        codes[e] = (unsigned char)code;
+        if (ldsc) {
+            int w = w0;
+            while (w + 1 < w1 && win_start[w + 1] <= c) w++;
+            if (w >= w1 || c < win_start[w] || c >= win_start[w] + win_len[w]) {
+                ok[1] = 0;
+                continue;
+            }
+            const int pos0 = win_off[w] + (c - win_start[w]) - lane;  // position of lane 0's column
+            const int old = atomicCAS(&sldsc[code], kEmpty, pos0);
+            if (old != kEmpty && old != pos0) ok[1] = 0;
+        }
+    }
+    if (ldsc) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < kCodes; i += 256) ldsc[(size_t)s * kCodes + i] = sldsc[i];
+    }
+}
+
 template <int kRpt, int kW, int kMinW, bool kNT, bool kFuse>
 __global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, bool prologue)
 {
@@ -628,31 +817,61 @@ __device__ __forceinline__ void ld_lcols(const unsigned short* __restrict__ p, u
     }
 }
 
-template <int kRpt, bool kNT, int kPre, int kP>
-__device__ __forceinline__ void lds_prefetch(const double* __restrict__ vp, const unsigned short* __restrict__ cp,
-                                             int wdt, Rows<kRpt> (&vpre)[kP], unsigned (&cpre)[kP][kRpt])
+
+// Index stream of the LDS kernels: 16-bit LDS positions (SELL-512-L) or 1-byte
+// offset codes (SELL-512-C, position = lane + ldsc[code]).
+template <bool kCode>
+struct LdsIdx {
+    using T = typename std::conditional<kCode, unsigned char, unsigned short>::type;
+    static constexpr unsigned kPad = kCode ? kCodePad : kLdsPad;
+};
+
+template <int kRpt, bool kNT, bool kCode>
+__device__ __forceinline__ void ld_idx(const typename LdsIdx<kCode>::T* __restrict__ p, unsigned (&c)[kRpt])
+{
+    if constexpr (kCode)
+        ld_codes<kRpt, kNT>(p, c);
+    else
+        ld_lcols<kRpt, kNT>(p, c);
+}
+
+template <bool kCode>
+__device__ __forceinline__ int lds_pos(unsigned c, int lrow, const int* sldsc)
+{
+    if constexpr (kCode)
+        return lrow + sldsc[c];
+    else
+        return (int)c;
+}
+
+template <int kRpt, bool kNT, bool kCode, int kPre, int kP>
+__device__ __forceinline__ void lds_prefetch(const double* __restrict__ vp,
+                                             const typename LdsIdx<kCode>::T* __restrict__ cp, int wdt,
+                                             Rows<kRpt> (&vpre)[kP], unsigned (&cpre)[kP][kRpt])
 {
 #pragma unroll
     for (int j = 0; j < kPre; j++) {
         if (j < wdt) {
-            ld_lcols<kRpt, kNT>(cp + (size_t)j * kSliceRows, cpre[j]);
+            ld_idx<kRpt, kNT, kCode>(cp + (size_t)j * kSliceRows, cpre[j]);
             vpre[j] = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
         }
     }
 }
 
-template <int kRpt, bool kNT>
-__device__ __forceinline__ void lds_stream(const double* __restrict__ vp, const unsigned short* __restrict__ cp,
-                                           int j0, int wdt, const double* xs, double (&sum)[kRpt])
+template <int kRpt, bool kNT, bool kCode>
+__device__ __forceinline__ void lds_stream(const double* __restrict__ vp,
+                                           const typename LdsIdx<kCode>::T* __restrict__ cp, int j0, int wdt,
+                                           const double* xs, const int* sldsc, double (&sum)[kRpt])
 {
+    const int lrow = threadIdx.x * kRpt;
 #pragma unroll 3
     for (int j = j0; j < wdt; j++) {
         unsigned c[kRpt];
-        ld_lcols<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
+        ld_idx<kRpt, kNT, kCode>(cp + (size_t)j * kSliceRows, c);
         const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
 #pragma unroll
         for (int i = 0; i < kRpt; i++) {
-            const double xv = (c[i] != kLdsPad) ? xs[c[i]] : 0.0;
+            const double xv = (c[i] != LdsIdx<kCode>::kPad) ? xs[lds_pos<kCode>(c[i], lrow + i, sldsc)] : 0.0;
             sum[i] = sum[i] + v.v[i] * xv;
         }
     }
@@ -660,10 +879,12 @@ __device__ __forceinline__ void lds_stream(const double* __restrict__ vp, const 
 
 // kPre > 0: the first kPre slots of the matrix stream are loaded before the
 // window staging and its barrier, so the block's HBM stream starts at once.
-template <int kRpt, bool kNT, bool kFuse, int kPre>
+template <int kRpt, bool kNT, bool kFuse, int kPre, bool kCode = false>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool prologue)
 {
     extern __shared__ __attribute__((aligned(16))) double xs[];
+    __shared__ int sldsc[kCode ? kCodes : 1];
+    using IdxT = typename LdsIdx<kCode>::T;
     int k = 0;
     if (!prologue) {
         k = a.kst[0];
@@ -684,7 +905,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     const size_t base = (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
     const int wdt = (int)(a.slice_base[s + 1] - a.slice_base[s]);
     const double* __restrict__ vp = a.vals + base;
-    const unsigned short* __restrict__ cp = a.lcols + base;
+    const IdxT* __restrict__ cp = (kCode ? (const IdxT*)(const void*)a.ccodes : (const IdxT*)(const void*)a.lcols) + base;
     constexpr int kP = kPre > 0 ? kPre : 1;
     unsigned cpre[kP][kRpt];
     Rows<kRpt> vpre[kP];
@@ -693,9 +914,11 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     // spread evenly over the XCDs), the rest non-temporal
     const bool nt = kNT && (s % (a.grid / kNumXcd)) >= a.nt_split;
     if (nt)
-        lds_prefetch<kRpt, true, kPre>(vp, cp, wdt, vpre, cpre);
+        lds_prefetch<kRpt, true, kCode, kPre>(vp, cp, wdt, vpre, cpre);
     else
-        lds_prefetch<kRpt, false, kPre>(vp, cp, wdt, vpre, cpre);
+        lds_prefetch<kRpt, false, kCode, kPre>(vp, cp, wdt, vpre, cpre);
+    if constexpr (kCode)
+        for (int i = threadIdx.x; i < kCodes; i += kSliceRows / kRpt) sldsc[i] = a.ldsc[(size_t)s * kCodes + i];
     // stage the windows; with kFuse the staged value of an own row is
     // p_k = r + beta*p_{k-1}, the exact expression k_p_update stores
     double beta = 0.0;
@@ -726,15 +949,17 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
         if (j < wdt) {
 #pragma unroll
             for (int i = 0; i < kRpt; i++) {
-                const double xv = (cpre[j][i] != kLdsPad) ? xs[cpre[j][i]] : 0.0;
+                const double xv = (cpre[j][i] != LdsIdx<kCode>::kPad)
+                                      ? xs[lds_pos<kCode>(cpre[j][i], threadIdx.x * kRpt + i, sldsc)]
+                                      : 0.0;
                 sum[i] = sum[i] + vpre[j].v[i] * xv;
             }
         }
     }
     if (nt)
-        lds_stream<kRpt, true>(vp, cp, kPre, wdt, xs, sum);
+        lds_stream<kRpt, true, kCode>(vp, cp, kPre, wdt, xs, sldsc, sum);
     else
-        lds_stream<kRpt, false>(vp, cp, kPre, wdt, xs, sum);
+        lds_stream<kRpt, false, kCode>(vp, cp, kPre, wdt, xs, sldsc, sum);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     Rows<kRpt> o;
 #pragma unroll
@@ -1088,6 +1313,15 @@ void launch_cg_p_update(const CgArgs& a, hipStream_t s)
     hipLaunchKernelGGL(k_p_update<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
 }
 
+void launch_build_c(const unsigned int* slice_base, int nslices, const int* cols, const int* win_ptr,
+                    const int* win_start, const int* win_off, const int* win_len, unsigned char* codes,
+                    int* cdict, int* ldsc, int* ok, hipStream_t s)
+{
+    if (nslices <= 0) return;
+    hipLaunchKernelGGL(k_build_c, dim3(nslices), dim3(256), 0, s, slice_base, nslices, cols, win_ptr, win_start,
+                       win_off, win_len, codes, cdict, ldsc, ok);
+}
+
 void launch_cg_pack(const CgArgs& a, const int* idx, int cnt, double* buf, bool prologue, hipStream_t s)
 {
     if (cnt <= 0) return;
@@ -1121,22 +1355,33 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
             hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, false>), dim3(a.grid),                    \
                                dim3(kSliceRows / RPT), 0, s, a, prologue);                          \
     } while (0)
-#define HPCCG_SPMV_LDS(RPT, NT, PRE)                                                               \
+#define HPCCG_SPMV_C(RPT, NT)                                                                      \
+    do {                                                                                           \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_c<RPT, NT, true>), dim3(a.grid), dim3(kSliceRows / RPT), 0, s, a, \
+                               prologue);                                                          \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_c<RPT, NT, false>), dim3(a.grid), dim3(kSliceRows / RPT), 0, s, a, \
+                               prologue);                                                          \
+    } while (0)
+#define HPCCG_SPMV_LDSX(RPT, NT, PRE, CODE)                                                        \
     do {                                                                                           \
         const size_t smem = (size_t)a.lds_doubles * sizeof(double);                                \
         if (a.fuse_p && !prologue)                                                                 \
-            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, true, PRE>), dim3(a.grid), dim3(kSliceRows / RPT), \
+            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, true, PRE, CODE>), dim3(a.grid), dim3(kSliceRows / RPT), \
                                smem, s, a, prologue);                                              \
         else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, false, PRE>), dim3(a.grid), dim3(kSliceRows / RPT), \
+            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, false, PRE, CODE>), dim3(a.grid), dim3(kSliceRows / RPT), \
                                smem, s, a, prologue);                                              \
     } while (0)
+#define HPCCG_SPMV_LDS(RPT, NT, PRE) HPCCG_SPMV_LDSX(RPT, NT, PRE, false)
 bool spmv_variant_ok(int v)
 {
     switch (v) {
     case 0: case 1: case 2: case 27: case 7: case 327: case 427:
     case 1000: case 1001: case 1002: case 1027: case 1007: case 9999:
     case 2000: case 2001: case 2002: case 2100: case 2200: case 2208: case 2300: case 2308:
+    case 3000: case 3001: case 3002: case 3100: case 4000: case 4200: case 4300:
         return true;
     default:
         return false;
@@ -1166,11 +1411,20 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 2208: HPCCG_SPMV_LDS(2, true, 8); break;
     case 2300: HPCCG_SPMV_LDS(2, false, 4); break;
     case 2308: HPCCG_SPMV_LDS(2, false, 8); break;
+    case 4200: HPCCG_SPMV_LDSX(2, true, 4, true); break;
+    case 4300: HPCCG_SPMV_LDSX(2, false, 4, true); break;
+    case 4000: HPCCG_SPMV_LDSX(2, true, 0, true); break;
+    case 3000: HPCCG_SPMV_C(2, true); break;
+    case 3001: HPCCG_SPMV_C(1, true); break;
+    case 3002: HPCCG_SPMV_C(4, true); break;
+    case 3100: HPCCG_SPMV_C(2, false); break;
     default: HPCCG_SPMV(2, 0, 1, false); break;
     }
 }
 #undef HPCCG_SPMV
 #undef HPCCG_SPMV_LDS
+#undef HPCCG_SPMV_LDSX
+#undef HPCCG_SPMV_C
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
 {

@@ -217,6 +217,10 @@ struct hpccg_hip_matrix {
     // SELL-512-L (LDS-staged x windows)
     int has_lds = 0, lds_doubles = 0, nwin = 0;
     unsigned short* d_lcols = nullptr;
+    // SELL-512-C (per-slice offset dictionary + 1-byte codes)
+    int has_c = 0, has_c_lds = 0;
+    unsigned char* d_ccodes = nullptr;
+    int *d_cdict = nullptr, *d_ldsc = nullptr;
     int *d_win_ptr = nullptr, *d_win_start = nullptr, *d_win_len = nullptr, *d_win_off = nullptr;
     // workspace (padded to a multiple of kSliceRows rows)
     size_t npad = 0;
@@ -266,7 +270,7 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_tickets,
                     M->d_kst,        M->d_hist,    M->d_stamps, M->d_ddot_partial, M->d_gen_b,
                     M->d_gen_x0,     M->d_gen_xexact, M->d_lcols, M->d_win_ptr, M->d_win_start,
-                    M->d_win_len,    M->d_win_off, M->d_send_idx, M->d_send_buf};
+                    M->d_win_len,    M->d_win_off, M->d_send_idx, M->d_send_buf, M->d_ccodes, M->d_cdict, M->d_ldsc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -488,6 +492,41 @@ int exchange_plan(hpccg_hip_matrix* M, int* mode = nullptr, std::vector<int>* al
     return 0;
 }
 
+// SELL-512-C from the uploaded SELL-512 cols (and windows, if any) on the
+// device; dropped when a slice has more than 255 distinct offsets, LDS form
+// dropped when a code's entries fall in different windows.
+int build_c_image(hpccg_hip_matrix* M)
+{
+    const size_t ndict = (size_t)std::max(1, M->nslices) * kCodes;
+    HIP_TRY(hipMalloc(&M->d_ccodes, std::max<size_t>(1, (size_t)M->nslots)));
+    HIP_TRY(hipMalloc(&M->d_cdict, sizeof(int) * ndict));
+    if (M->has_lds) HIP_TRY(hipMalloc(&M->d_ldsc, sizeof(int) * ndict));
+    int* d_ok = nullptr;
+    HIP_TRY(hipMalloc(&d_ok, sizeof(int) * 2));
+    const int ones[2] = {1, 1};
+    HIP_TRY(hipMemcpyAsync(d_ok, ones, sizeof ones, hipMemcpyHostToDevice, M->stream));
+    launch_build_c(M->d_slice_base, M->nslices, M->d_cols, M->has_lds ? M->d_win_ptr : nullptr, M->d_win_start,
+                   M->d_win_off, M->d_win_len, M->d_ccodes, M->d_cdict, M->d_ldsc, d_ok, M->stream);
+    HIP_TRY(hipGetLastError());
+    int ok[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(ok, d_ok, sizeof ok, hipMemcpyDeviceToHost, M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    (void)hipFree(d_ok);
+    M->has_c = ok[0];
+    M->has_c_lds = ok[0] && ok[1] && M->has_lds;
+    if (!M->has_c_lds && M->d_ldsc) {
+        (void)hipFree(M->d_ldsc);
+        M->d_ldsc = nullptr;
+    }
+    if (!M->has_c) {
+        (void)hipFree(M->d_ccodes);
+        (void)hipFree(M->d_cdict);
+        M->d_ccodes = nullptr;
+        M->d_cdict = nullptr;
+    }
+    return 0;
+}
+
 int alloc_workspace(hpccg_hip_matrix* M)
 {
     M->npad = (size_t)M->nslices * kSliceRows;
@@ -549,8 +588,20 @@ int choose_variant(const hpccg_hip_matrix* M)
     const bool lds = M->has_lds && (double)M->nnz / rows >= 2.5 * M->lds_doubles / (double)kSliceRows;
     const double image = (double)M->nslots * (lds ? 10.0 : 12.0);
     const bool big = image > 180e6;
-    if (lds) return big ? 2200 : 2300;
+    // SELL-512-C (1-byte offset codes, 9 B per slot) where the image allows it:
+    // 200^3 in-CG SpMV 407-414 vs 433 us (LDS), 7-pt 256^3 265-272 vs 328-340 us
+    if (lds) return M->has_c_lds ? 4200 : (big ? 2200 : 2300);
+    if (M->has_c) return big ? 3000 : 3100;
     return big ? 1000 : 0;
+}
+
+// Matrix-stream bytes per stored slot of the kernel in use.
+double slot_bytes(const hpccg_hip_matrix* M)
+{
+    const int v = M->spmv_variant;
+    if ((v >= 3000 && v < 5000)) return 9.0;
+    if (v >= 2000 && v < 3000) return 10.0;
+    return 12.0;
 }
 
 // resident_mb auto: an NT image not far above the 256 MB Infinity Cache keeps
@@ -560,7 +611,7 @@ int choose_variant(const hpccg_hip_matrix* M)
 long long resident_mb_effective(const hpccg_hip_matrix* M)
 {
     if (M->resident_mb >= 0) return M->resident_mb;
-    const double image = (double)M->nslots * (M->has_lds ? 10.0 : 12.0);
+    const double image = (double)M->nslots * slot_bytes(M);
     return image <= 400e6 ? 128 : 0;
 }
 
@@ -572,8 +623,10 @@ long long resident_mb_effective(const hpccg_hip_matrix* M)
 bool fuse_p_effective(const hpccg_hip_matrix* M)
 {
     if (M->spmv_variant == 9999) return false;
-    if (M->nranks != 1 && M->spmv_variant < 2000) return false;
-    if (M->fuse_p < 0) return M->spmv_variant >= 2000;
+    const int v = M->spmv_variant;
+    const bool lds = (v >= 2000 && v < 3000) || (v >= 4000 && v < 5000);
+    if (M->nranks != 1 && !lds) return false;
+    if (M->fuse_p < 0) return lds;
     return M->fuse_p != 0;
 }
 
@@ -608,7 +661,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.xdefer = M->x_defer ? 1 : 0;
     a.rev = M->rev_update ? 1 : 0;
     {
-        const double per_slice = (double)M->nslots / std::max(1, M->nslices) * (M->has_lds ? 10.0 : 12.0);
+        const double per_slice = (double)M->nslots / std::max(1, M->nslices) * slot_bytes(M);
         const double sl = (double)resident_mb_effective(M) * 1e6 / std::max(1.0, per_slice);
         a.nt_split = (int)std::min<double>(M->grid / kNumXcd, sl / kNumXcd);
     }
@@ -628,6 +681,9 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.cols = M->d_cols;
     a.vals = M->d_vals;
     a.lcols = M->d_lcols;
+    a.ccodes = M->d_ccodes;
+    a.cdict = M->d_cdict;
+    a.ldsc = M->d_ldsc;
     a.win_ptr = M->d_win_ptr;
     a.win_start = M->d_win_start;
     a.win_len = M->d_win_len;
@@ -1313,6 +1369,7 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
             HIP_TRY(hipMalloc(&M->d_lcols, sizeof(unsigned short) * lc.size()));
             HIP_TRY(hipMemcpy(M->d_lcols, lc.data(), sizeof(unsigned short) * lc.size(), hipMemcpyHostToDevice));
         }
+        TRY(build_c_image(M));
         M->spmv_variant = choose_variant(M);
         return alloc_workspace(M);
     }();
@@ -1625,12 +1682,13 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
         HIP_TRY(hipMemset(M->d_gen_b, 0, sizeof(double) * M->npad));
         HIP_TRY(hipMemset(M->d_gen_x0, 0, sizeof(double) * M->npad));
         HIP_TRY(hipMemset(M->d_gen_xexact, 0, sizeof(double) * M->npad));
-        M->spmv_variant = choose_variant(M);
         launch_generate(nx, ny, nz, rank, size, use_7pt, start - M->ghost_lo, M->d_slice_base, M->d_cols,
                         M->d_vals, M->d_gen_b, M->d_gen_xexact, n, M->d_win_ptr, M->d_win_start,
                         M->d_win_len, M->d_win_off, M->d_lcols, M->stream);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipStreamSynchronize(M->stream));
+        TRY(build_c_image(M));
+        M->spmv_variant = choose_variant(M);
         return 0;
     }();
     if (rc) {
@@ -1780,6 +1838,10 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
             return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform width-%d SELL image", v, w);
         if (v >= 2000 && v < 3000 && !M->has_lds)
             return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-L windows (not built)", v);
+        if (v >= 3000 && v < 4000 && !M->has_c)
+            return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-C image (not built)", v);
+        if (v >= 4000 && v < 5000 && !M->has_c_lds)
+            return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-C LDS image (not built)", v);
         M->spmv_variant = v;
     } else {
         return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
@@ -1831,6 +1893,10 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_
     if (!spmv_variant_ok(variant)) return set_err(HPCCG_HIP_EINVAL, "unknown variant %d", variant);
     if (variant >= 2000 && variant < 3000 && !M->has_lds)
         return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-L windows", variant);
+    if (variant >= 3000 && variant < 4000 && !M->has_c)
+        return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-C image", variant);
+    if (variant >= 4000 && variant < 5000 && !M->has_c_lds)
+        return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-C LDS image", variant);
     if ((w == 27 || w == 7 || variant == 9999) && !(M->uniform && M->width == (variant == 9999 ? 27 : w)))
         return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform SELL image of that width", variant);
     HIP_TRY(hipSetDevice(M->device));

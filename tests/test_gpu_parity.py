@@ -53,7 +53,8 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 1000, 1001, 1002, 1027, 2000, 2001,
-                                     2002, 2100, 2200, 2208, 2300, 2308])
+                                     2002, 2100, 2200, 2208, 2300, 2308, 3000, 3001, 3002, 3100,
+                                     4000, 4200, 4300])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
@@ -68,7 +69,7 @@ def test_sparsemv_variants_agree(hp, gpu, variant):
     x0 = prob.x
     _, it0, nr0, _ = hp.HPCCG(M, prob.b, x0, max_iter=60)
     assert it == it0
-    if variant in (1, 2, 1001, 1002, 2001, 2002):
+    if variant in (1, 2, 1001, 1002, 2001, 2002, 3001, 3002):
         assert check_trace(tr, M.last_trace(), RTRANS_RTOL_1GPU) > 10
     else:
         assert nr == nr0
@@ -104,7 +105,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # and the LDS kernels (same rows per thread), fused or not, give the same bits
-    for v, fuse in itertools.product((2000, 2100, 2200, 2308), (0, 1)):
+    for v, fuse in itertools.product((2000, 2100, 2200, 2308, 3000, 3100, 4200, 4300), (0, 1)):
         M.set_option("spmv_variant", v)
         M.set_option("fuse_p", fuse)
         M.set_option("resident_mb", fuse)  # 1 MB on default-policy loads: no value changes
@@ -368,3 +369,42 @@ def test_7pt_256_properties(hp, gpu):
     assert it == 499
     assert nr / tr[0] <= 1e-15
     assert (x - 1.0).abs().max().item() <= 1e-12
+
+
+def test_sell_c_fallback_for_many_offsets(hp, gpu):
+    """SELL-512-C codes a slice's (column - row) offsets with one byte; a slice
+    with more than 255 distinct offsets cannot, and the library falls back to
+    the int32 SELL-512 kernels (same bits either way)."""
+    n = 20000
+    rows_c, rows_v = [], []
+    for i in range(n):
+        far = (i * 7919 + 13) % n  # a different offset on every row
+        nb = [c for c in (i - 1, i + 1) if 0 <= c < n]
+        cols = [i] + nb + ([far] if far not in nb and far != i else [])
+        rows_c.append(cols)
+        rows_v.append([6.0 if c == i else -1.0 for c in cols])
+    # make it symmetric: add the transpose of the far couplings
+    extra = {}
+    for i in range(n):
+        for c in rows_c[i][3:]:
+            extra.setdefault(c, []).append(i)
+    for c, lst in extra.items():
+        for i in lst:
+            if i not in rows_c[c]:
+                rows_c[c].append(i)
+                rows_v[c].append(-1.0)
+        rows_v[c][0] = 2.0 + len(rows_c[c])
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum([len(c) for c in rows_c])
+    cols = np.array([c for r in rows_c for c in r], np.int32)
+    vals = np.array([v for r in rows_v for v in r], np.float64)
+    M = hp.Matrix.from_csr(rp, cols, vals)
+    assert M.get_option("spmv_variant") < 3000  # no SELL-512-C for this image
+    with pytest.raises(hp.HPCCGError, match="SELL-512-C"):
+        M.set_option("spmv_variant", 3000)
+    b = 1.0 + (np.arange(n) % 5)
+    x = np.zeros(n)
+    _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=30)
+    A = oracle.CSR(rp, cols, vals, np.zeros(n), b, np.zeros(n))
+    ref = oracle.hpccg(A, max_iter=30)
+    assert check_trace(M.last_trace(), ref["trace"], RTRANS_RTOL_1GPU) >= 5

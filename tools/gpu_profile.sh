@@ -6,8 +6,8 @@
 set -u
 export TMPDIR=/tmp
 N=${N:-200}
-OUT=gpurun_out/prof_$N
-mkdir -p $OUT
+OUT=gpurun_out/prof_$N${STENCIL:+_$STENCIL}
+rm -rf $OUT; mkdir -p $OUT
 step() {
     local name=$1 secs=$2; shift 2
     timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2> "$OUT/$name.err"
@@ -17,7 +17,8 @@ step() {
     return 0
 }
 
-step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --steps 2 --warmup 1 --no-cpu-baseline
-step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python tools/pmc_workload.py --n $N
-step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python tools/pmc_workload.py --n $N
+S=${STENCIL:-27}
+step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --stencil $S --steps 2 --warmup 1 --no-cpu-baseline
+step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python tools/pmc_workload.py --n $N --stencil $S
+step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python tools/pmc_workload.py --n $N --stencil $S
 find $OUT -name "*.csv" | head -20

@@ -9,7 +9,7 @@
   12 * sell_slots bytes (vals fp64 + cols int32, 16 B / 8 B per lane, the
   SpMV's own matrix access pattern) and writes 8 * nrow.
 
-usage: tools/pmc_summary.py <prof_dir> <tag> <nx> [<bench_json_log>]
+usage: tools/pmc_summary.py <prof_dir> <tag> <nx> [<bench_json_log>] [<stencil 27|7>]
 """
 import csv
 import glob
@@ -20,6 +20,14 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def newest(pattern):
+    """The most recent file matching pattern (gpurun_out keeps older runs)."""
+    files = glob.glob(pattern)
+    if not files:
+        raise FileNotFoundError(pattern)
+    return max(files, key=os.path.getmtime)
 
 
 def counters(path):
@@ -47,34 +55,41 @@ def main():
     bench_log = sys.argv[4] if len(sys.argv) > 4 else None
     outdir = os.path.join(ROOT, "profiles", tag)
     os.makedirs(outdir, exist_ok=True)
-    stats = glob.glob(os.path.join(prof, "stats", "*", "*_kernel_stats.csv"))[0]
+    stats = newest(os.path.join(prof, "stats", "*", "*_kernel_stats.csv"))
     shutil.copy(stats, os.path.join(outdir, "kernel_stats.csv"))
     dom = glob.glob(os.path.join(prof, "stats", "*", "*_domain_stats.csv"))
     if dom:
-        shutil.copy(dom[0], os.path.join(outdir, "domain_stats.csv"))
-    fetch = counters(glob.glob(os.path.join(prof, "fetch", "*", "*_counter_collection.csv"))[0])
-    write = counters(glob.glob(os.path.join(prof, "write", "*", "*_counter_collection.csv"))[0])
+        shutil.copy(newest(os.path.join(prof, "stats", "*", "*_domain_stats.csv")),
+                    os.path.join(outdir, "domain_stats.csv"))
+    fetch = counters(newest(os.path.join(prof, "fetch", "*", "*_counter_collection.csv")))
+    write = counters(newest(os.path.join(prof, "write", "*", "*_counter_collection.csv")))
     for src, name in [("fetch", "pmc_fetch_size.csv"), ("write", "pmc_write_size.csv")]:
-        shutil.copy(glob.glob(os.path.join(prof, src, "*", "*_counter_collection.csv"))[0],
+        shutil.copy(newest(os.path.join(prof, src, "*", "*_counter_collection.csv")),
                     os.path.join(outdir, name))
 
+    stencil = int(sys.argv[5]) if len(sys.argv) > 5 else 27
     nrow = n ** 3
-    # SELL-512 uniform width 27 image of the 27-pt problem
-    slots = ((nrow + 511) // 512) * 512 * 27
-    nnz = (3 * n - 2) ** 3
-    stream_read = 12.0 * slots  # k_stream_diag reads the 12 B/slot SELL-512 image
-    f_stream, _ = pick(fetch, "k_stream_diag", "FETCH_SIZE")
-    w_stream, _ = pick(write, "k_stream_diag", "WRITE_SIZE")
-    fetch_factor = stream_read / (f_stream * 1024.0)
-    SPMV = ("k_spmv<", "k_spmv_lds<")
+    # SELL-512 uniform image of the stencil problem
+    width = 27 if stencil == 27 else 7
+    slots = ((nrow + 511) // 512) * 512 * width
+    nnz = (3 * n - 2) ** 3 if stencil == 27 else 7 * n ** 3 - 6 * n * n
+    if stencil == 27:
+        stream_read = 12.0 * slots  # k_stream_diag reads the 12 B/slot SELL-512 image
+        f_stream, _ = pick(fetch, "k_stream_diag", "FETCH_SIZE")
+        w_stream, _ = pick(write, "k_stream_diag", "WRITE_SIZE")
+        fetch_factor = stream_read / (f_stream * 1024.0)
+    else:  # no width-27 image to stream: the factor the 27-pt calibrations measure (2.0)
+        stream_read, f_stream, w_stream, fetch_factor = None, None, None, 2.0
+    SPMV = ("k_spmv<", "k_spmv_lds<", "k_spmv_c<")
     f_spmv, kname = pick(fetch, SPMV, "FETCH_SIZE")
     w_spmv, _ = pick(write, SPMV, "WRITE_SIZE")
     spmv_read = f_spmv * 1024.0 * fetch_factor
     spmv_write = w_spmv * 1024.0
     import re
     targs = re.search(r"k_spmv\w*<([^>]*)>", kname).group(1).split(",")
-    # k_spmv<kRpt, kW, kMinW, kNT, kFuse>, k_spmv_lds<kRpt, kNT, kFuse, kPre>
-    fuse_p = (targs[2] if "k_spmv_lds" in kname else targs[-1]).strip() == "true"
+    # k_spmv<kRpt, kW, kMinW, kNT, kFuse>, k_spmv_lds<kRpt, kNT, kFuse, kPre, kCode>,
+    # k_spmv_c<kRpt, kNT, kFuse>
+    fuse_p = (targs[2] if ("k_spmv_lds" in kname or "k_spmv_c" in kname) else targs[-1]).strip() == "true"
     algo = 12.0 * nnz + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fuse_p else 0.0)
 
     avg_ns = None
@@ -84,8 +99,9 @@ def main():
             avg_ns, calls = float(row["AverageNs"]), int(row["Calls"])
     out = {
         "tag": tag,
-        "problem": f"27-pt {n}^3, SELL-512 width 27 ({slots} slots, nnz {nnz}); "
-                   "k_spmv_lds reads the SELL-512-L image (8 B value + 2 B index per slot)",
+        "problem": f"{stencil}-pt {n}^3, SELL-512 width {width} ({slots} slots, nnz {nnz}); "
+                   "k_spmv_lds<..., true> streams the SELL-512-C image (8 B value + 1 B offset code "
+                   "per slot, x from LDS windows)",
         "kernel": kname,
         "fuse_p": fuse_p,
         "bytes_formula": "12 nnz + 20 n + 16 n" + (" + 24 n" if fuse_p else ""),
@@ -120,7 +136,7 @@ def main():
             out["bench_avg_launch_us"] = b["roofline"]["avg_launch_us"]
             out["bench_value"] = b["value"]
             shutil.copy(bench_log, os.path.join(outdir, "bench_under_rocprof.json"))
-    with open(os.path.join(ROOT, "profiles", f"pmc_spmv_27pt_{n}.json"), "w") as f:
+    with open(os.path.join(ROOT, "profiles", f"pmc_spmv_{stencil}pt_{n}.json"), "w") as f:
         json.dump(out, f, indent=1)
     with open(os.path.join(outdir, "summary.json"), "w") as f:
         json.dump(out, f, indent=1)

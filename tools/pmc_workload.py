@@ -12,12 +12,14 @@ from bench import load_pkg  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=200)
 ap.add_argument("--iters", type=int, default=12)
+ap.add_argument("--stencil", type=int, default=27, choices=[27, 7])
 args = ap.parse_args()
 import torch  # noqa: E402,F401
 hp = load_pkg()
 hp.set_device(0)
-M = hp.Matrix.generate(args.n, args.n, args.n)
-M.diag_spmv(9999, 3)
+M = hp.Matrix.generate(args.n, args.n, args.n, use_7pt=args.stencil == 7)
+if args.stencil == 27:
+    M.diag_spmv(9999, 3)  # known-bytes stream of the uniform width-27 image (FETCH calibration)
 b, _, _ = M.vectors()
 x = torch.zeros(args.n ** 3, dtype=torch.float64, device="cuda:0")
 M.set_option("use_graph", 0)
