@@ -212,8 +212,9 @@ def test_solve_vs_reference(hp, gpu, golden, name, how):
     assert tr[0] == ref_tr[0]  # KAT-2: integer-valued rtrans_0, exact in any order
     assert tr[1] == ref_tr[1]  # normr after iteration 1 is sqrt(rtrans_0) (HPCCG.cpp:371)
     # KAT-3: p = r_0 and A p are integer-valued, alpha_1 a correctly rounded quotient, so
-    # r_1 matches elementwise and r_1.r_1 differs only by summation order (~1 ulp per level)
-    assert abs(tr[2] ** 2 - ref_tr[2] ** 2) <= 1e-13 * ref_tr[2] ** 2
+    # r_1 matches elementwise and r_1.r_1 (a sum of n positive terms) differs only by the
+    # summation order: the reference's serial sum is within (n-1) u of the exact value
+    assert abs(tr[2] ** 2 - ref_tr[2] ** 2) <= 2 * n * 2.0 ** -53 * ref_tr[2] ** 2
     assert check_trace(tr, ref_tr, RTRANS_RTOL_1GPU) >= 5
     for mi, rr in c["runs"].items():
         it, nr, times, x = run(int(mi))
