@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--variant", type=int, default=-1, help="SpMV kernel variant (-1 auto)")
     ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1 default)")
     ap.add_argument("--fold", type=int, default=-1, help="last-block dot completion (-1 default)")
+    ap.add_argument("--redund", type=int, default=-1,
+                    help="consumers complete the dot products themselves (-1 default)")
     ap.add_argument("--x-defer", type=int, default=-1, help="batched x update (-1 default)")
     ap.add_argument("--resident-mb", type=int, default=-1,
                     help="MB of the matrix image streamed with default-policy loads (-1 default)")
@@ -160,6 +162,8 @@ def main():
         M.set_option("fuse_p", args.fuse_p)
     if args.fold >= 0:
         M.set_option("fold", args.fold)
+    if args.redund >= 0:
+        M.set_option("redund", args.redund)
     if args.x_defer >= 0:
         M.set_option("x_defer", args.x_defer)
     if args.rev_update >= 0:

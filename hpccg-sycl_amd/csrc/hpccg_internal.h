@@ -48,6 +48,8 @@ struct CgArgs {
     int nring;             // p_k lives in ring buffer k % nring (1 = in place)
     int xdefer;            // 1: x += alpha_j p_j applied every nring iterations
     int rev;               // 1: the update kernel walks each XCD's slices backwards
+    int redund;            // 1: no finalize kernels: consumers sum the producers' partials themselves
+    int ugrid;             // k_update_g grid (groups rounded up to a multiple of kNumXcd)
     int nt_split;          // NT matrix kernels: per XCD, this many leading slices use default-policy loads
     double* ahist;         // [max_iter + 1]: alpha_k (for the deferred x update)
     int fuse_p;            // 1: p = r + beta p computed inside the SpMV (single rank)

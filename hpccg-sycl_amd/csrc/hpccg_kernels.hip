@@ -120,12 +120,12 @@ __device__ __forceinline__ void mark_end(const CgArgs& a)
 // where normr is the value computed in iteration k-1, i.e. sqrt(r_{k-2}.r_{k-2})
 // (sqrt(r_0.r_0) for k = 1). hist[j] = r_j.r_j is filled by the p-update
 // kernel of iteration j+1; that kernel itself reads r_{k-1}.r_{k-1} from g.
-__device__ __forceinline__ bool cg_run(const CgArgs& a, int k, bool in_p_update)
+__device__ __forceinline__ bool cg_run(const CgArgs& a, int k, bool in_p_update, double rr = 0.0)
 {
     if (k >= a.max_iter) return false;
     double chk;
     if (k == 1)
-        chk = in_p_update ? a.g[kRR] : a.hist[0];
+        chk = in_p_update ? rr : a.hist[0];
     else
         chk = a.hist[k - 2];
     return sqrt(chk) > a.tol;
@@ -332,6 +332,18 @@ __device__ __forceinline__ double top_sum_wave(Ld ld, int ng, int lane)
     return s;
 }
 
+// r_{k-1}.r_{k-1} from the update's group sums, in every thread (redund mode),
+// else g[kRR].
+__device__ __forceinline__ double cur_rr(const CgArgs& a)
+{
+    if (!a.redund) return a.g[kRR];
+    const int ng = ngroups_of(a);
+    const double* gp = a.partial + a.nslices + kRR * ng;
+    const int lane = threadIdx.x & (kWave - 1);
+    const double v = top_sum_wave([gp](int i) { return gp[i]; }, ng, lane);
+    return __shfl(v, 0, kWave);
+}
+
 __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which, int kfinal)
 {
     a.loc[which] = s;
@@ -417,9 +429,10 @@ template <int kRpt>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_p_update(CgArgs a)
 {
     const int k = a.kst[0];
-    const bool run = cg_run(a, k, true);
+    const double rr = cur_rr(a);
+    const bool run = cg_run(a, k, true, rr);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (k == 1 || run) a.hist[k - 1] = a.g[kRR];
+        if (k == 1 || run) a.hist[k - 1] = rr;
         if (run)
             stamp(a, kStampPUpdate);
         else
@@ -429,7 +442,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_p_update(CgArgs a)
     const int s = xcd_slice(a.grid);
     if (s >= a.nslices) return;
     const int row = s * kSliceRows + threadIdx.x * kRpt;
-    const double beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+    const double beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
     const Rows<kRpt> rv = ld<kRpt>(a.r + row);
     const Rows<kRpt> yv = (k == 1) ? rv : ld<kRpt>(cur_p(a, k - 1) + row);
     Rows<kRpt> o;
@@ -445,11 +458,12 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_p_update(CgArgs a)
 __global__ __launch_bounds__(256) void k_p_boundary(CgArgs a, int nlo, int nhi)
 {
     const int k = a.kst[0];
-    if (!cg_run(a, k, true)) return;
+    const double rr = cur_rr(a);
+    if (!cg_run(a, k, true, rr)) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= nlo + nhi) return;
     const int row = i < nlo ? i : a.n - nhi + (i - nlo);
-    const double beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+    const double beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
     const double rv = a.r[row];
     const double yv = (k == 1) ? rv : cur_p(a, k - 1)[row];
     cur_p(a, k)[row] = rv + beta * yv;
@@ -463,9 +477,11 @@ __global__ __launch_bounds__(256) void k_pack(CgArgs a, const int* __restrict__ 
                                               double* __restrict__ buf, bool prologue)
 {
     int k = 0;
+    double rr = 0.0;
     if (!prologue) {
         k = a.kst[0];
-        if (!cg_run(a, k, true)) return;
+        rr = cur_rr(a);
+        if (!cg_run(a, k, true, rr)) return;
     }
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= cnt) return;
@@ -474,7 +490,7 @@ __global__ __launch_bounds__(256) void k_pack(CgArgs a, const int* __restrict__ 
     if (prologue) {
         v = a.p[e];
     } else if (a.fuse_p) {
-        const double beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+        const double beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
         const double rv = a.r[e];
         const double yv = (k == 1) ? rv : cur_p(a, k - 1)[e];
         v = rv + beta * yv;
@@ -581,11 +597,13 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool pro
 {
     __shared__ int sdict[kCodes];
     int k = 0;
+    double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
     if (!prologue) {
         k = a.kst[0];
-        const bool run = cg_run(a, k, kFuse);
+        if (kFuse) rr = cur_rr(a);
+        const bool run = cg_run(a, k, kFuse, rr);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            if (kFuse && (k == 1 || run)) a.hist[k - 1] = a.g[kRR];
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = rr;
             if (run)
                 stamp(a, kStampSpmv);
             else
@@ -607,7 +625,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool pro
     double beta = 0.0;
     const double* pold = a.r;
     if constexpr (kFuse) {
-        beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+        beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
         pold = (k == 1) ? a.r : cur_p(a, k - 1);
     }
     const double* __restrict__ xext = p - a.ghost_lo;
@@ -714,7 +732,12 @@ __global__ __launch_bounds__(256) void k_build_c(const unsigned int* __restrict_
         const int lane = (int)((e - e0) % kSliceRows);
         const int d = c - (row0 + lane);
         int h = slot_of(d);
-        while (keys[h] != d) h = (h + 1) & (kH - 1);
+        int probe = 0;
+        while (keys[h] != d && probe++ < kH) h = (h + 1) & (kH - 1);  // present: <= 255 keys inserted
+        if (keys[h] != d) {
+            ok[0] = 0;
+            continue;
+        }
         const int code = code_of[h];
         codes[e] = (unsigned char)code;
         if (ldsc) {
@@ -739,11 +762,13 @@ template <int kRpt, int kW, int kMinW, bool kNT, bool kFuse>
 __global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, bool prologue)
 {
     int k = 0;
+    double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
     if (!prologue) {
         k = a.kst[0];
-        const bool run = cg_run(a, k, kFuse);
+        if (kFuse) rr = cur_rr(a);
+        const bool run = cg_run(a, k, kFuse, rr);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            if (kFuse && (k == 1 || run)) a.hist[k - 1] = a.g[kRR];
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = rr;
             if (run)
                 stamp(a, kStampSpmv);
             else
@@ -759,7 +784,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, boo
     Rows<kRpt> pv;
     if constexpr (kFuse) {
         // beta and p_{k-1} exactly as k_p_update uses them
-        const double beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+        const double beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
         const double* pold = (k == 1) ? a.r : cur_p(a, k - 1);
         const GatherRP gat{a.r, pold, beta};
         spmv_rows<kRpt, kW, kNT>(a, gat, s, sum);
@@ -886,11 +911,13 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     __shared__ int sldsc[kCode ? kCodes : 1];
     using IdxT = typename LdsIdx<kCode>::T;
     int k = 0;
+    double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
     if (!prologue) {
         k = a.kst[0];
-        const bool run = cg_run(a, k, kFuse);
+        if (kFuse) rr = cur_rr(a);
+        const bool run = cg_run(a, k, kFuse, rr);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            if (kFuse && (k == 1 || run)) a.hist[k - 1] = a.g[kRR];
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = rr;
             if (run)
                 stamp(a, kStampSpmv);
             else
@@ -924,7 +951,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     double beta = 0.0;
     const double* __restrict__ pold = a.r;
     if constexpr (kFuse) {
-        beta = (k == 1) ? 0.0 : a.g[kRR] / a.hist[k - 2];
+        beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
         pold = (k == 1) ? a.r : cur_p(a, k - 1);
     }
     const int w0 = a.win_ptr[s], w1 = a.win_ptr[s + 1];
@@ -1081,24 +1108,13 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
 //           alpha = rtrans / (p.Ap); then the r.r partial that the next
 //           iteration's ddot(r, r) (HPCCG.cpp:367) would compute.
 // ---------------------------------------------------------------------------
+// One slice's share of the update for the thread owning rows lt*kRpt.. of
+// slice s (HPCCG.cpp:352 in the prologue; :382-384 with the deferred x
+// update); returns the thread's r.r contribution.
 template <int kRpt, bool kPrologue>
-__global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
+__device__ __forceinline__ double update_slice(const CgArgs& a, int s, int lt, int k, double alpha)
 {
-    int k = 0;
-    if constexpr (!kPrologue) {
-        k = a.kst[0];
-        const bool run = cg_run(a, k, false);
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            if (run)
-                stamp(a, kStampUpdate);
-            else
-                mark_end(a);
-        }
-        if (!run) return;
-    }
-    const int s = a.rev ? xcd_slice_rev(a.grid) : xcd_slice(a.grid);
-    if (s >= a.nslices) return;
-    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    const int row = s * kSliceRows + lt * kRpt;
     const Rows<kRpt> apv = ld<kRpt>(a.Ap + row);
     Rows<kRpt> rn;
     if constexpr (kPrologue) {
@@ -1106,8 +1122,6 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
 #pragma unroll
         for (int i = 0; i < kRpt; i++) rn.v[i] = bv.v[i] + (-1.0) * apv.v[i];
     } else {
-        const double alpha = a.g[kRR] / a.g[kPAP];
-        if (blockIdx.x == 0 && threadIdx.x == 0) a.ahist[k] = alpha;
         const Rows<kRpt> rv = ld<kRpt>(a.r + row);
 #pragma unroll
         for (int i = 0; i < kRpt; i++) rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
@@ -1136,9 +1150,144 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
 #pragma unroll
     for (int i = 0; i < kRpt; i++)
         if (row + i < a.n) d += rn.v[i] * rn.v[i];
+    return d;
+}
+
+template <int kRpt, bool kPrologue>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
+{
+    int k = 0;
+    if constexpr (!kPrologue) {
+        k = a.kst[0];
+        const bool run = cg_run(a, k, false);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (run)
+                stamp(a, kStampUpdate);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = a.rev ? xcd_slice_rev(a.grid) : xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    double alpha = 0.0;
+    if constexpr (!kPrologue) {
+        alpha = a.g[kRR] / a.g[kPAP];
+        if (blockIdx.x == 0 && threadIdx.x == 0) a.ahist[k] = alpha;
+    }
+    const double d = update_slice<kRpt, kPrologue>(a, s, threadIdx.x, k, alpha);
     const double bs = block_sum<kSliceRows / kRpt>(d);
     complete_dot<kSliceRows / kRpt>(a, s, bs, kRR, kPrologue ? 1 : k + 1);
 }
+
+// ---------------------------------------------------------------------------
+// Redundant dot completion (single rank, a.redund): no finalize kernels and no
+// tickets between workgroups. The update runs one workgroup per 64-slice group
+// (1024 threads, four slices at a time); each workgroup first sums ALL p.Ap
+// slice partials itself (the fixed two-level shape of k_finalize), keeps its
+// slices' r.r partials in LDS and stores its group's r.r sum; every SpMV
+// workgroup then sums the group sums itself (cur_rr). One arrival counter per
+// update workgroup advances k.
+// ---------------------------------------------------------------------------
+constexpr int kUGThreads = 1024;
+
+// p.Ap (which = kPAP) or r.r total from the slice partials, in every thread.
+__device__ double total_from_partials(const CgArgs& a, int which, double* gs_lds)
+{
+    const int ng = ngroups_of(a);
+    (void)which;
+    const double* part = a.partial;  // the producing kernel's slice partials
+    const int lane = threadIdx.x & (kWave - 1);
+    const int nw = blockDim.x / kWave;
+    constexpr int kB = 8;
+    for (int g0 = threadIdx.x / kWave; g0 < ng; g0 += nw * kB) {
+        double v[kB];
+#pragma unroll
+        for (int b = 0; b < kB; b++) {
+            const int i = (g0 + b * nw) * kGroup + lane;
+            v[b] = (g0 + b * nw < ng && i < a.nslices) ? part[i] : 0.0;
+        }
+#pragma unroll
+        for (int b = 0; b < kB; b++) {
+            const double w = wave_sum(v[b]);
+            if (lane == 0 && g0 + b * nw < ng) gs_lds[g0 + b * nw] = w;
+        }
+    }
+    __syncthreads();
+    __shared__ double tot;
+    if (threadIdx.x < kWave) {
+        const double t = top_sum_wave([gs_lds](int i) { return gs_lds[i]; }, ng, lane);
+        if (lane == 0) tot = t;
+    }
+    __syncthreads();
+    return tot;
+}
+
+template <int kRpt, bool kPrologue>
+__global__ __launch_bounds__(kUGThreads) void k_update_g(CgArgs a)
+{
+    __shared__ double gs[kFinLdsGroups];
+    __shared__ double wsum[kUGThreads / kWave];
+    __shared__ double spart[kGroup];
+    int k = 0;
+    if constexpr (!kPrologue) {
+        k = a.kst[0];
+        const bool run = cg_run(a, k, false);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (run)
+                stamp(a, kStampUpdate);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int ng = ngroups_of(a);
+    const int per = a.ugrid / kNumXcd;
+    const int b = blockIdx.x;
+    const int g = (b % kNumXcd) * per + (a.rev ? per - 1 - b / kNumXcd : b / kNumXcd);
+    double alpha = 0.0;
+    if constexpr (!kPrologue) {
+        const double pap = total_from_partials(a, kPAP, gs);
+        alpha = a.hist[k - 1] / pap;  // rtrans / (p.Ap), HPCCG.cpp:380
+        if (b == 0 && threadIdx.x == 0) a.ahist[k] = alpha;
+    }
+    if (g >= ng) return;
+    constexpr int kTps = kSliceRows / kRpt;       // threads per slice
+    constexpr int kSpp = kUGThreads / kTps;       // slices per pass
+    const int q = threadIdx.x / kTps, lt = threadIdx.x % kTps;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const int s0 = g * kGroup, cnt = min(kGroup, a.nslices - s0);
+    for (int j0 = 0; j0 < cnt; j0 += kSpp) {
+        const int j = j0 + q;
+        double d = 0.0;
+        if (j < cnt) d = update_slice<kRpt, kPrologue>(a, s0 + j, lt, k, alpha);
+        // the block_sum<kTps> shape per slice: wave sums, then in wave order
+        d = wave_sum(d);
+        if (lane == 0) wsum[w] = d;
+        __syncthreads();
+        if (lt == 0 && j < cnt) {
+            double bs = 0.0;
+#pragma unroll
+            for (int i = 0; i < kTps / kWave; i++) bs += wsum[q * (kTps / kWave) + i];
+            spart[j] = bs;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < kWave) {
+        const double v = wave_sum(lane < cnt ? spart[lane] : 0.0);  // group_sum's shape
+        if (lane == 0) {
+            a.partial[a.nslices + kRR * ng + g] = v;
+            __threadfence();
+            const unsigned t = atomicAdd(a.tickets, 1u);
+            if (t == (unsigned)ng - 1u) {  // every group stored: advance k
+                stamp(a, kStampFinRR);
+                a.kst[0] = kPrologue ? 1 : k + 1;
+                atomicExch(a.tickets, 0u);
+            }
+        }
+    }
+}
+
 
 // Timestamp-only kernel around RCCL calls (multi-rank): one lane, one store.
 __global__ void k_stamp(CgArgs a, int slot, bool prologue)
@@ -1433,6 +1582,13 @@ void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s
 
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)
 {
+    if (a.redund) {
+        if (prologue)
+            hipLaunchKernelGGL((k_update_g<kRpt, true>), dim3(a.ugrid), dim3(kUGThreads), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_update_g<kRpt, false>), dim3(a.ugrid), dim3(kUGThreads), 0, s, a);
+        return;
+    }
     if (prologue)
         hipLaunchKernelGGL((k_update<kRpt, true>), dim3(a.grid), dim3(kBlock), 0, s, a);
     else

@@ -231,6 +231,7 @@ struct hpccg_hip_matrix {
     int x_defer = 1;           // batched x update every kXDefer iterations
     int rev_update = 1;        // update kernel walks slices backwards (reads the SpMV's latest writes first)
     long long resident_mb = -1; // NT kernels: MB of leading slices on default-policy loads (-1 auto)
+    int redund = 0;            // consumers complete the dots themselves, no finalize kernels (measured slower)
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_partial = nullptr;
     unsigned int* d_tickets = nullptr;
@@ -641,6 +642,15 @@ int fold_effective(const hpccg_hip_matrix* M)
     return M->nslices <= 8192 ? 2 : 0;
 }
 
+// Redundant dot completion (k_update_g + cur_rr): single rank, group sums that
+// fit the update's LDS, at least one iteration (trace[0] then comes from hist).
+bool redund_effective(const hpccg_hip_matrix* M, int max_iter)
+{
+    if (M->nranks != 1 || max_iter < 2 || M->nslices < 1) return false;
+    if ((M->nslices + 63) / 64 > 4096) return false;  // kFinLdsGroups
+    return M->redund > 0;
+}
+
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
 {
     CgArgs a;
@@ -668,6 +678,12 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.nring = a.xdefer ? kXDefer : (a.fuse_p ? 2 : 1);
     a.ahist = M->d_ahist;
     a.fold = fold_effective(M);
+    a.redund = redund_effective(M, max_iter) ? 1 : 0;
+    if (a.redund) a.fold = 0;
+    {
+        const int ng = (M->nslices + 63) / 64;
+        a.ugrid = std::max(kNumXcd, (ng + kNumXcd - 1) / kNumXcd * kNumXcd);
+    }
     a.tickets = M->d_tickets;
     a.Ap = M->d_Ap;
     a.partial = M->d_partial;
@@ -900,7 +916,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
         launch_cg_spmv(a, M->spmv_variant, false, M->stream);
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
-        if (!fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
+        if (!a.redund && !fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
     }
     if (multi) TRY(exch_allreduce(R, kPAP, false));
     for (int r = 0; r < R.P; r++) {
@@ -910,7 +926,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], M->stream));
         launch_cg_update(a, false, M->stream);
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 3], M->stream));
-        if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, false, M->stream);
+        if (!a.redund && !fold_of(a, kRR)) launch_cg_finalize(a, kRR, false, M->stream);
     }
     if (multi) TRY(exch_allreduce(R, kRR, false));
     HIP_TRY(hipGetLastError());
@@ -936,7 +952,7 @@ int enqueue_prologue(const Ranks& R, bool events)
         if (events) HIP_TRY(hipEventRecord(M->ev[2], s));
         launch_cg_update(a, true, s);                  // r = b - Ap (+ r.r partials)
         if (events) HIP_TRY(hipEventRecord(M->ev[3], s));
-        if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, true, s);  // rtrans, k = 1
+        if (!a.redund && !fold_of(a, kRR)) launch_cg_finalize(a, kRR, true, s);  // rtrans, k = 1
     }
     if (multi) TRY(exch_allreduce(R, kRR, true));
     HIP_TRY(hipGetLastError());
@@ -1825,6 +1841,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->x_defer = (int)value;
     } else if (!std::strcmp(key, "rev_update")) {
         M->rev_update = (int)value;
+    } else if (!std::strcmp(key, "redund")) {
+        M->redund = (int)value;
     } else if (!std::strcmp(key, "resident_mb")) {
         M->resident_mb = value < 0 ? -1 : value;
     } else if (!std::strcmp(key, "fold")) {
@@ -1930,6 +1948,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "resident_mb")) *value = resident_mb_effective(M);
+    else if (!std::strcmp(key, "redund")) *value = redund_effective(M, 2) ? 1 : 0;  // off unless set
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
     else if (!std::strcmp(key, "num_external")) *value = M->general ? M->ghost_hi : M->ghost_lo + M->ghost_hi;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_lds ? M->lds_doubles : 0;

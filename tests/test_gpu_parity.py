@@ -88,17 +88,19 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     results = []
     M.set_option("spmv_variant", 1000)  # fuse_p is implemented by the SELL-512 kernels
     import itertools
-    for fuse, fold, graph, defer in itertools.product((0, 1), (0, 1), (0, 1), (0, 1)):
+    for fuse, fold, graph, defer, red in itertools.product((0, 1), (0, 1), (0, 1), (0, 1), (0, 1)):
         M.set_option("fuse_p", fuse)
         M.set_option("fold", fold)
         M.set_option("use_graph", graph)
         M.set_option("x_defer", defer)
+        M.set_option("redund", red)  # consumers complete the dots themselves (fold unused then)
         M.set_option("rev_update", (fuse + fold + defer) % 2)  # slice order: no value changes
         x = prob.x
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)  # 119 iterations: 7 pending x updates
         assert M.get_option("fuse_p") == fuse
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # one dot folded, the other finalized by its own kernel
+    M.set_option("redund", 0)
     for fold in (2, 3):
         M.set_option("fold", fold)
         x = prob.x
@@ -108,6 +110,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     for v, fuse in itertools.product((2000, 2100, 2200, 2308, 3000, 3100, 4200, 4300), (0, 1)):
         M.set_option("spmv_variant", v)
         M.set_option("fuse_p", fuse)
+        M.set_option("redund", 1 - fuse)
         M.set_option("resident_mb", fuse)  # 1 MB on default-policy loads: no value changes
         assert M.get_option("fuse_p") == fuse
         x = prob.x
@@ -123,6 +126,7 @@ def test_folded_dot_completion_stress(hp, gpu):
     k_finalize path (data handed over by a kernel boundary)."""
     prob = hp.generate_matrix(64, 64, 48)  # 384 slices -> 6 groups, partial last group
     M = hp.Matrix.from_hpc(prob)
+    M.set_option("redund", 0)
     M.set_option("fold", 0)
     x = prob.x
     hp.HPCCG(M, prob.b, x, max_iter=150)
