@@ -1530,7 +1530,7 @@ bool spmv_variant_ok(int v)
     case 0: case 1: case 2: case 27: case 7: case 327: case 427:
     case 1000: case 1001: case 1002: case 1027: case 1007: case 9999:
     case 2000: case 2001: case 2002: case 2100: case 2200: case 2208: case 2300: case 2308:
-    case 3000: case 3001: case 3002: case 3100: case 4000: case 4200: case 4300:
+    case 3000: case 3001: case 3002: case 3100: case 4000: case 4200: case 4300: case 4202: case 4206: case 4208:
         return true;
     default:
         return false;
@@ -1561,6 +1561,9 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 2300: HPCCG_SPMV_LDS(2, false, 4); break;
     case 2308: HPCCG_SPMV_LDS(2, false, 8); break;
     case 4200: HPCCG_SPMV_LDSX(2, true, 4, true); break;
+    case 4202: HPCCG_SPMV_LDSX(2, true, 2, true); break;
+    case 4206: HPCCG_SPMV_LDSX(2, true, 6, true); break;
+    case 4208: HPCCG_SPMV_LDSX(2, true, 8, true); break;
     case 4300: HPCCG_SPMV_LDSX(2, false, 4, true); break;
     case 4000: HPCCG_SPMV_LDSX(2, true, 0, true); break;
     case 3000: HPCCG_SPMV_C(2, true); break;

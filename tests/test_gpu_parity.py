@@ -333,9 +333,30 @@ def test_csr_entry_and_ragged_rows(hp, gpu):
 # ---------------------------------------------------------------------------
 # BASELINE sizes: size-independent properties (the oracle is too slow there)
 # ---------------------------------------------------------------------------
+def kat2_rr0(nx, ny, nz):
+    """sum over rows of b_i^2 = (28 - nnz_i)^2, nnz_i a product of per-axis counts
+    (generate_matrix.cpp:259-286); exact in integers."""
+    def axis(n):
+        c = np.full(n, 3, np.int64)
+        c[0] -= 1
+        c[-1] -= 1
+        return np.unique(c, return_counts=True)
+    tot = 0
+    for cx, nx_ in zip(*axis(nx)):
+        for cy, ny_ in zip(*axis(ny)):
+            for cz, nz_ in zip(*axis(nz)):
+                tot += int(nx_) * int(ny_) * int(nz_) * (28 - int(cx * cy * cz)) ** 2
+    return tot
+
+
 @pytest.mark.parametrize("dims,s7,rr0", [((100, 100, 100), False, 7007848),
-                                         ((200, 200, 200), False, 31896248)])
+                                         ((200, 200, 200), False, 31896248),
+                                         ((320, 320, 320), False, None)])
 def test_full_size_properties(hp, gpu, dims, s7, rr0):
+    """Full and beyond-BASELINE sizes (320^3: 32.8 M rows, 0.88 G nonzeros,
+    0.88 G SELL slots) through size-independent properties."""
+    if rr0 is None:
+        rr0 = kat2_rr0(*dims)
     import torch
     M = hp.Matrix.generate(*dims, use_7pt=s7)
     info = M.info()
