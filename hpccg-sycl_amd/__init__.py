@@ -104,6 +104,7 @@ def lib() -> C.CDLL:
         "hpccg_slab_plan": (ip, [ip, ip, PI, PI]),
         "hpccg_hip_group_generate": (ip, [ip, ip, ip, ip, ip, PI, C.POINTER(vp)]),
         "hpccg_hip_set_halo_mode": (ip, [ip]),
+        "hpccg_gather_plan": (ip, [ip, PI, ip, ip, vp, vp, ip, PI, PI, PI, PI, PI, PI]),
         "hpccg_read_HPC_row": (ip, [C.c_char_p, ip, ip, C.POINTER(C.POINTER(_HPCMatrix)),
                                     C.POINTER(PD), C.POINTER(PD), C.POINTER(PD)]),
         "hpccg_hip_group_create_csr": (ip, [ip, PI, PI, PI, ip, C.POINTER(vp), C.POINTER(vp),
@@ -470,6 +471,26 @@ def halo_plan(row_ptr, cols, start_row, total_nrow):
     _check(lib().hpccg_halo_plan(len(row_ptr) - 1, start_row, total_nrow, row_ptr.ctypes.data,
                                  cols.ctypes.data, out), "halo_plan")
     return {"ghost_lo": out[0], "ghost_hi": out[1], "min_col": out[2], "max_col": out[3]}
+
+
+def gather_plan(nranks: int, info, row_ptr, cols, start_row: int) -> dict:
+    """Local half of the gather plan: external columns in local order and the
+    receive runs per owner (make_local_matrix.cpp:96-200)."""
+    row_ptr = np.ascontiguousarray(row_ptr, np.int64)
+    cols = np.ascontiguousarray(cols, np.int32)
+    arr = (C.c_int * (4 * nranks))(*[int(v) for v in np.asarray(info).ravel()])
+    ne, nr = C.c_int(0), C.c_int(0)
+    L = lib()
+    n = len(row_ptr) - 1
+    _check(L.hpccg_gather_plan(nranks, arr, n, start_row, row_ptr.ctypes.data, cols.ctypes.data, 0, None,
+                               C.byref(ne), C.byref(nr), None, None, None), "gather_plan")
+    cap = max(ne.value, nr.value, 1)
+    ext = (C.c_int * cap)()
+    rr, ro, rc = (C.c_int * cap)(), (C.c_int * cap)(), (C.c_int * cap)()
+    _check(L.hpccg_gather_plan(nranks, arr, n, start_row, row_ptr.ctypes.data, cols.ctypes.data, cap, ext,
+                               C.byref(ne), C.byref(nr), rr, ro, rc), "gather_plan")
+    return {"ext_global": np.array(ext[:ne.value], np.int64),
+            "recv": [(rr[i], ro[i], rc[i]) for i in range(nr.value)]}
 
 
 def slab_plan(nranks: int, rank: int, info) -> tuple[int, int]:

@@ -2065,6 +2065,33 @@ long long hpccg_sell_build(int nrow, long long col_base, long long ncol_ext, con
     return bad ? HPCCG_HIP_EPLAN : r;
 }
 
+int hpccg_gather_plan(int nranks, const int* info, int nrow, int start_row, const long long* row_ptr,
+                      const int* cols, int cap, int* ext_global, int* num_external, int* nrecv, int* recv_rank,
+                      int* recv_off, int* recv_cnt)
+{
+    if (nranks < 1 || !info || nrow < 0 || (nrow > 0 && (!row_ptr || !cols)) || !num_external || !nrecv)
+        return set_err(HPCCG_HIP_EINVAL, "bad argument");
+    GatherPlan g;
+    gather_externals(
+        nrow, start_row, info, nranks, [row_ptr](int i) { return (int)(row_ptr[i + 1] - row_ptr[i]); },
+        [row_ptr, cols](int i, int j, long long* c, double* v) {
+            *c = cols[row_ptr[i] + j];
+            *v = 0.0;
+        },
+        g);
+    *num_external = (int)g.ext_global.size();
+    *nrecv = (int)g.recv_rank.size();
+    if (ext_global && cap >= *num_external)
+        for (int j = 0; j < *num_external; j++) ext_global[j] = (int)g.ext_global[j];
+    if (recv_rank && recv_off && recv_cnt && cap >= *nrecv)
+        for (int i = 0; i < *nrecv; i++) {
+            recv_rank[i] = g.recv_rank[i];
+            recv_off[i] = g.recv_off[i];
+            recv_cnt[i] = g.recv_cnt[i];
+        }
+    return 0;
+}
+
 int hpccg_slab_plan(int nranks, int rank, const int* info, int sends[2])
 {
     if (nranks < 1 || rank < 0 || rank >= nranks || !info || !sends)

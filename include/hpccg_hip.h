@@ -198,6 +198,15 @@ int hpccg_halo_plan(int nrow, int start_row, int total_nrow, const long long* ro
  * all-gather the library does at matrix creation); sends[0] = rows to
  * rank-1 (its first rows), sends[1] = rows to rank+1 (its last rows). */
 int hpccg_slab_plan(int nranks, int rank, const int* info, int sends[2]);
+/* The local half of the gather plan (make_local_matrix.cpp:96-200) for one
+ * rank's rows (global columns): the external columns in local-index order
+ * (ext_global[j] is local column nrow + j: grouped by owning rank, groups in
+ * order of first appearance, first appearance inside a group) and the receive
+ * runs per owner. info as for hpccg_slab_plan. Arrays of at least cap
+ * entries, filled when large enough; counts always. Host only. */
+int hpccg_gather_plan(int nranks, const int* info, int nrow, int start_row, const long long* row_ptr,
+                      const int* cols, int cap, int* ext_global, int* num_external, int* nrecv, int* recv_rank,
+                      int* recv_off, int* recv_cnt);
 
 #ifdef __cplusplus
 }
