@@ -349,6 +349,8 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
     a.loc[which] = s;
     if (a.nranks == 1) a.g[which] = s;
     if (which == kRR) a.kst[0] = kfinal;
+    // multi-rank: the local sum is done, the all-reduce comes next (t4 class)
+    if (a.nranks > 1) stamp(a, which == kRR ? kStampArRR : kStampArPAP);
 }
 
 // bs valid in thread 0. Only wave 0 takes part in the hand-off: the other waves
@@ -460,6 +462,7 @@ __global__ __launch_bounds__(256) void k_p_boundary(CgArgs a, int nlo, int nhi)
     const int k = a.kst[0];
     const double rr = cur_rr(a);
     if (!cg_run(a, k, true, rr)) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) stamp(a, kStampHalo);  // halo class from here
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= nlo + nhi) return;
     const int row = i < nlo ? i : a.n - nhi + (i - nlo);
@@ -483,6 +486,7 @@ __global__ __launch_bounds__(256) void k_pack(CgArgs a, const int* __restrict__ 
         rr = cur_rr(a);
         if (!cg_run(a, k, true, rr)) return;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) stamp(a, kStampHalo);  // halo class from here
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= cnt) return;
     const int e = idx[i];

@@ -872,7 +872,10 @@ int group_allreduce(const Ranks& R, int which)
 
 int exch_halo(const Ranks& R, int k_host, bool prologue)
 {
-    for (int r = 0; r < R.P; r++) {
+    // k_pack (gather plan) and k_p_boundary (fused slab) stamp the halo class
+    // themselves; otherwise a one-lane stamp kernel does
+    const bool stamped = R.M[0]->general || (!prologue && R.a[0].fuse_p);
+    for (int r = 0; r < R.P && !stamped; r++) {
         TRY(use_device(R, r));
         launch_cg_stamp(R.a[r], kStampHalo, prologue, R.M[r]->stream);
     }
@@ -886,10 +889,7 @@ int exch_halo(const Ranks& R, int k_host, bool prologue)
 
 int exch_allreduce(const Ranks& R, int which, bool prologue)
 {
-    for (int r = 0; r < R.P; r++) {
-        TRY(use_device(R, r));
-        launch_cg_stamp(R.a[r], which == kRR ? kStampArRR : kStampArPAP, prologue, R.M[r]->stream);
-    }
+    (void)prologue;  // the all-reduce class is stamped where the local sum completes (finish_dot)
     if (R.P > 1) return group_allreduce(R, which);
     return enqueue_allreduce(R.M[0], R.a[0], which);
 }
