@@ -50,6 +50,8 @@ struct CgArgs {
     int rev;               // 1: the update kernel walks each XCD's slices backwards
     int redund;            // 1: no finalize kernels: consumers sum the producers' partials themselves
     int ugrid;             // k_update_g grid (groups rounded up to a multiple of kNumXcd)
+    int s0, sn0, s1, sn1;  // SpMV launch: slices [s0, s0 + sn0) then [s1, s1 + sn1)
+    int sgrid;             // SpMV launch grid (sn0 + sn1 rounded up to a multiple of kNumXcd)
     int nt_split;          // NT matrix kernels: per XCD, this many leading slices use default-policy loads
     double* ahist;         // [max_iter + 1]: alpha_k (for the deferred x update)
     int fuse_p;            // 1: p = r + beta p computed inside the SpMV (single rank)

@@ -47,6 +47,16 @@ __device__ __forceinline__ int xcd_slice_rev(int grid)
     return (b % kNumXcd) * per + (per - 1 - b / kNumXcd);
 }
 
+// The SpMV launches cover up to two slice ranges ([s0, s0 + n0) then
+// [s1, s1 + n1)): all slices, or the interior / halo-dependent slices of a
+// multi-rank iteration that overlaps its halo exchange. -1: no slice.
+__device__ __forceinline__ int spmv_slice(const CgArgs& a)
+{
+    const int i = xcd_slice(a.sgrid);
+    if (i >= a.sn0 + a.sn1) return -1;
+    return i < a.sn0 ? a.s0 + i : a.s1 + (i - a.sn0);
+}
+
 // Lane l < off receives lane l + off (gfx950 lane moves, no LDS traffic):
 // permlane32/16_swap for the cross-row steps, DPP row_shl inside a row.
 template <int kOff>
@@ -615,8 +625,8 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool pro
         }
         if (!run) return;
     }
-    const int s = xcd_slice(a.grid);
-    if (s >= a.nslices) return;
+    const int s = spmv_slice(a);
+    if (s < 0) return;
     for (int i = threadIdx.x; i < kCodes; i += kSliceRows / kRpt) sdict[i] = a.cdict[(size_t)s * kCodes + i];
     __syncthreads();
     const int row = s * kSliceRows + threadIdx.x * kRpt;
@@ -780,8 +790,8 @@ __global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, boo
         }
         if (!run) return;
     }
-    const int s = xcd_slice(a.grid);
-    if (s >= a.nslices) return;
+    const int s = spmv_slice(a);
+    if (s < 0) return;
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     double* __restrict__ p = cur_p(a, k);
     double sum[kRpt];
@@ -929,8 +939,8 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
         }
         if (!run) return;
     }
-    const int s = xcd_slice(a.grid);
-    if (s >= a.nslices) return;
+    const int s = spmv_slice(a);
+    if (s < 0) return;
     double* __restrict__ p = cur_p(a, k);
     const double* __restrict__ xext = p - a.ghost_lo;
     const size_t base = (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
@@ -943,7 +953,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     // the first nt_split slices of every XCD's eighth stream with the default
     // policy (they may stay resident in the Infinity Cache between iterations,
     // spread evenly over the XCDs), the rest non-temporal
-    const bool nt = kNT && (s % (a.grid / kNumXcd)) >= a.nt_split;
+    const bool nt = kNT && (xcd_slice(a.sgrid) % (a.sgrid / kNumXcd)) >= a.nt_split;
     if (nt)
         lds_prefetch<kRpt, true, kCode, kPre>(vp, cp, wdt, vpre, cpre);
     else
@@ -1502,29 +1512,29 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
 #define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
     do {                                                                                            \
         if (a.fuse_p && !prologue)                                                                  \
-            hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, true>), dim3(a.grid), dim3(kSliceRows / RPT), \
+            hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, true>), dim3(a.sgrid), dim3(kSliceRows / RPT), \
                                0, s, a, prologue);                                                  \
         else                                                                                        \
-            hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, false>), dim3(a.grid),                    \
+            hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, false>), dim3(a.sgrid),                   \
                                dim3(kSliceRows / RPT), 0, s, a, prologue);                          \
     } while (0)
 #define HPCCG_SPMV_C(RPT, NT)                                                                      \
     do {                                                                                           \
         if (a.fuse_p && !prologue)                                                                 \
-            hipLaunchKernelGGL((k_spmv_c<RPT, NT, true>), dim3(a.grid), dim3(kSliceRows / RPT), 0, s, a, \
+            hipLaunchKernelGGL((k_spmv_c<RPT, NT, true>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, a, \
                                prologue);                                                          \
         else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_c<RPT, NT, false>), dim3(a.grid), dim3(kSliceRows / RPT), 0, s, a, \
+            hipLaunchKernelGGL((k_spmv_c<RPT, NT, false>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, a, \
                                prologue);                                                          \
     } while (0)
 #define HPCCG_SPMV_LDSX(RPT, NT, PRE, CODE)                                                        \
     do {                                                                                           \
         const size_t smem = (size_t)a.lds_doubles * sizeof(double);                                \
         if (a.fuse_p && !prologue)                                                                 \
-            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, true, PRE, CODE>), dim3(a.grid), dim3(kSliceRows / RPT), \
+            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, true, PRE, CODE>), dim3(a.sgrid), dim3(kSliceRows / RPT), \
                                smem, s, a, prologue);                                              \
         else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, false, PRE, CODE>), dim3(a.grid), dim3(kSliceRows / RPT), \
+            hipLaunchKernelGGL((k_spmv_lds<RPT, NT, false, PRE, CODE>), dim3(a.sgrid), dim3(kSliceRows / RPT), \
                                smem, s, a, prologue);                                              \
     } while (0)
 #define HPCCG_SPMV_LDS(RPT, NT, PRE) HPCCG_SPMV_LDSX(RPT, NT, PRE, false)

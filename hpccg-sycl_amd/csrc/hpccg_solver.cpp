@@ -205,6 +205,12 @@ struct hpccg_hip_matrix {
     int nsend = 0;
     int* d_send_idx = nullptr;
     double* d_send_buf = nullptr;
+    // halo / interior overlap (multi-rank slab plan): the leading b_lo and
+    // trailing b_hi slices read ghost columns, the rest do not
+    int halo_b_lo = -1, halo_b_hi = -1;
+    int overlap = 1;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_pb = nullptr, ev_halo = nullptr;
     long long nnz = 0, nslots = 0;
     int nslices = 0, grid = 0, width = 0, uniform = 0;
     int spmv_variant = 0;
@@ -276,6 +282,9 @@ int free_matrix(hpccg_hip_matrix* M)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
     if (M->stream) (void)hipStreamDestroy(M->stream);
+    if (M->stream2) (void)hipStreamDestroy(M->stream2);
+    if (M->ev_pb) (void)hipEventDestroy(M->ev_pb);
+    if (M->ev_halo) (void)hipEventDestroy(M->ev_halo);
     delete M;
     return 0;
 }
@@ -670,6 +679,11 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.fuse_p = fuse_p_effective(M) ? 1 : 0;
     a.xdefer = M->x_defer ? 1 : 0;
     a.rev = M->rev_update ? 1 : 0;
+    a.s0 = 0;
+    a.sn0 = M->nslices;
+    a.s1 = 0;
+    a.sn1 = 0;
+    a.sgrid = M->grid;
     {
         const double per_slice = (double)M->nslots / std::max(1, M->nslices) * slot_bytes(M);
         const double sl = (double)resident_mb_effective(M) * 1e6 / std::max(1.0, per_slice);
@@ -711,19 +725,20 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
 // Halo exchange of p (exchange_externals.cpp:51-131): the z-slab ghosts are
 // contiguous, so no pack: rank r sends its first send_lo rows down and its
 // last send_hi rows up, and receives straight into the ghost regions.
-int enqueue_halo(hpccg_hip_matrix* M, double* p)
+int enqueue_halo(hpccg_hip_matrix* M, double* p, hipStream_t st = nullptr)
 {
     if (g_comm.nranks == 1) return 0;
+    if (!st) st = M->stream;
     const int r = g_comm.rank;
     NCCL_TRY(ncclGroupStart());
     if (r > 0) {
-        if (M->ghost_lo) NCCL_TRY(ncclRecv(p - M->ghost_lo, M->ghost_lo, ncclFloat64, r - 1, g_comm.comm, M->stream));
-        if (M->send_lo) NCCL_TRY(ncclSend(p, M->send_lo, ncclFloat64, r - 1, g_comm.comm, M->stream));
+        if (M->ghost_lo) NCCL_TRY(ncclRecv(p - M->ghost_lo, M->ghost_lo, ncclFloat64, r - 1, g_comm.comm, st));
+        if (M->send_lo) NCCL_TRY(ncclSend(p, M->send_lo, ncclFloat64, r - 1, g_comm.comm, st));
     }
     if (r < g_comm.nranks - 1) {
-        if (M->ghost_hi) NCCL_TRY(ncclRecv(p + M->nrow, M->ghost_hi, ncclFloat64, r + 1, g_comm.comm, M->stream));
+        if (M->ghost_hi) NCCL_TRY(ncclRecv(p + M->nrow, M->ghost_hi, ncclFloat64, r + 1, g_comm.comm, st));
         if (M->send_hi)
-            NCCL_TRY(ncclSend(p + M->nrow - M->send_hi, M->send_hi, ncclFloat64, r + 1, g_comm.comm, M->stream));
+            NCCL_TRY(ncclSend(p + M->nrow - M->send_hi, M->send_hi, ncclFloat64, r + 1, g_comm.comm, st));
     }
     NCCL_TRY(ncclGroupEnd());
     return 0;
@@ -898,9 +913,99 @@ int exch_allreduce(const Ranks& R, int which, bool prologue)
 // rank of R. slot >= 0 (single matrix): bracket the SpMV and the fused update
 // with that slot's hipEvents. k_host is the iteration being enqueued: it
 // addresses p_k's ring slot for the halo.
+// SpMV launch arguments over a slice subset (interior or halo-dependent runs).
+CgArgs spmv_range(const CgArgs& a, int s0, int n0, int s1, int n1)
+{
+    CgArgs b = a;
+    b.s0 = s0;
+    b.sn0 = n0;
+    b.s1 = s1;
+    b.sn1 = n1;
+    b.sgrid = std::max(kNumXcd, (n0 + n1 + kNumXcd - 1) / kNumXcd * kNumXcd);
+    return b;
+}
+
+// Multi-rank slab iteration with the halo exchange overlapped (SURVEY 5,
+// "overlap the halo with the interior-row SpMV"): the halo rows of p_k first
+// (k_p_boundary), then the exchange on the second stream while the main stream
+// runs the SpMV over the slices that read no ghost column; the ghost-reading
+// slices follow once the halo has landed. Same values, same partial slots.
+bool overlap_ok(const Ranks& R)
+{
+    for (int r = 0; r < R.P; r++) {
+        const hpccg_hip_matrix* M = R.M[r];
+        if (!M->overlap || M->general || M->halo_b_lo < 0 || !R.a[r].fuse_p) return false;
+    }
+    return true;
+}
+
+int enqueue_spmv_overlapped(const Ranks& R, int slot, int k_host)
+{
+    for (int r = 0; r < R.P; r++) {
+        hpccg_hip_matrix* M = R.M[r];
+        TRY(use_device(R, r));
+        launch_cg_p_boundary(R.a[r], M->send_lo, M->send_hi, M->stream);  // stamps the halo class
+        HIP_TRY(hipEventRecord(M->ev_pb, M->stream));
+    }
+    for (int r = 0; r < R.P; r++) {
+        hpccg_hip_matrix* M = R.M[r];
+        TRY(use_device(R, r));
+        double* p = ring_p(R.a[r], k_host);
+        if (R.P == 1) {
+            HIP_TRY(hipStreamWaitEvent(M->stream2, M->ev_pb, 0));
+            TRY(enqueue_halo(M, p, M->stream2));
+        } else {
+            if (r > 0 && M->ghost_lo) {
+                const hpccg_hip_matrix* L = R.M[r - 1];
+                HIP_TRY(hipStreamWaitEvent(M->stream2, L->ev_pb, 0));
+                HIP_TRY(hipMemcpyPeerAsync(p - M->ghost_lo, M->device,
+                                           ring_p(R.a[r - 1], k_host) + L->nrow - M->ghost_lo, L->device,
+                                           sizeof(double) * M->ghost_lo, M->stream2));
+            }
+            if (r < R.P - 1 && M->ghost_hi) {
+                const hpccg_hip_matrix* U = R.M[r + 1];
+                HIP_TRY(hipStreamWaitEvent(M->stream2, U->ev_pb, 0));
+                HIP_TRY(hipMemcpyPeerAsync(p + M->nrow, M->device, ring_p(R.a[r + 1], k_host), U->device,
+                                           sizeof(double) * M->ghost_hi, M->stream2));
+            }
+        }
+        HIP_TRY(hipEventRecord(M->ev_halo, M->stream2));
+    }
+    for (int r = 0; r < R.P; r++) {
+        hpccg_hip_matrix* M = R.M[r];
+        const CgArgs& a = R.a[r];
+        TRY(use_device(R, r));
+        const int lo = M->halo_b_lo, hi = M->halo_b_hi, mid = M->nslices - lo - hi;
+        if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
+        launch_cg_spmv(spmv_range(a, lo, mid, 0, 0), M->spmv_variant, false, M->stream);
+        HIP_TRY(hipStreamWaitEvent(M->stream, M->ev_halo, 0));
+        if (lo + hi > 0)
+            launch_cg_spmv(spmv_range(a, 0, lo, M->nslices - hi, hi), M->spmv_variant, false, M->stream);
+        if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
+        if (!a.redund && !fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
+    }
+    return 0;
+}
+
 int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
 {
     const bool multi = R.a[0].nranks > 1;
+    if (multi && overlap_ok(R)) {
+        TRY(enqueue_spmv_overlapped(R, slot, k_host));
+        TRY(exch_allreduce(R, kPAP, false));
+        for (int r = 0; r < R.P; r++) {
+            hpccg_hip_matrix* M = R.M[r];
+            const CgArgs& a = R.a[r];
+            TRY(use_device(R, r));
+            if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], M->stream));
+            launch_cg_update(a, false, M->stream);
+            if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 3], M->stream));
+            if (!a.redund && !fold_of(a, kRR)) launch_cg_finalize(a, kRR, false, M->stream);
+        }
+        TRY(exch_allreduce(R, kRR, false));
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     for (int r = 0; r < R.P; r++) {
         TRY(use_device(R, r));
         if (!R.a[r].fuse_p)
@@ -1256,8 +1361,30 @@ bool build_windows_stencil(int nslices, int nrow, int nx, int nxy, int ghost_lo,
     return true;
 }
 
+// Which slices read ghost columns (their windows reach outside [ghost_lo,
+// ghost_lo + n)): a leading and a trailing run for slab plans, else no overlap.
+void halo_runs(hpccg_hip_matrix* M, const Windows& W)
+{
+    M->halo_b_lo = M->halo_b_hi = -1;
+    if (M->nslices < 1 || (int)W.ptr.size() != M->nslices + 1) return;
+    const long long lo = M->ghost_lo, hi = (long long)M->ghost_lo + M->nrow;
+    std::vector<char> t(M->nslices, 0);
+    for (int s = 0; s < M->nslices; s++)
+        for (int w = W.ptr[s]; w < W.ptr[s + 1]; w++)
+            if (W.start[w] < lo || (long long)W.start[w] + W.len[w] > hi) t[s] = 1;
+    int a = 0, b = 0;
+    while (a < M->nslices && t[a]) a++;
+    while (b < M->nslices - a && t[M->nslices - 1 - b]) b++;
+    for (int s = a; s < M->nslices - b; s++)
+        if (t[s]) return;  // a ghost reader in the middle: no overlap
+    if (a + b >= M->nslices) return;
+    M->halo_b_lo = a;
+    M->halo_b_hi = b;
+}
+
 int upload_windows(hpccg_hip_matrix* M, const Windows& W)
 {
+    halo_runs(M, W);
     M->nwin = (int)W.start.size();
     const size_t nw = std::max<size_t>(1, W.start.size());
     HIP_TRY(hipMalloc(&M->d_win_ptr, sizeof(int) * W.ptr.size()));
@@ -1306,6 +1433,15 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
         return set_err(HPCCG_HIP_EPLAN, "column outside [0, total_nrow)");
     }
     HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamDefault));
+    {
+        // halo stream at the highest priority: its small transfer kernels get CUs
+        // while the interior SpMV fills the chip
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&M->stream2, hipStreamDefault, greatest));
+    }
+    HIP_TRY(hipEventCreateWithFlags(&M->ev_pb, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&M->ev_halo, hipEventDisableTiming));
     int mode = 1;
     std::vector<int> all;
     GatherPlan gp_local;
@@ -1636,6 +1772,15 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     M->ghost_hi = rank < size - 1 ? std::min(nxy, n) : 0;
     // rows per z-plane beyond one plane would need rank+-2 (nz >= 1 keeps it at +-1)
     HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamDefault));
+    {
+        // halo stream at the highest priority: its small transfer kernels get CUs
+        // while the interior SpMV fills the chip
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&M->stream2, hipStreamDefault, greatest));
+    }
+    HIP_TRY(hipEventCreateWithFlags(&M->ev_pb, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&M->ev_halo, hipEventDisableTiming));
     int rc = exchange_plan(M);
     if (rc) {
         free_matrix(M);
@@ -1843,6 +1988,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->rev_update = (int)value;
     } else if (!std::strcmp(key, "redund")) {
         M->redund = (int)value;
+    } else if (!std::strcmp(key, "overlap")) {
+        M->overlap = (int)value;
     } else if (!std::strcmp(key, "resident_mb")) {
         M->resident_mb = value < 0 ? -1 : value;
     } else if (!std::strcmp(key, "fold")) {
@@ -1950,6 +2097,8 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "resident_mb")) *value = resident_mb_effective(M);
     else if (!std::strcmp(key, "redund")) *value = redund_effective(M, 2) ? 1 : 0;  // off unless set
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
+    else if (!std::strcmp(key, "overlap"))
+        *value = (M->overlap && M->nranks > 1 && !M->general && M->halo_b_lo >= 0) ? 1 : 0;
     else if (!std::strcmp(key, "num_external")) *value = M->general ? M->ghost_hi : M->ghost_lo + M->ghost_hi;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_lds ? M->lds_doubles : 0;
     else if (!std::strcmp(key, "windows")) *value = M->nwin;

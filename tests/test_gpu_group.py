@@ -52,25 +52,30 @@ def test_group_matches_global_reference(hp, gpu, golden, name):
 
 def test_group_kernel_variants_bitwise(hp, gpu):
     """Multi-rank SpMV kernels (plain SELL-512, NT, LDS-staged windows that
-    include the ghost planes), the p update fused into the LDS SpMV (halo rows
-    by k_p_boundary first), the dot completion modes and the deferred x update
-    give the same bits."""
+    include the ghost planes, 1-byte offset codes), the p update fused into the
+    LDS SpMV (halo rows by k_p_boundary first), the halo overlapped with the
+    interior slices, the dot completion modes and the deferred x update give
+    the same bits."""
     Ms = hp.group_generate(24, 20, 9, 3)
     ref = None
     import itertools
-    for v, fold, fuse, defer in itertools.product((1000, 0, 2000, 2100), (0, 1, 2), (0, 1), (0, 1)):
+    for v, fold, fuse, defer, ovl in itertools.product((1000, 0, 2000, 2100, 4200), (0, 1, 2), (0, 1), (0, 1),
+                                                      (0, 1)):
         for M in Ms:
             M.set_option("spmv_variant", v)
             M.set_option("fold", fold)
             M.set_option("fuse_p", fuse)
             M.set_option("x_defer", defer)
+            M.set_option("overlap", ovl)  # halo on the second stream beside the interior SpMV
+        if v >= 2000 and fuse:
+            assert Ms[1].get_option("overlap") == ovl
         # p = r + beta p inside the SpMV: LDS kernels only on multiple ranks
         assert Ms[1].get_option("fuse_p") == (fuse if v >= 2000 else 0)
         niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
         got = (niters, normr, Ms[0].last_trace().tobytes(), b"".join(x.tobytes() for x in xs))
         if ref is None:
             ref = got
-        assert got == ref, (v, fold, fuse, defer)
+        assert got == ref, (v, fold, fuse, defer, ovl)
     assert Ms[0].get_option("lds_doubles") > 0
 
 
