@@ -214,6 +214,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    # outside the timed region: the last solve's answer (xexact = 1, generate_matrix.cpp:286)
+    # and residual reduction, max over ranks -- a wrong multi-rank exchange shows here
+    tr = M.last_trace()
+    chk = torch.tensor([(x - 1.0).abs().max().item(), float(nr / tr[0]) if tr[0] > 0 else 0.0],
+                       dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(chk, op=dist.ReduceOp.MAX)
 
     # Algorithmic bytes of the reference operations the SpMV kernel performs
     # (fused kernels are credited with the unfused bytes):
@@ -254,7 +261,9 @@ def main():
                 "nx": n, "ny": n, "nz_per_gpu": n, "stencil": args.stencil,
                 "max_iter": args.max_iter, "parallelism": f"z-slab x{world} (RCCL)",
                 "nnz_per_gpu": info["nnz"], "sell_slots_per_gpu": info["slots"],
-                "spmv_variant": info["spmv_variant"],
+                "spmv_variant": M.get_option("spmv_variant"),
+                "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "x_defer", "rev_update",
+                                                         "resident_mb", "overlap")},
             },
             "cg_iterations_per_s_global": round(it_per_s, 3),
             "spmv_effective_gbs": round(achieved, 1),
@@ -274,6 +283,8 @@ def main():
                 "timing": timing_src,
             },
             "update_kernel_avg_us": round(upd_ms / upd_n * 1e3, 2) if upd_n else None,
+            "check": {"x_minus_xexact_inf": chk[0].item(), "final_normr_over_initial": chk[1].item(),
+                      "niters_per_solve": it},
             "times_per_step_s": {"total": times_acc[0] / args.steps,
                                  "ddot": times_acc[1] / args.steps,
                                  "waxpby": times_acc[2] / args.steps,
