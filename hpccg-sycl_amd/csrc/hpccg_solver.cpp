@@ -289,6 +289,21 @@ int free_matrix(hpccg_hip_matrix* M)
     return 0;
 }
 
+// Frees a matrix under construction on every early return; release() on success.
+struct MatrixGuard {
+    hpccg_hip_matrix* m;
+    ~MatrixGuard()
+    {
+        if (m) free_matrix(m);
+    }
+    hpccg_hip_matrix* release()
+    {
+        hpccg_hip_matrix* t = m;
+        m = nullptr;
+        return t;
+    }
+};
+
 // Can the z-slab plan serve rank r? (ghosts from rank+-1 only, contiguous,
 // the planes those ranks own; the condition hpccg_slab_plan enforces)
 bool slab_serves(const int* info, int P, int r)
@@ -1407,7 +1422,8 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
 {
     if (!out) return set_err(HPCCG_HIP_EINVAL, "out is NULL");
     if (nrow < 0) return set_err(HPCCG_HIP_EINVAL, "nrow < 0");
-    auto* M = new hpccg_hip_matrix();
+    MatrixGuard guard{new hpccg_hip_matrix()};
+    hpccg_hip_matrix* M = guard.m;
     HIP_TRY(hipGetDevice(&M->device));
     M->nrow = nrow;
     M->start_row = start_row;
@@ -1428,10 +1444,7 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
     M->nnz = nnz;
     M->ghost_lo = (int)std::max(0LL, (long long)start_row - mn);
     M->ghost_hi = (int)std::max(0LL, mx - ((long long)start_row + nrow - 1));
-    if (mn < 0 || mx >= total_nrow) {
-        delete M;
-        return set_err(HPCCG_HIP_EPLAN, "column outside [0, total_nrow)");
-    }
+    if (mn < 0 || mx >= total_nrow) return set_err(HPCCG_HIP_EPLAN, "column outside [0, total_nrow)");
     HIP_TRY(hipStreamCreateWithFlags(&M->stream, hipStreamDefault));
     {
         // halo stream at the highest priority: its small transfer kernels get CUs
@@ -1465,7 +1478,6 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
         M->send_hi = sends[1];
     }
     if (rc) {
-        free_matrix(M);
         return rc;
     }
     M->nslices = (nrow + kSliceRows - 1) / kSliceRows;
@@ -1503,7 +1515,6 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
         build(SlabCols{col_base, ncol_ext});
     }
     if (bad) {
-        free_matrix(M);
         return set_err(HPCCG_HIP_EPLAN, "column index outside the halo plan");
     }
     Windows W;
@@ -1526,10 +1537,9 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
         return alloc_workspace(M);
     }();
     if (rc) {
-        free_matrix(M);
         return rc;
     }
-    *out = M;
+    *out = guard.release();
     return 0;
 }
 
@@ -1762,7 +1772,8 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     const long long n64 = (long long)nx * ny * nz;
     if (n64 * comm_nranks() >= (1LL << 31)) return set_err(HPCCG_HIP_EINVAL, "global rows exceed int32");
     const int n = (int)n64, rank = comm_rank(), size = comm_nranks();
-    auto* M = new hpccg_hip_matrix();
+    MatrixGuard guard{new hpccg_hip_matrix()};
+    hpccg_hip_matrix* M = guard.m;
     HIP_TRY(hipGetDevice(&M->device));
     M->nrow = n;
     M->start_row = n * rank;
@@ -1783,7 +1794,6 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     HIP_TRY(hipEventCreateWithFlags(&M->ev_halo, hipEventDisableTiming));
     int rc = exchange_plan(M);
     if (rc) {
-        free_matrix(M);
         return rc;
     }
     M->nslices = (n + kSliceRows - 1) / kSliceRows;
@@ -1853,10 +1863,9 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
         return 0;
     }();
     if (rc) {
-        free_matrix(M);
         return rc;
     }
-    *out = M;
+    *out = guard.release();
     return 0;
 }
 
