@@ -1334,7 +1334,7 @@ bool build_windows_from_image(int nslices, const std::vector<unsigned int>& sb, 
 // Stencil slabs, analytically: a superset of the columns a slice of rows
 // [r0, r1) can touch -- the three z-planes' ranges widened by nx + 1.
 bool build_windows_stencil(int nslices, int nrow, int nx, int nxy, int ghost_lo, long long ncol_ext,
-                           Windows& W)
+                           Windows& W, bool use_7pt = false)
 {
     W = Windows();
     W.ptr.push_back(0);
@@ -1342,8 +1342,11 @@ bool build_windows_stencil(int nslices, int nrow, int nx, int nxy, int ghost_lo,
         const long long r0 = (long long)s * kSliceRows, r1 = std::min<long long>(nrow, r0 + kSliceRows);
         std::vector<std::pair<long long, long long>> iv;
         for (int sz = -1; sz <= 1; sz++) {
-            long long lo = ghost_lo + r0 + (long long)sz * nxy - nx - 1;
-            long long hi = ghost_lo + r1 - 1 + (long long)sz * nxy + nx + 1;
+            // 27-pt: every plane +-(nx+1); 7-pt: the +-1 planes only straight across,
+            // the own plane +-nx (generate_matrix.cpp:259-281)
+            const long long m = use_7pt ? (sz == 0 ? nx : 0) : nx + 1;
+            long long lo = ghost_lo + r0 + (long long)sz * nxy - m;
+            long long hi = ghost_lo + r1 - 1 + (long long)sz * nxy + m;
             lo = std::max(0LL, lo);
             hi = std::min(ncol_ext - 1, hi);
             if (lo <= hi) iv.push_back({lo, hi});
@@ -1836,7 +1839,7 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     M->width = M->uniform ? wmax : 0;
     Windows W;
     const long long ncol_ext = (long long)M->ghost_lo + n + M->ghost_hi;
-    const bool lds_ok = build_windows_stencil(M->nslices, n, nx, nxy, M->ghost_lo, ncol_ext, W);
+    const bool lds_ok = build_windows_stencil(M->nslices, n, nx, nxy, M->ghost_lo, ncol_ext, W, use_7pt != 0);
     rc = [&]() -> int {
         HIP_TRY(hipMalloc(&M->d_slice_base, sizeof(unsigned int) * sb.size()));
         HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
