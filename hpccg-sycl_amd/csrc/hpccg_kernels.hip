@@ -606,7 +606,7 @@ __device__ __forceinline__ void ld_codes(const unsigned char* __restrict__ p, un
     }
 }
 
-template <int kRpt, bool kNT, bool kFuse>
+template <int kRpt, bool kNT, bool kFuse, int kW = 0>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool prologue)
 {
     __shared__ int sdict[kCodes];
@@ -631,8 +631,9 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool pro
     __syncthreads();
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     double* __restrict__ p = cur_p(a, k);
-    const size_t b0 = (size_t)a.slice_base[s];
-    const int w = (int)(a.slice_base[s + 1] - b0);
+    // kW > 0: uniform image of width kW, the slot loop fully unrolled
+    const size_t b0 = kW > 0 ? (size_t)s * kW : (size_t)a.slice_base[s];
+    const int w = kW > 0 ? kW : (int)(a.slice_base[s + 1] - b0);
     const size_t base = b0 * kSliceRows + (size_t)threadIdx.x * kRpt;
     const double* __restrict__ vp = a.vals + base;
     const unsigned char* __restrict__ cp = a.ccodes + base;
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool pro
     double sum[kRpt];
 #pragma unroll
     for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
-#pragma unroll 3
+#pragma unroll(kW > 0 ? kW : 3)
     for (int j = 0; j < w; j++) {
         unsigned c[kRpt];
         ld_codes<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
@@ -1518,15 +1519,16 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
             hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, false>), dim3(a.sgrid),                   \
                                dim3(kSliceRows / RPT), 0, s, a, prologue);                          \
     } while (0)
-#define HPCCG_SPMV_C(RPT, NT)                                                                      \
+#define HPCCG_SPMV_CW(RPT, NT, W)                                                                  \
     do {                                                                                           \
         if (a.fuse_p && !prologue)                                                                 \
-            hipLaunchKernelGGL((k_spmv_c<RPT, NT, true>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, a, \
+            hipLaunchKernelGGL((k_spmv_c<RPT, NT, true, W>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, a, \
                                prologue);                                                          \
         else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_c<RPT, NT, false>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, a, \
+            hipLaunchKernelGGL((k_spmv_c<RPT, NT, false, W>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, a, \
                                prologue);                                                          \
     } while (0)
+#define HPCCG_SPMV_C(RPT, NT) HPCCG_SPMV_CW(RPT, NT, 0)
 #define HPCCG_SPMV_LDSX(RPT, NT, PRE, CODE)                                                        \
     do {                                                                                           \
         const size_t smem = (size_t)a.lds_doubles * sizeof(double);                                \
@@ -1544,7 +1546,7 @@ bool spmv_variant_ok(int v)
     case 0: case 1: case 2: case 27: case 7: case 327: case 427:
     case 1000: case 1001: case 1002: case 1027: case 1007: case 9999:
     case 2000: case 2001: case 2002: case 2100: case 2200: case 2208: case 2300: case 2308:
-    case 3000: case 3001: case 3002: case 3100: case 4000: case 4200: case 4300: case 4202: case 4206: case 4208:
+    case 3000: case 3001: case 3002: case 3100: case 3007: case 3027: case 4000: case 4200: case 4300: case 4202: case 4206: case 4208:
         return true;
     default:
         return false;
@@ -1584,6 +1586,8 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 3001: HPCCG_SPMV_C(1, true); break;
     case 3002: HPCCG_SPMV_C(4, true); break;
     case 3100: HPCCG_SPMV_C(2, false); break;
+    case 3007: HPCCG_SPMV_CW(2, true, 7); break;
+    case 3027: HPCCG_SPMV_CW(2, true, 27); break;
     default: HPCCG_SPMV(2, 0, 1, false); break;
     }
 }
@@ -1591,6 +1595,7 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
 #undef HPCCG_SPMV_LDS
 #undef HPCCG_SPMV_LDSX
 #undef HPCCG_SPMV_C
+#undef HPCCG_SPMV_CW
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
 {

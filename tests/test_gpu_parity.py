@@ -54,7 +54,7 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 1000, 1001, 1002, 1027, 2000, 2001,
                                      2002, 2100, 2200, 2208, 2300, 2308, 3000, 3001, 3002, 3100,
-                                     4000, 4200, 4300])
+                                     4000, 4200, 4300, 3027])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
