@@ -182,8 +182,12 @@ def main():
         x.zero_()
         return hp.HPCCG(M, b, x, max_iter=args.max_iter, device=True)
 
+    cold_s = None
     for i in range(args.warmup):
+        t0 = time.perf_counter()
         step(i == 0)
+        if i == 0:
+            cold_s = time.perf_counter() - t0  # first solve: graph build, cold caches
 
     def barrier():
         if world > 1:
@@ -195,9 +199,12 @@ def main():
     niters_total = 0
     spmv_ms = spmv_n = upd_ms = upd_n = 0.0
     times_acc = [0.0] * 7
+    step_s = []
     for i in range(args.steps):
         ev = i < args.event_steps
+        t0 = time.perf_counter()
         _, it, nr, times = step(ev)
+        step_s.append(time.perf_counter() - t0)
         niters_total += it
         if ev:
             kt = M.kernel_times()
@@ -285,6 +292,14 @@ def main():
             "update_kernel_avg_us": round(upd_ms / upd_n * 1e3, 2) if upd_n else None,
             "check": {"x_minus_xexact_inf": chk[0].item(), "final_normr_over_initial": chk[1].item(),
                       "niters_per_solve": it},
+            # per-solve wall times on rank 0 (first/cold and median of the solves);
+            # event steps launch eagerly with hipEvents and are slower than the graph replays
+            "solve_ms": {"cold": round(cold_s * 1e3, 3) if cold_s is not None else None,
+                         "median": round(sorted(step_s)[len(step_s) // 2] * 1e3, 3),
+                         "min": round(min(step_s) * 1e3, 3), "max": round(max(step_s) * 1e3, 3),
+                         "median_graph_replay": round(sorted(step_s[args.event_steps:])[
+                             len(step_s[args.event_steps:]) // 2] * 1e3, 3)
+                         if len(step_s) > args.event_steps else None},
             "times_per_step_s": {"total": times_acc[0] / args.steps,
                                  "ddot": times_acc[1] / args.steps,
                                  "waxpby": times_acc[2] / args.steps,
