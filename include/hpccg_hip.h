@@ -12,8 +12,12 @@
  *            slice (vals[slice][slot][512] fp64, cols[...] int32, padding
  *            col = -1); slice width = max row length in the slice; entry
  *            order per row is the caller's order (so rounding matches).
+ *            SELL-512-L adds per-slice x windows staged in LDS; SELL-512-C
+ *            replaces the column by a 1-byte code into a per-slice dictionary
+ *            of (column - row) offsets (9 B per stored entry). DESIGN.md 3.
  *   vectors  fp64, length padded to a multiple of 512; p carries the halo:
- *            [ghost_lo | local rows | ghost_hi].
+ *            [ghost_lo | local rows | ghost_hi] (z-slab plan) or
+ *            [local rows | externals] (gather plan).
  */
 #ifndef HPCCG_HIP_H
 #define HPCCG_HIP_H
@@ -30,7 +34,8 @@ typedef struct hpccg_hip_matrix hpccg_hip_matrix; /* opaque, device resident */
 #define HPCCG_HIP_EHIP (-2)    /* HIP runtime error */
 #define HPCCG_HIP_ERCCL (-3)   /* RCCL error */
 #define HPCCG_HIP_ENOMEM (-4)  /* device allocation failed */
-#define HPCCG_HIP_EPLAN (-5)   /* matrix couples ranks other than r-1, r+1 */
+#define HPCCG_HIP_EPLAN (-5)   /* no halo plan for this partition (e.g. halo mode 1 and a
+                                  matrix coupling ranks other than r-1, r+1) */
 #define HPCCG_HIP_ENODEV (-6)  /* no HIP device */
 
 /* ---- library ---------------------------------------------------------- */
