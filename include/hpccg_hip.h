@@ -79,11 +79,12 @@ void hpccg_free_problem(struct HPC_Sparse_Matrix_STRUCT* A, double* x, double* b
 
 /* ---- device matrix -------------------------------------------------------
  * hpccg_hip_matrix_create: converts the caller's HPC_Sparse_Matrix
- * (HPC_Sparse_Matrix.hpp:54-85; read-only, caller keeps ownership) to
- * SELL-512 and uploads it. Global column indices in [start_row - G_lo,
- * stop_row + G_hi] are localised against rank+-1 (the z-slab plan that
- * make_local_matrix.cpp:58-610 derives with MPI); anything else returns
- * HPCCG_HIP_EPLAN. Collective over the communicator when nranks > 1. */
+ * (HPC_Sparse_Matrix.hpp:54-85; read-only, caller keeps ownership, global
+ * column indices) to SELL-512 (+ -L, -C where they apply) and uploads it.
+ * The halo plan replaces make_local_matrix.cpp:58-610: the z-slab plan when
+ * every rank's external columns are contiguous planes of rank+-1, else the
+ * gather plan (see hpccg_hip_set_halo_mode). Collective over the
+ * communicator when nranks > 1. */
 int hpccg_hip_matrix_create(const struct HPC_Sparse_Matrix_STRUCT* A, hpccg_hip_matrix** out);
 /* Same from plain CSR (row_ptr[nrow+1] int64, cols int32 global, vals fp64). */
 int hpccg_hip_matrix_create_csr(int nrow, int start_row, int total_nrow, const long long* row_ptr,
