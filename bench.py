@@ -122,6 +122,7 @@ def main():
     ap.add_argument("--variant", type=int, default=-1, help="SpMV kernel variant (-1 auto)")
     ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1 default)")
     ap.add_argument("--fold", type=int, default=-1, help="last-block dot completion (-1 default)")
+    ap.add_argument("--graph-chunk", type=int, default=-1, help="CG iterations per hipGraph (-1 default)")
     ap.add_argument("--redund", type=int, default=-1,
                     help="consumers complete the dot products themselves (-1 default)")
     ap.add_argument("--x-defer", type=int, default=-1, help="batched x update (-1 default)")
@@ -164,6 +165,8 @@ def main():
         M.set_option("fold", args.fold)
     if args.redund >= 0:
         M.set_option("redund", args.redund)
+    if args.graph_chunk > 0:
+        M.set_option("graph_chunk", args.graph_chunk)
     if args.x_defer >= 0:
         M.set_option("x_defer", args.x_defer)
     if args.rev_update >= 0:

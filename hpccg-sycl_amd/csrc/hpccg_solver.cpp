@@ -253,7 +253,8 @@ struct hpccg_hip_matrix {
     double *d_gen_b = nullptr, *d_gen_x0 = nullptr, *d_gen_xexact = nullptr;
     hipStream_t stream = nullptr;
     hipGraphExec_t graph_exec = nullptr;
-    int graph_chunk = 0;
+    int graph_chunk = 0;       // iterations in the captured graph
+    int graph_iters = 8;       // option graph_chunk: iterations per captured graph
     CgArgs graph_args{};
     int graph_variant = -1;
     // hipEvent timing (event_timing option)
@@ -1079,7 +1080,6 @@ int enqueue_prologue(const Ranks& R, bool events)
     return 0;
 }
 
-constexpr int kGraphChunk = 8;  // CG iterations per captured graph
 
 
 int build_graph(hpccg_hip_matrix* M, const CgArgs& a)
@@ -1092,14 +1092,14 @@ int build_graph(hpccg_hip_matrix* M, const CgArgs& a)
     HIP_TRY(hipStreamBeginCapture(M->stream, hipStreamCaptureModeThreadLocal));
     int rc = 0;
     const Ranks R{&M, &a, 1, nullptr};
-    for (int i = 0; i < kGraphChunk && rc == 0; i++) rc = enqueue_iteration(R, -1, i + 1);
+    for (int i = 0; i < M->graph_iters && rc == 0; i++) rc = enqueue_iteration(R, -1, i + 1);
     hipError_t e = hipStreamEndCapture(M->stream, &g);
     if (rc) return rc;
     if (e != hipSuccess) return set_err(HPCCG_HIP_EHIP, "graph capture failed: %s", hipGetErrorString(e));
     e = hipGraphInstantiate(&M->graph_exec, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     if (e != hipSuccess) return set_err(HPCCG_HIP_EHIP, "graph instantiate failed: %s", hipGetErrorString(e));
-    M->graph_chunk = kGraphChunk;
+    M->graph_chunk = M->graph_iters;
     return 0;
 }
 
@@ -1171,17 +1171,18 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     const Ranks R{Ms, av.data(), P, gev.data()};
     if (events) TRY(ensure_events(M, iters + 1));
     TRY(enqueue_prologue(R, events));
-    const bool graph = P == 1 && !events && M->use_graph && M->nranks == 1 && iters >= kGraphChunk;
+    const int chunk = std::max(1, M->graph_iters);
+    const bool graph = P == 1 && !events && M->use_graph && M->nranks == 1 && iters >= chunk;
     int done = 0;
     if (graph) {
         // kernel arguments are baked into the graph: rebuild only when they change
         if (!M->graph_exec || std::memcmp(&M->graph_args, &a, sizeof a) != 0 ||
-            M->graph_variant != M->spmv_variant) {
+            M->graph_variant != M->spmv_variant || M->graph_chunk != chunk) {
             TRY(build_graph(M, a));
             M->graph_args = a;
             M->graph_variant = M->spmv_variant;
         }
-        for (; done + kGraphChunk <= iters; done += kGraphChunk)
+        for (; done + chunk <= iters; done += chunk)
             HIP_TRY(hipGraphLaunch(M->graph_exec, M->stream));
     }
     for (; done < iters; done++) TRY(enqueue_iteration(R, events ? done + 1 : -1, done + 1));
@@ -2002,6 +2003,9 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->redund = (int)value;
     } else if (!std::strcmp(key, "overlap")) {
         M->overlap = (int)value;
+    } else if (!std::strcmp(key, "graph_chunk")) {
+        if (value < 1 || value > 4096) return set_err(HPCCG_HIP_EINVAL, "graph_chunk must be 1..4096");
+        M->graph_iters = (int)value;
     } else if (!std::strcmp(key, "resident_mb")) {
         M->resident_mb = value < 0 ? -1 : value;
     } else if (!std::strcmp(key, "fold")) {
@@ -2109,6 +2113,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "resident_mb")) *value = resident_mb_effective(M);
     else if (!std::strcmp(key, "redund")) *value = redund_effective(M, 2) ? 1 : 0;  // off unless set
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
+    else if (!std::strcmp(key, "graph_chunk")) *value = M->graph_iters;
     else if (!std::strcmp(key, "overlap"))
         *value = (M->overlap && M->nranks > 1 && !M->general && M->halo_b_lo >= 0) ? 1 : 0;
     else if (!std::strcmp(key, "num_external")) *value = M->general ? M->ghost_hi : M->ghost_lo + M->ghost_hi;
