@@ -10,8 +10,8 @@
 // reference key is changed.
 //
 // Multi-GPU (the reference's `mpirun -np P test_HPCCG nx ny nz`): start one
-// process per GPU with WORLD_SIZE / RANK / LOCAL_RANK set (torchrun, or
-// hpccg-sycl_amd/bin/hpccg_launch) and HPCCG_ID_FILE naming a shared path for
+// process per GPU with WORLD_SIZE / RANK / LOCAL_RANK set (python -m
+// torch.distributed.run --no-python ...) and HPCCG_ID_FILE naming a shared path for
 // the RCCL unique id. nz is per rank; the global grid is nx x ny x (P*nz).
 //
 // Environment knobs (the reference only had compile-time switches):
