@@ -124,3 +124,21 @@ def test_group_errors(hp, gpu):
         hp.group_HPCCG(Ms[::-1], [b, b], [x, x], max_iter=10)  # wrong rank order
     with pytest.raises(hp.HPCCGError):
         hp.group_generate(6, 6, 4, 17)  # more than 16 ranks
+
+
+@pytest.mark.parametrize("nx,ny,nz,P,s7", [(33, 17, 9, 3, False), (7, 5, 1, 4, False), (1, 9, 6, 2, True),
+                                           (19, 1, 3, 5, True), (40, 30, 2, 6, False)])
+def test_group_odd_shapes_vs_oracle(hp, gpu, nx, ny, nz, P, s7):
+    """Odd and degenerate slabs (one plane per rank: the ghosts are the whole
+    neighbours; nx or ny = 1; partial last slices) against the serial oracle of
+    the z-stacked global problem (SURVEY 4 multi-GPU oracle), 1e-7."""
+    import oracle
+    Ms = hp.group_generate(nx, ny, nz, P, use_7pt=s7)
+    niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=120)
+    ref = oracle.hpccg(oracle.generate(nx, ny, nz * P, use_7pt=s7), max_iter=120)
+    tr = Ms[0].last_trace()
+    assert tr[0] == ref["trace"][0]
+    assert check_trace(tr, ref["trace"], RTRANS_RTOL_MULTI) >= 3
+    check_final(niters, normr, tr, ref["niters"], ref["normr"], ref["trace"], 120)
+    x = np.concatenate(xs)
+    assert np.max(np.abs(x - 1.0)) <= 1e-12 or ref["normr"] > 1e-15 * ref["trace"][0]
