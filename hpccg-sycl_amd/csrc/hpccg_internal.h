@@ -74,6 +74,10 @@ struct CgArgs {
     const unsigned char* ccodes;  // SELL-512-C: per entry, code of its (column - row) offset
     const int* cdict;             // SELL-512-C: per slice, kCodes offsets
     const int* ldsc;              // SELL-512-C: per slice, LDS position of lane 0's column per code
+    const double* cval;           // SELL-512-V: per slice, kCodes values (codes name (offset, value) pairs)
+    const int* ccount;            // SELL-512-C / -V: per slice, codes in use (dictionary entries to load)
+    const unsigned int* vbase4;   // SELL-512-V4: [nslices + 1] first chunk of each slice (4 slots x 512 rows)
+    const unsigned char* vcodes4; // SELL-512-V4: the V codes, a row's 4 codes of a chunk contiguous
     const int* win_ptr;    // [nslices + 1] into the window arrays
     const int* win_start;  // first local column of the window
     const int* win_len;    // entries
@@ -127,15 +131,20 @@ void launch_ddot(int n, const double* x, const double* y, double* partial, int n
 int ddot_nparts(int n);
 void launch_sparsemv(const CgArgs& a, const double* xext, double* y, int variant, hipStream_t s);
 
-// Device generator (SURVEY 8(f) #1): writes the SELL-512 image, b, xexact.
-// SELL-512-C from the SELL-512 cols on the device (windows optional). ok[0]
-// = 0 if a slice has more than 255 distinct offsets, ok[1] = 0 if a code's
-// entries fall in different windows (no LDS form).
+// SELL-512-C from the SELL-512 cols on the device (windows optional); with
+// vals and cval non-null, SELL-512-V (codes of (offset, value) pairs, cval[s *
+// kCodes + code] = value). ccount[s] = codes in use. ok[0] = 0 if a slice has more than 255 distinct
+// keys, ok[1] = 0 if a code's entries fall in different windows (no LDS form).
 constexpr int kCodes = 256;
 constexpr unsigned kCodePad = 255;
-void launch_build_c(const unsigned int* slice_base, int nslices, const int* cols, const int* win_ptr,
-                    const int* win_start, const int* win_off, const int* win_len, unsigned char* codes,
-                    int* cdict, int* ldsc, int* ok, hipStream_t s);
+void launch_build_c(const unsigned int* slice_base, int nslices, const int* cols, const double* vals,
+                    const int* win_ptr, const int* win_start, const int* win_off, const int* win_len,
+                    unsigned char* codes, int* cdict, double* cval, int* ldsc, int* ccount, int* ok,
+                    hipStream_t s);
+// SELL-512-V4 regrouping of the V codes (vbase4 in chunks of 4 slots).
+void launch_interleave_v4(const unsigned int* slice_base, const unsigned int* vbase4, int nslices,
+                          const unsigned char* codes, unsigned char* out, hipStream_t s);
+// Device generator (SURVEY 8(f) #1): writes the SELL-512 image, b, xexact.
 // With win_* non-null it also writes the SELL-512-L index image (lcols).
 void launch_generate(int nx, int ny, int nz, int rank, int size, int use_7pt, long long col_base,
                      const unsigned int* slice_base, int* cols, double* vals, double* b,

@@ -606,10 +606,11 @@ __device__ __forceinline__ void ld_codes(const unsigned char* __restrict__ p, un
     }
 }
 
-template <int kRpt, bool kNT, bool kFuse, int kW = 0>
+template <int kRpt, bool kNT, bool kFuse, int kW = 0, bool kVal = false>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool prologue)
 {
     __shared__ int sdict[kCodes];
+    __shared__ double sval[kVal ? kCodes : 1];
     int k = 0;
     double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
     if (!prologue) {
@@ -627,7 +628,14 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool pro
     }
     const int s = spmv_slice(a);
     if (s < 0) return;
-    for (int i = threadIdx.x; i < kCodes; i += kSliceRows / kRpt) sdict[i] = a.cdict[(size_t)s * kCodes + i];
+    {
+        const int nc = a.ccount[s];  // codes in use; kCodePad has value 0
+        for (int i = threadIdx.x; i < nc; i += kSliceRows / kRpt) {
+            sdict[i] = a.cdict[(size_t)s * kCodes + i];
+            if constexpr (kVal) sval[i] = a.cval[(size_t)s * kCodes + i];
+        }
+        if (kVal && threadIdx.x == 0) sval[kCodePad] = 0.0;
+    }
     __syncthreads();
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     double* __restrict__ p = cur_p(a, k);
@@ -651,7 +659,13 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool pro
     for (int j = 0; j < w; j++) {
         unsigned c[kRpt];
         ld_codes<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
-        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+        Rows<kRpt> v;
+        if constexpr (kVal) {
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) v.v[i] = sval[c[i]];
+        } else {
+            v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+        }
 #pragma unroll
         for (int i = 0; i < kRpt; i++) {
             double xv = 0.0;
@@ -686,57 +700,295 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool pro
     complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
 }
 
-// SELL-512-C build: one block per slice. An LDS hash of the slice's distinct
-// (column - row) offsets gives the codes; with windows, ldsc[code] is the LDS
+// ---------------------------------------------------------------------------
+// SELL-512-V4: the SELL-512-V codes regrouped in chunks of kVC = 4 slots, row
+// by row inside a chunk (a row's 4 codes are one dword; 2 rows one qword), so
+// a thread fetches 4 slots per load instead of 1. Chunk padding is kCodePad.
+// The kernel gathers x[row + dict[code]] from global memory (L1/L2 hits) with
+// every gather of a chunk in flight; the values come from the slice's LDS
+// dictionary. Same products in the same order as SELL-512. With one row per
+// thread, the p.Ap partial is formed on thread pairs and reduced in the
+// 256-thread tree of the two-rows-per-thread kernels: the same bits.
+// ---------------------------------------------------------------------------
+constexpr int kVC = 4;
+
+__global__ __launch_bounds__(256) void k_interleave_v4(const unsigned int* __restrict__ slice_base,
+                                                       const unsigned int* __restrict__ vbase4, int nslices,
+                                                       const unsigned char* __restrict__ codes,
+                                                       unsigned char* __restrict__ out)
+{
+    const int s = blockIdx.x;
+    if (s >= nslices) return;
+    const size_t e0 = (size_t)slice_base[s] * kSliceRows, e1 = (size_t)slice_base[s + 1] * kSliceRows;
+    unsigned char* o = out + (size_t)vbase4[s] * (kSliceRows * kVC);
+    for (size_t e = e0 + threadIdx.x; e < e1; e += 256) {
+        const int j = (int)((e - e0) / kSliceRows), lane = (int)((e - e0) % kSliceRows);
+        o[(size_t)(j / kVC) * (kSliceRows * kVC) + lane * kVC + j % kVC] = codes[e];
+    }
+}
+
+template <int kRpt, bool kNT>
+__device__ __forceinline__ void ld_chunk(const unsigned char* __restrict__ p, unsigned (&c)[kRpt])
+{
+    if constexpr (kRpt == 1) {
+        c[0] = kNT ? __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p))
+                   : *reinterpret_cast<const unsigned*>(p);
+    } else {
+        static_assert(kRpt == 2, "1 or 2 rows per thread");
+        typedef unsigned u2v __attribute__((ext_vector_type(2)));
+        const u2v t = kNT ? __builtin_nontemporal_load(reinterpret_cast<const u2v*>(p))
+                          : *reinterpret_cast<const u2v*>(p);
+        c[0] = t.x;
+        c[1] = t.y;
+    }
+}
+
+// kPre > 0: the first kPre chunks of codes are loaded before the dictionary
+// barrier (the whole row for widths <= 4 kPre).
+template <int kRpt, bool kNT, bool kFuse, int kW, int kPre = 0>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_v4(CgArgs a, bool prologue)
+{
+    __shared__ int sdict[kCodes];
+    __shared__ double sval[kCodes];
+    __shared__ double spair[kRpt == 1 ? kSliceRows / 2 : 1];
+    __shared__ double wsum[4];
+    int k = 0;
+    double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
+    if (!prologue) {
+        k = a.kst[0];
+        if (kFuse) rr = cur_rr(a);
+        const bool run = cg_run(a, k, kFuse, rr);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = rr;
+            if (run)
+                stamp(a, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = spmv_slice(a);
+    if (s < 0) return;
+    const unsigned c0 = a.vbase4[s];
+    const int nch = kW > 0 ? (kW + kVC - 1) / kVC : (int)(a.vbase4[s + 1] - c0);
+    const unsigned char* __restrict__ cp =
+        a.vcodes4 + (size_t)c0 * (kSliceRows * kVC) + (size_t)threadIdx.x * (kRpt * kVC);
+    // dictionary loads first (the first kDict entries without waiting for the
+    // count), then the code prefetch: vmcnt retires in order
+    constexpr int kDict = 32;
+    const int nc = a.ccount[s];  // codes in use; kCodePad has value 0
+    int dk = 0;
+    double dv = 0.0;
+    if (threadIdx.x < kDict) {
+        dk = a.cdict[(size_t)s * kCodes + threadIdx.x];
+        dv = a.cval[(size_t)s * kCodes + threadIdx.x];
+    }
+    constexpr int kP = kPre > 0 ? kPre : 1;
+    unsigned cpre[kP][kRpt];
+#pragma unroll
+    for (int q = 0; q < kPre; q++)
+        if (q < nch) ld_chunk<kRpt, kNT>(cp + (size_t)q * (kSliceRows * kVC), cpre[q]);
+    if (threadIdx.x < kDict) {
+        sdict[threadIdx.x] = dk;
+        sval[threadIdx.x] = dv;
+    }
+    for (int i = kDict + threadIdx.x; i < nc; i += kSliceRows / kRpt) {
+        sdict[i] = a.cdict[(size_t)s * kCodes + i];
+        sval[i] = a.cval[(size_t)s * kCodes + i];
+    }
+    if (threadIdx.x == 0) sval[kCodePad] = 0.0;
+    __syncthreads();
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    double* __restrict__ p = cur_p(a, k);
+    double beta = 0.0;
+    const double* pold = a.r;
+    if constexpr (kFuse) {
+        beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
+        pold = (k == 1) ? a.r : cur_p(a, k - 1);
+    }
+    const double* __restrict__ xext = p - a.ghost_lo;
+    double sum[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+    auto chunk = [&](const unsigned (&cw)[kRpt]) {
+#pragma unroll
+        for (int jj = 0; jj < kVC; jj++) {
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) {
+                const unsigned c = (cw[i] >> (8 * jj)) & 0xFFu;
+                double xv = 0.0;
+                if (c != kCodePad) {
+                    const int col = row + i + sdict[c];
+                    if constexpr (kFuse) xv = a.r[col - a.ghost_lo] + beta * pold[col - a.ghost_lo];
+                    else xv = xext[col];
+                }
+                sum[i] = sum[i] + sval[c] * xv;
+            }
+        }
+    };
+#pragma unroll
+    for (int q = 0; q < kPre; q++)
+        if (q < nch) chunk(cpre[q]);
+#pragma unroll(kW > 0 ? (kW + kVC - 1) / kVC : 2)
+    for (int q = kPre; q < nch; q++) {
+        unsigned cw[kRpt];
+        ld_chunk<kRpt, kNT>(cp + (size_t)q * (kSliceRows * kVC), cw);
+        chunk(cw);
+    }
+    Rows<kRpt> pv;
+    if constexpr (kFuse) {
+        const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+        const Rows<kRpt> yv = ld<kRpt>(pold + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + beta * yv.v[i];
+        st_rows<kRpt>(p, row, a.n, pv);
+    } else {
+        pv = ld<kRpt>(p + row);
+    }
+    Rows<kRpt> o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+    st_rows<kRpt>(a.Ap, row, a.n, o);
+    if (prologue) return;
+    double bs;
+    if constexpr (kRpt == 2) {
+        double d = 0.0;
+#pragma unroll
+        for (int i = 0; i < kRpt; i++)
+            if (row + i < a.n) d += pv.v[i] * o.v[i];
+        bs = block_sum<kSliceRows / kRpt>(d);
+    } else {
+        // (0 + p_2t Ap_2t) + p_2t+1 Ap_2t+1 on the even lane (an absent row
+        // adds +0: the sum is never -0), then block_sum<256>'s tree
+        const double t = (row < a.n) ? pv.v[0] * o.v[0] : 0.0;
+        const double u = from_lane_plus<1>(t);
+        if ((threadIdx.x & 1) == 0) spair[threadIdx.x >> 1] = (0.0 + t) + u;
+        __syncthreads();
+        double v = 0.0;
+        if (threadIdx.x < kSliceRows / 2) v = wave_sum(spair[threadIdx.x]);
+        if (threadIdx.x < kSliceRows / 2 && (threadIdx.x & (kWave - 1)) == 0) wsum[threadIdx.x / kWave] = v;
+        __syncthreads();
+        bs = 0.0;
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) bs += wsum[i];
+        }
+    }
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
+}
+
+// SELL-512-C / -V build: one block per slice. An LDS hash of the slice's
+// distinct keys gives the codes: the (column - row) offset (C), or the pair
+// (offset, value) (V; the values get their own hash first, so a pair is one
+// 64-bit key: offset, value code). With windows, ldsc[code] is the LDS
 // position of row 0's column for that offset, and every entry must agree.
+// ok[0] = 0: more than 255 keys in a slice; ok[1] = 0: no LDS form.
 __global__ __launch_bounds__(256) void k_build_c(const unsigned int* __restrict__ slice_base, int nslices,
-                                                 const int* __restrict__ cols, const int* __restrict__ win_ptr,
+                                                 const int* __restrict__ cols, const double* __restrict__ vals,
+                                                 const int* __restrict__ win_ptr,
                                                  const int* __restrict__ win_start, const int* __restrict__ win_off,
                                                  const int* __restrict__ win_len,
                                                  unsigned char* __restrict__ codes, int* __restrict__ cdict,
-                                                 int* __restrict__ ldsc, int* ok)
+                                                 double* __restrict__ cval, int* __restrict__ ldsc,
+                                                 int* __restrict__ ccount, int* ok)
 {
+    typedef unsigned long long u64;
     constexpr int kH = 1024;
-    constexpr int kEmpty = INT_MIN;
-    __shared__ int keys[kH];
+    constexpr u64 kEmpty = ~0ull;  // neither a pair key (value code <= 254) nor, checked, a value
+    constexpr int kEmptyPos = INT_MIN;
+    __shared__ u64 keys[kH];
     __shared__ int code_of[kH];
+    __shared__ u64 vkeys[kH];
+    __shared__ int vcode_of[kH];
+    __shared__ double svals[kCodePad];
     __shared__ int sldsc[kCodes];
-    __shared__ int cnt;
+    __shared__ int cnt, vcnt;
     const int s = blockIdx.x;
     if (s >= nslices) return;
-    for (int h = threadIdx.x; h < kH; h += 256) keys[h] = kEmpty;
-    if (threadIdx.x == 0) cnt = 0;
+    for (int h = threadIdx.x; h < kH; h += 256) {
+        keys[h] = kEmpty;
+        vkeys[h] = kEmpty;
+    }
+    if (threadIdx.x == 0) {
+        cnt = 0;
+        vcnt = 0;
+    }
     for (int i = threadIdx.x; i < kCodes; i += 256) {
         cdict[(size_t)s * kCodes + i] = 0;
-        sldsc[i] = kEmpty;
+        if (cval) cval[(size_t)s * kCodes + i] = 0.0;  // code kCodePad: value 0
+        sldsc[i] = kEmptyPos;
     }
     __syncthreads();
     const int row0 = s * kSliceRows;
     const size_t e0 = (size_t)slice_base[s] * kSliceRows, e1 = (size_t)slice_base[s + 1] * kSliceRows;
-    auto slot_of = [](int d) { return (int)(((unsigned)d * 2654435761u) >> 22); };  // 10 bits
+    auto slot_of = [](u64 k) { return (int)(((k ^ (k >> 29)) * 0x9E3779B97F4A7C15ull) >> 54); };  // 10 bits
+    auto insert = [&](u64* tab, u64 key) {
+        int h = slot_of(key);
+        for (int probe = 0; probe < kH; probe++) {
+            const u64 old = atomicCAS(&tab[h], kEmpty, key);
+            if (old == kEmpty || old == key) return;
+            h = (h + 1) & (kH - 1);
+        }
+    };
+    auto find = [&](const u64* tab, u64 key) {
+        int h = slot_of(key);
+        for (int probe = 0; probe < kH && tab[h] != key; probe++) h = (h + 1) & (kH - 1);
+        return tab[h] == key ? h : -1;
+    };
+    // values (V only)
+    if (cval) {
+        for (size_t e = e0 + threadIdx.x; e < e1; e += 256) {
+            if (cols[e] < 0) continue;
+            const u64 vb = (u64)__double_as_longlong(vals[e]);
+            if (vb == kEmpty) ok[0] = 0;  // that NaN pattern is the empty marker
+            else insert(vkeys, vb);
+        }
+        __syncthreads();
+        for (int h = threadIdx.x; h < kH; h += 256)
+            if (vkeys[h] != kEmpty) {
+                const int vc = atomicAdd(&vcnt, 1);
+                vcode_of[h] = vc;
+                if (vc < kCodePad) svals[vc] = __longlong_as_double((long long)vkeys[h]);
+            }
+        __syncthreads();
+        if (vcnt > kCodePad) {
+            if (threadIdx.x == 0) ok[0] = 0;
+            return;
+        }
+    }
+    auto key_of = [&](size_t e, int d) -> u64 {
+        u64 vc = 0;
+        if (cval) {
+            const int h = find(vkeys, (u64)__double_as_longlong(vals[e]));
+            vc = h < 0 ? 0xFFFFull : (u64)vcode_of[h];
+        }
+        return ((u64)(unsigned)d << 32) | vc;
+    };
     for (size_t e = e0 + threadIdx.x; e < e1; e += 256) {
         const int c = cols[e];
         if (c < 0) continue;
-        const int d = c - (row0 + (int)((e - e0) % kSliceRows));
-        int h = slot_of(d);
-        for (int probe = 0; probe < kH; probe++) {
-            const int old = atomicCAS(&keys[h], kEmpty, d);
-            if (old == kEmpty || old == d) break;
-            h = (h + 1) & (kH - 1);
-        }
+        insert(keys, key_of(e, c - (row0 + (int)((e - e0) % kSliceRows))));
     }
     __syncthreads();
     for (int h = threadIdx.x; h < kH; h += 256) {
         if (keys[h] == kEmpty) continue;
         const int code = atomicAdd(&cnt, 1);
         code_of[h] = code;
-        if (code < kCodePad) cdict[(size_t)s * kCodes + code] = keys[h];
+        if (code < kCodePad) {
+            cdict[(size_t)s * kCodes + code] = (int)(unsigned)(keys[h] >> 32);
+            if (cval) {
+                const unsigned vc = (unsigned)(keys[h] & 0xFFFFFFFFull);
+                if (vc < kCodePad) cval[(size_t)s * kCodes + code] = svals[vc];
+                else ok[0] = 0;
+            }
+        }
     }
     __syncthreads();
     if (cnt > kCodePad) {
         if (threadIdx.x == 0) ok[0] = 0;
         return;
     }
+    if (threadIdx.x == 0) ccount[s] = cnt;
     const int w0 = win_ptr ? win_ptr[s] : 0, w1 = win_ptr ? win_ptr[s + 1] : 0;
     for (size_t e = e0 + threadIdx.x; e < e1; e += 256) {
         const int c = cols[e];
@@ -745,11 +997,8 @@ __global__ __launch_bounds__(256) void k_build_c(const unsigned int* __restrict_
             continue;
         }
         const int lane = (int)((e - e0) % kSliceRows);
-        const int d = c - (row0 + lane);
-        int h = slot_of(d);
-        int probe = 0;
-        while (keys[h] != d && probe++ < kH) h = (h + 1) & (kH - 1);  // present: <= 255 keys inserted
-        if (keys[h] != d) {
+        const int h = find(keys, key_of(e, c - (row0 + lane)));  // present: <= 255 keys inserted
+        if (h < 0) {
             ok[0] = 0;
             continue;
         }
@@ -763,8 +1012,8 @@ __global__ __launch_bounds__(256) void k_build_c(const unsigned int* __restrict_
                 continue;
             }
             const int pos0 = win_off[w] + (c - win_start[w]) - lane;  // position of lane 0's column
-            const int old = atomicCAS(&sldsc[code], kEmpty, pos0);
-            if (old != kEmpty && old != pos0) ok[1] = 0;
+            const int old = atomicCAS(&sldsc[code], kEmptyPos, pos0);
+            if (old != kEmptyPos && old != pos0) ok[1] = 0;
         }
     }
     if (ldsc) {
@@ -884,7 +1133,8 @@ __device__ __forceinline__ int lds_pos(unsigned c, int lrow, const int* sldsc)
         return (int)c;
 }
 
-template <int kRpt, bool kNT, bool kCode, int kPre, int kP>
+// kVal (SELL-512-V): no value stream; the value of code c is sval[c].
+template <int kRpt, bool kNT, bool kCode, bool kVal, int kPre, int kP>
 __device__ __forceinline__ void lds_prefetch(const double* __restrict__ vp,
                                              const typename LdsIdx<kCode>::T* __restrict__ cp, int wdt,
                                              Rows<kRpt> (&vpre)[kP], unsigned (&cpre)[kP][kRpt])
@@ -893,22 +1143,29 @@ __device__ __forceinline__ void lds_prefetch(const double* __restrict__ vp,
     for (int j = 0; j < kPre; j++) {
         if (j < wdt) {
             ld_idx<kRpt, kNT, kCode>(cp + (size_t)j * kSliceRows, cpre[j]);
-            vpre[j] = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+            if constexpr (!kVal) vpre[j] = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
         }
     }
 }
 
-template <int kRpt, bool kNT, bool kCode>
+template <int kRpt, bool kNT, bool kCode, bool kVal>
 __device__ __forceinline__ void lds_stream(const double* __restrict__ vp,
                                            const typename LdsIdx<kCode>::T* __restrict__ cp, int j0, int wdt,
-                                           const double* xs, const int* sldsc, double (&sum)[kRpt])
+                                           const double* xs, const int* sldsc, const double* sval,
+                                           double (&sum)[kRpt])
 {
     const int lrow = threadIdx.x * kRpt;
-#pragma unroll 3
+#pragma unroll(kVal ? 4 : 3)
     for (int j = j0; j < wdt; j++) {
         unsigned c[kRpt];
         ld_idx<kRpt, kNT, kCode>(cp + (size_t)j * kSliceRows, c);
-        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+        Rows<kRpt> v;
+        if constexpr (kVal) {
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) v.v[i] = sval[c[i]];
+        } else {
+            v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+        }
 #pragma unroll
         for (int i = 0; i < kRpt; i++) {
             const double xv = (c[i] != LdsIdx<kCode>::kPad) ? xs[lds_pos<kCode>(c[i], lrow + i, sldsc)] : 0.0;
@@ -919,11 +1176,16 @@ __device__ __forceinline__ void lds_stream(const double* __restrict__ vp,
 
 // kPre > 0: the first kPre slots of the matrix stream are loaded before the
 // window staging and its barrier, so the block's HBM stream starts at once.
-template <int kRpt, bool kNT, bool kFuse, int kPre, bool kCode = false>
+// kFmt: 0 SELL-512-L (16-bit LDS indices + values), 1 SELL-512-C (offset
+// codes + values), 2 SELL-512-V (codes of (offset, value) pairs only).
+template <int kRpt, bool kNT, bool kFuse, int kPre, int kFmt = 0>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool prologue)
 {
+    constexpr bool kCode = kFmt != 0;
+    constexpr bool kVal = kFmt == 2;
     extern __shared__ __attribute__((aligned(16))) double xs[];
     __shared__ int sldsc[kCode ? kCodes : 1];
+    __shared__ double sval[kVal ? kCodes : 1];
     using IdxT = typename LdsIdx<kCode>::T;
     int k = 0;
     double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
@@ -956,11 +1218,18 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     // spread evenly over the XCDs), the rest non-temporal
     const bool nt = kNT && (xcd_slice(a.sgrid) % (a.sgrid / kNumXcd)) >= a.nt_split;
     if (nt)
-        lds_prefetch<kRpt, true, kCode, kPre>(vp, cp, wdt, vpre, cpre);
+        lds_prefetch<kRpt, true, kCode, kVal, kPre>(vp, cp, wdt, vpre, cpre);
     else
-        lds_prefetch<kRpt, false, kCode, kPre>(vp, cp, wdt, vpre, cpre);
+        lds_prefetch<kRpt, false, kCode, kVal, kPre>(vp, cp, wdt, vpre, cpre);
     if constexpr (kCode)
-        for (int i = threadIdx.x; i < kCodes; i += kSliceRows / kRpt) sldsc[i] = a.ldsc[(size_t)s * kCodes + i];
+    {
+        const int nc = a.ccount[s];  // codes in use; kCodePad has value 0
+        for (int i = threadIdx.x; i < nc; i += kSliceRows / kRpt) {
+            sldsc[i] = a.ldsc[(size_t)s * kCodes + i];
+            if constexpr (kVal) sval[i] = a.cval[(size_t)s * kCodes + i];
+        }
+        if (kVal && threadIdx.x == 0) sval[kCodePad] = 0.0;
+    }
     // stage the windows; with kFuse the staged value of an own row is
     // p_k = r + beta*p_{k-1}, the exact expression k_p_update stores
     double beta = 0.0;
@@ -994,14 +1263,15 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
                 const double xv = (cpre[j][i] != LdsIdx<kCode>::kPad)
                                       ? xs[lds_pos<kCode>(cpre[j][i], threadIdx.x * kRpt + i, sldsc)]
                                       : 0.0;
-                sum[i] = sum[i] + vpre[j].v[i] * xv;
+                const double v = kVal ? sval[cpre[j][i]] : vpre[j].v[i];
+                sum[i] = sum[i] + v * xv;
             }
         }
     }
     if (nt)
-        lds_stream<kRpt, true, kCode>(vp, cp, kPre, wdt, xs, sldsc, sum);
+        lds_stream<kRpt, true, kCode, kVal>(vp, cp, kPre, wdt, xs, sldsc, sval, sum);
     else
-        lds_stream<kRpt, false, kCode>(vp, cp, kPre, wdt, xs, sldsc, sum);
+        lds_stream<kRpt, false, kCode, kVal>(vp, cp, kPre, wdt, xs, sldsc, sval, sum);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     Rows<kRpt> o;
 #pragma unroll
@@ -1477,13 +1747,21 @@ void launch_cg_p_update(const CgArgs& a, hipStream_t s)
     hipLaunchKernelGGL(k_p_update<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
 }
 
-void launch_build_c(const unsigned int* slice_base, int nslices, const int* cols, const int* win_ptr,
-                    const int* win_start, const int* win_off, const int* win_len, unsigned char* codes,
-                    int* cdict, int* ldsc, int* ok, hipStream_t s)
+void launch_interleave_v4(const unsigned int* slice_base, const unsigned int* vbase4, int nslices,
+                          const unsigned char* codes, unsigned char* out, hipStream_t s)
 {
     if (nslices <= 0) return;
-    hipLaunchKernelGGL(k_build_c, dim3(nslices), dim3(256), 0, s, slice_base, nslices, cols, win_ptr, win_start,
-                       win_off, win_len, codes, cdict, ldsc, ok);
+    hipLaunchKernelGGL(k_interleave_v4, dim3(nslices), dim3(256), 0, s, slice_base, vbase4, nslices, codes, out);
+}
+
+void launch_build_c(const unsigned int* slice_base, int nslices, const int* cols, const double* vals,
+                    const int* win_ptr, const int* win_start, const int* win_off, const int* win_len,
+                    unsigned char* codes, int* cdict, double* cval, int* ldsc, int* ccount, int* ok,
+                    hipStream_t s)
+{
+    if (nslices <= 0) return;
+    hipLaunchKernelGGL(k_build_c, dim3(nslices), dim3(256), 0, s, slice_base, nslices, cols, vals, win_ptr,
+                       win_start, win_off, win_len, codes, cdict, cval, ldsc, ccount, ok);
 }
 
 void launch_cg_pack(const CgArgs& a, const int* idx, int cnt, double* buf, bool prologue, hipStream_t s)
@@ -1519,16 +1797,28 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
             hipLaunchKernelGGL((k_spmv<RPT, W, MINW, NT, false>), dim3(a.sgrid),                   \
                                dim3(kSliceRows / RPT), 0, s, a, prologue);                          \
     } while (0)
-#define HPCCG_SPMV_CW(RPT, NT, W)                                                                  \
+#define HPCCG_SPMV_CWV(RPT, NT, W, VAL)                                                            \
     do {                                                                                           \
         if (a.fuse_p && !prologue)                                                                 \
-            hipLaunchKernelGGL((k_spmv_c<RPT, NT, true, W>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, a, \
-                               prologue);                                                          \
+            hipLaunchKernelGGL((k_spmv_c<RPT, NT, true, W, VAL>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, \
+                               a, prologue);                                                       \
         else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_c<RPT, NT, false, W>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, a, \
-                               prologue);                                                          \
+            hipLaunchKernelGGL((k_spmv_c<RPT, NT, false, W, VAL>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, \
+                               s, a, prologue);                                                    \
     } while (0)
+#define HPCCG_SPMV_V4P(RPT, NT, W, PRE)                                                            \
+    do {                                                                                           \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_v4<RPT, NT, true, W, PRE>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, s, \
+                               a, prologue);                                                       \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_v4<RPT, NT, false, W, PRE>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, \
+                               s, a, prologue);                                                    \
+    } while (0)
+#define HPCCG_SPMV_V4(RPT, NT, W) HPCCG_SPMV_V4P(RPT, NT, W, 0)
+#define HPCCG_SPMV_CW(RPT, NT, W) HPCCG_SPMV_CWV(RPT, NT, W, false)
 #define HPCCG_SPMV_C(RPT, NT) HPCCG_SPMV_CW(RPT, NT, 0)
+#define HPCCG_SPMV_V(RPT, NT) HPCCG_SPMV_CWV(RPT, NT, 0, true)
 #define HPCCG_SPMV_LDSX(RPT, NT, PRE, CODE)                                                        \
     do {                                                                                           \
         const size_t smem = (size_t)a.lds_doubles * sizeof(double);                                \
@@ -1539,7 +1829,7 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
             hipLaunchKernelGGL((k_spmv_lds<RPT, NT, false, PRE, CODE>), dim3(a.sgrid), dim3(kSliceRows / RPT), \
                                smem, s, a, prologue);                                              \
     } while (0)
-#define HPCCG_SPMV_LDS(RPT, NT, PRE) HPCCG_SPMV_LDSX(RPT, NT, PRE, false)
+#define HPCCG_SPMV_LDS(RPT, NT, PRE) HPCCG_SPMV_LDSX(RPT, NT, PRE, 0)
 bool spmv_variant_ok(int v)
 {
     switch (v) {
@@ -1547,6 +1837,10 @@ bool spmv_variant_ok(int v)
     case 1000: case 1001: case 1002: case 1027: case 1007: case 9999:
     case 2000: case 2001: case 2002: case 2100: case 2200: case 2208: case 2300: case 2308:
     case 3000: case 3001: case 3002: case 3100: case 3007: case 3027: case 4000: case 4200: case 4300: case 4202: case 4206: case 4208:
+    case 5000: case 5100: case 5200: case 5208: case 5300: case 5308: case 5401: case 5404: case 5204:
+    case 6000: case 6100: case 6104: case 6001:
+    case 7001: case 7101: case 7002: case 7102: case 7027: case 7127: case 7007: case 7107:
+    case 7201: case 7202: case 7301: case 7302: case 7204:
         return true;
     default:
         return false;
@@ -1576,12 +1870,38 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 2208: HPCCG_SPMV_LDS(2, true, 8); break;
     case 2300: HPCCG_SPMV_LDS(2, false, 4); break;
     case 2308: HPCCG_SPMV_LDS(2, false, 8); break;
-    case 4200: HPCCG_SPMV_LDSX(2, true, 4, true); break;
-    case 4202: HPCCG_SPMV_LDSX(2, true, 2, true); break;
-    case 4206: HPCCG_SPMV_LDSX(2, true, 6, true); break;
-    case 4208: HPCCG_SPMV_LDSX(2, true, 8, true); break;
-    case 4300: HPCCG_SPMV_LDSX(2, false, 4, true); break;
-    case 4000: HPCCG_SPMV_LDSX(2, true, 0, true); break;
+    case 4200: HPCCG_SPMV_LDSX(2, true, 4, 1); break;
+    case 4202: HPCCG_SPMV_LDSX(2, true, 2, 1); break;
+    case 4206: HPCCG_SPMV_LDSX(2, true, 6, 1); break;
+    case 4208: HPCCG_SPMV_LDSX(2, true, 8, 1); break;
+    case 4300: HPCCG_SPMV_LDSX(2, false, 4, 1); break;
+    case 4000: HPCCG_SPMV_LDSX(2, true, 0, 1); break;
+    case 5200: HPCCG_SPMV_LDSX(2, true, 4, 2); break;
+    case 5208: HPCCG_SPMV_LDSX(2, true, 8, 2); break;
+    case 5300: HPCCG_SPMV_LDSX(2, false, 4, 2); break;
+    case 5308: HPCCG_SPMV_LDSX(2, false, 8, 2); break;
+    case 5000: HPCCG_SPMV_LDSX(2, true, 0, 2); break;
+    case 5100: HPCCG_SPMV_LDSX(2, false, 0, 2); break;
+    case 5401: HPCCG_SPMV_LDSX(1, false, 8, 2); break;
+    case 5404: HPCCG_SPMV_LDSX(4, false, 4, 2); break;
+    case 5204: HPCCG_SPMV_LDSX(4, true, 4, 2); break;
+    case 6000: HPCCG_SPMV_V(2, true); break;
+    case 6100: HPCCG_SPMV_V(2, false); break;
+    case 6104: HPCCG_SPMV_V(4, false); break;
+    case 6001: HPCCG_SPMV_V(1, true); break;
+    case 7001: HPCCG_SPMV_V4(1, true, 0); break;
+    case 7101: HPCCG_SPMV_V4(1, false, 0); break;
+    case 7002: HPCCG_SPMV_V4(2, true, 0); break;
+    case 7102: HPCCG_SPMV_V4(2, false, 0); break;
+    case 7027: HPCCG_SPMV_V4(1, true, 27); break;
+    case 7127: HPCCG_SPMV_V4(1, false, 27); break;
+    case 7007: HPCCG_SPMV_V4(1, true, 7); break;
+    case 7107: HPCCG_SPMV_V4(1, false, 7); break;
+    case 7201: HPCCG_SPMV_V4P(1, true, 0, 8); break;
+    case 7202: HPCCG_SPMV_V4P(2, true, 0, 8); break;
+    case 7301: HPCCG_SPMV_V4P(1, false, 0, 8); break;
+    case 7302: HPCCG_SPMV_V4P(2, false, 0, 8); break;
+    case 7204: HPCCG_SPMV_V4P(2, true, 0, 4); break;
     case 3000: HPCCG_SPMV_C(2, true); break;
     case 3001: HPCCG_SPMV_C(1, true); break;
     case 3002: HPCCG_SPMV_C(4, true); break;
@@ -1596,6 +1916,10 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
 #undef HPCCG_SPMV_LDSX
 #undef HPCCG_SPMV_C
 #undef HPCCG_SPMV_CW
+#undef HPCCG_SPMV_CWV
+#undef HPCCG_SPMV_V
+#undef HPCCG_SPMV_V4
+#undef HPCCG_SPMV_V4P
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
 {

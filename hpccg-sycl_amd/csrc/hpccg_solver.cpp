@@ -211,7 +211,7 @@ struct hpccg_hip_matrix {
     int overlap = 1;
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_pb = nullptr, ev_halo = nullptr;
-    long long nnz = 0, nslots = 0;
+    long long nnz = 0, nslots = 0, nslots4 = 0;
     int nslices = 0, grid = 0, width = 0, uniform = 0;
     int spmv_variant = 0;
     int use_graph = 1;
@@ -226,7 +226,14 @@ struct hpccg_hip_matrix {
     // SELL-512-C (per-slice offset dictionary + 1-byte codes)
     int has_c = 0, has_c_lds = 0;
     unsigned char* d_ccodes = nullptr;
-    int *d_cdict = nullptr, *d_ldsc = nullptr;
+    int *d_cdict = nullptr, *d_ldsc = nullptr, *d_ccount = nullptr;
+    // SELL-512-V (per-slice dictionary of (offset, value) pairs + 1-byte codes)
+    int has_v = 0, has_v_lds = 0;
+    unsigned char* d_vcodes = nullptr;
+    int *d_vdict = nullptr, *d_vldsc = nullptr, *d_vcount = nullptr;
+    double* d_vval = nullptr;
+    unsigned int* d_vbase4 = nullptr;  // SELL-512-V4: the V codes in 4-slot chunks
+    unsigned char* d_vcodes4 = nullptr;
     int *d_win_ptr = nullptr, *d_win_start = nullptr, *d_win_len = nullptr, *d_win_off = nullptr;
     // workspace (padded to a multiple of kSliceRows rows)
     size_t npad = 0;
@@ -278,7 +285,9 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_tickets,
                     M->d_kst,        M->d_hist,    M->d_stamps, M->d_ddot_partial, M->d_gen_b,
                     M->d_gen_x0,     M->d_gen_xexact, M->d_lcols, M->d_win_ptr, M->d_win_start,
-                    M->d_win_len,    M->d_win_off, M->d_send_idx, M->d_send_buf, M->d_ccodes, M->d_cdict, M->d_ldsc};
+                    M->d_win_len,    M->d_win_off, M->d_send_idx, M->d_send_buf, M->d_ccodes, M->d_cdict, M->d_ldsc,
+                    M->d_vcodes,     M->d_vdict,   M->d_vval,  M->d_vldsc, M->d_vbase4, M->d_vcodes4,
+                    M->d_ccount,     M->d_vcount};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -518,38 +527,67 @@ int exchange_plan(hpccg_hip_matrix* M, int* mode = nullptr, std::vector<int>* al
     return 0;
 }
 
-// SELL-512-C from the uploaded SELL-512 cols (and windows, if any) on the
-// device; dropped when a slice has more than 255 distinct offsets, LDS form
-// dropped when a code's entries fall in different windows.
-int build_c_image(hpccg_hip_matrix* M)
+// SELL-512-C and SELL-512-V from the uploaded SELL-512 image (and windows, if
+// any) on the device. A format is dropped when a slice has more than 255
+// distinct keys (C: offsets; V: (offset, value) pairs), its LDS form when a
+// code's entries fall in different windows.
+int build_code_image(hpccg_hip_matrix* M, bool with_vals, unsigned char** codes, int** dict, double** val,
+                     int** ldsc, int** count, int* has, int* has_lds)
 {
     const size_t ndict = (size_t)std::max(1, M->nslices) * kCodes;
-    HIP_TRY(hipMalloc(&M->d_ccodes, std::max<size_t>(1, (size_t)M->nslots)));
-    HIP_TRY(hipMalloc(&M->d_cdict, sizeof(int) * ndict));
-    if (M->has_lds) HIP_TRY(hipMalloc(&M->d_ldsc, sizeof(int) * ndict));
+    HIP_TRY(hipMalloc(codes, std::max<size_t>(1, (size_t)M->nslots)));
+    HIP_TRY(hipMalloc(count, sizeof(int) * std::max(1, M->nslices)));
+    HIP_TRY(hipMalloc(dict, sizeof(int) * ndict));
+    if (with_vals) HIP_TRY(hipMalloc(val, sizeof(double) * ndict));
+    if (M->has_lds) HIP_TRY(hipMalloc(ldsc, sizeof(int) * ndict));
     int* d_ok = nullptr;
     HIP_TRY(hipMalloc(&d_ok, sizeof(int) * 2));
     const int ones[2] = {1, 1};
     HIP_TRY(hipMemcpyAsync(d_ok, ones, sizeof ones, hipMemcpyHostToDevice, M->stream));
-    launch_build_c(M->d_slice_base, M->nslices, M->d_cols, M->has_lds ? M->d_win_ptr : nullptr, M->d_win_start,
-                   M->d_win_off, M->d_win_len, M->d_ccodes, M->d_cdict, M->d_ldsc, d_ok, M->stream);
+    launch_build_c(M->d_slice_base, M->nslices, M->d_cols, with_vals ? M->d_vals : nullptr,
+                   M->has_lds ? M->d_win_ptr : nullptr, M->d_win_start, M->d_win_off, M->d_win_len, *codes, *dict,
+                   with_vals ? *val : nullptr, M->has_lds ? *ldsc : nullptr, *count, d_ok, M->stream);
     HIP_TRY(hipGetLastError());
     int ok[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(ok, d_ok, sizeof ok, hipMemcpyDeviceToHost, M->stream));
     HIP_TRY(hipStreamSynchronize(M->stream));
     (void)hipFree(d_ok);
-    M->has_c = ok[0];
-    M->has_c_lds = ok[0] && ok[1] && M->has_lds;
-    if (!M->has_c_lds && M->d_ldsc) {
-        (void)hipFree(M->d_ldsc);
-        M->d_ldsc = nullptr;
+    *has = ok[0];
+    *has_lds = ok[0] && ok[1] && M->has_lds;
+    auto drop = [](auto** q) {
+        if (*q) (void)hipFree(*q);
+        *q = nullptr;
+    };
+    if (!*has_lds) drop(ldsc);
+    if (!*has) {
+        drop(codes);
+        drop(dict);
+        drop(count);
+        if (val) drop(val);
     }
-    if (!M->has_c) {
-        (void)hipFree(M->d_ccodes);
-        (void)hipFree(M->d_cdict);
-        M->d_ccodes = nullptr;
-        M->d_cdict = nullptr;
-    }
+    return 0;
+}
+
+int build_c_image(hpccg_hip_matrix* M)
+{
+    TRY(build_code_image(M, false, &M->d_ccodes, &M->d_cdict, nullptr, &M->d_ldsc, &M->d_ccount, &M->has_c,
+                         &M->has_c_lds));
+    TRY(build_code_image(M, true, &M->d_vcodes, &M->d_vdict, &M->d_vval, &M->d_vldsc, &M->d_vcount, &M->has_v,
+                         &M->has_v_lds));
+    if (!M->has_v || M->nslices < 1) return 0;
+    // SELL-512-V4: slice s owns chunks [vbase4[s], vbase4[s + 1]) of 4 slots
+    std::vector<unsigned int> sb(M->nslices + 1), vb(M->nslices + 1, 0);
+    HIP_TRY(hipMemcpy(sb.data(), M->d_slice_base, sizeof(unsigned int) * sb.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < M->nslices; i++) vb[i + 1] = vb[i] + (sb[i + 1] - sb[i] + 3) / 4;
+    const size_t bytes = (size_t)vb[M->nslices] * kSliceRows * 4;
+    M->nslots4 = (long long)vb[M->nslices] * 4 * kSliceRows;
+    HIP_TRY(hipMalloc(&M->d_vbase4, sizeof(unsigned int) * vb.size()));
+    HIP_TRY(hipMemcpy(M->d_vbase4, vb.data(), sizeof(unsigned int) * vb.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&M->d_vcodes4, std::max<size_t>(1, bytes)));
+    HIP_TRY(hipMemsetAsync(M->d_vcodes4, (int)kCodePad, bytes, M->stream));
+    launch_interleave_v4(M->d_slice_base, M->d_vbase4, M->nslices, M->d_vcodes, M->d_vcodes4, M->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(M->stream));
     return 0;
 }
 
@@ -608,6 +646,17 @@ int ensure_hist(hpccg_hip_matrix* M, int max_iter)
 // Infinity Cache (>= 128^3: nt 5-12 % faster; <= 100^3: default policy 2-20 %
 // faster). The LDS kernels prefetch 4 matrix slots ahead of the window staging
 // barrier (2200/2300; in-CG 200^3: 409-415 vs 420-441 us per SpMV, 100^3 even).
+// Which image variant v needs that M lacks (nullptr: none).
+const char* variant_unavailable(const hpccg_hip_matrix* M, int v)
+{
+    if (v >= 2000 && v < 3000 && !M->has_lds) return "the SELL-512-L windows";
+    if (v >= 3000 && v < 4000 && !M->has_c) return "the SELL-512-C image";
+    if (v >= 4000 && v < 5000 && !M->has_c_lds) return "the SELL-512-C LDS image";
+    if (v >= 5000 && v < 6000 && !M->has_v_lds) return "the SELL-512-V LDS image";
+    if (v >= 6000 && v < 8000 && !M->has_v) return "the SELL-512-V image";
+    return nullptr;
+}
+
 int choose_variant(const hpccg_hip_matrix* M)
 {
     const double rows = std::max(1, M->nrow);
@@ -616,15 +665,25 @@ int choose_variant(const hpccg_hip_matrix* M)
     const bool big = image > 180e6;
     // SELL-512-C (1-byte offset codes, 9 B per slot) where the image allows it:
     // 200^3 in-CG SpMV 407-414 vs 433 us (LDS), 7-pt 256^3 265-272 vs 328-340 us
+    // SELL-512-V4 (1-byte (offset, value) codes in 4-slot chunks, values from
+    // the slice dictionary; ~1 B per slot) wherever it fits: in-CG SpMV 200^3
+    // 155 vs 407 us (SELL-512-C LDS), 100^3 32 vs 58 us, 7-pt 256^3 187 vs
+    // 284 us. Non-temporal code loads above ~100 MB of codes.
+    if (M->has_v) return (double)M->nslots4 > 100e6 ? 7201 : 7301;
     if (lds) return M->has_c_lds ? 4200 : (big ? 2200 : 2300);
     if (M->has_c) return big ? 3000 : 3100;
     return big ? 1000 : 0;
 }
 
+// SELL-512-V kernels: 5xxx (LDS), 6xxx (plain), 7xxx (plain, 4-slot chunks).
+bool variant_is_v(int v) { return v >= 5000 && v < 8000; }
+
 // Matrix-stream bytes per stored slot of the kernel in use.
 double slot_bytes(const hpccg_hip_matrix* M)
 {
     const int v = M->spmv_variant;
+    if (v >= 7000 && v < 8000) return (double)M->nslots4 / std::max<long long>(1, M->nslots);
+    if (variant_is_v(v)) return 1.0;
     if ((v >= 3000 && v < 5000)) return 9.0;
     if (v >= 2000 && v < 3000) return 10.0;
     return 12.0;
@@ -650,7 +709,7 @@ bool fuse_p_effective(const hpccg_hip_matrix* M)
 {
     if (M->spmv_variant == 9999) return false;
     const int v = M->spmv_variant;
-    const bool lds = (v >= 2000 && v < 3000) || (v >= 4000 && v < 5000);
+    const bool lds = (v >= 2000 && v < 3000) || (v >= 4000 && v < 6000);
     if (M->nranks != 1 && !lds) return false;
     if (M->fuse_p < 0) return lds;
     return M->fuse_p != 0;
@@ -727,9 +786,14 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.cols = M->d_cols;
     a.vals = M->d_vals;
     a.lcols = M->d_lcols;
-    a.ccodes = M->d_ccodes;
-    a.cdict = M->d_cdict;
-    a.ldsc = M->d_ldsc;
+    const bool v = variant_is_v(M->spmv_variant);
+    a.ccodes = v ? M->d_vcodes : M->d_ccodes;
+    a.cdict = v ? M->d_vdict : M->d_cdict;
+    a.ldsc = v ? M->d_vldsc : M->d_ldsc;
+    a.cval = v ? M->d_vval : nullptr;
+    a.ccount = v ? M->d_vcount : M->d_ccount;
+    a.vbase4 = M->d_vbase4;
+    a.vcodes4 = M->d_vcodes4;
     a.win_ptr = M->d_win_ptr;
     a.win_start = M->d_win_start;
     a.win_len = M->d_win_len;
@@ -2017,12 +2081,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
             return set_err(HPCCG_HIP_EINVAL, "unknown spmv variant %lld", value);
         if ((w == 27 || w == 7) && !(M->uniform && M->width == w))
             return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform width-%d SELL image", v, w);
-        if (v >= 2000 && v < 3000 && !M->has_lds)
-            return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-L windows (not built)", v);
-        if (v >= 3000 && v < 4000 && !M->has_c)
-            return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-C image (not built)", v);
-        if (v >= 4000 && v < 5000 && !M->has_c_lds)
-            return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-C LDS image (not built)", v);
+        if (const char* why = variant_unavailable(M, v))
+            return set_err(HPCCG_HIP_EINVAL, "variant %d needs %s (not built)", v, why);
         M->spmv_variant = v;
     } else {
         return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
@@ -2072,17 +2132,16 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_
     if (!M || !avg_us || reps < 1) return set_err(HPCCG_HIP_EINVAL, "bad argument");
     const int w = variant % 100;
     if (!spmv_variant_ok(variant)) return set_err(HPCCG_HIP_EINVAL, "unknown variant %d", variant);
-    if (variant >= 2000 && variant < 3000 && !M->has_lds)
-        return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-L windows", variant);
-    if (variant >= 3000 && variant < 4000 && !M->has_c)
-        return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-C image", variant);
-    if (variant >= 4000 && variant < 5000 && !M->has_c_lds)
-        return set_err(HPCCG_HIP_EINVAL, "variant %d needs the SELL-512-C LDS image", variant);
+    if (const char* why = variant_unavailable(M, variant))
+        return set_err(HPCCG_HIP_EINVAL, "variant %d needs %s", variant, why);
     if ((w == 27 || w == 7 || variant == 9999) && !(M->uniform && M->width == (variant == 9999 ? 27 : w)))
         return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform SELL image of that width", variant);
     HIP_TRY(hipSetDevice(M->device));
     TRY(ensure_hist(M, 2));
+    const int keep = M->spmv_variant;
+    M->spmv_variant = variant;  // make_args picks that variant's image
     CgArgs a = make_args(M, M->d_b, M->d_x, 2, 0.0);
+    M->spmv_variant = keep;
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));

@@ -52,14 +52,15 @@ def test_group_matches_global_reference(hp, gpu, golden, name):
 
 def test_group_kernel_variants_bitwise(hp, gpu):
     """Multi-rank SpMV kernels (plain SELL-512, NT, LDS-staged windows that
-    include the ghost planes, 1-byte offset codes), the p update fused into the
-    LDS SpMV (halo rows by k_p_boundary first), the halo overlapped with the
+    include the ghost planes, 1-byte offset codes, 1-byte (offset, value)
+    codes), the p update fused into the LDS SpMV (halo rows by k_p_boundary
+    first), the halo overlapped with the
     interior slices, the dot completion modes and the deferred x update give
     the same bits."""
     Ms = hp.group_generate(24, 20, 9, 3)
     ref = None
     import itertools
-    for v, fold, fuse, defer, ovl in itertools.product((1000, 0, 2000, 2100, 4200), (0, 1, 2), (0, 1), (0, 1),
+    for v, fold, fuse, defer, ovl in itertools.product((1000, 0, 2000, 2100, 4200, 5200, 7201), (0, 1, 2), (0, 1), (0, 1),
                                                       (0, 1)):
         for M in Ms:
             M.set_option("spmv_variant", v)
@@ -70,7 +71,8 @@ def test_group_kernel_variants_bitwise(hp, gpu):
         if v >= 2000 and fuse:
             assert Ms[1].get_option("overlap") == ovl
         # p = r + beta p inside the SpMV: LDS kernels only on multiple ranks
-        assert Ms[1].get_option("fuse_p") == (fuse if v >= 2000 else 0)
+        lds = 2000 <= v < 3000 or 4000 <= v < 6000
+        assert Ms[1].get_option("fuse_p") == (fuse if lds else 0)
         niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
         got = (niters, normr, Ms[0].last_trace().tobytes(), b"".join(x.tobytes() for x in xs))
         if ref is None:

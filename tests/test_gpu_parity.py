@@ -54,7 +54,9 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 1000, 1001, 1002, 1027, 2000, 2001,
                                      2002, 2100, 2200, 2208, 2300, 2308, 3000, 3001, 3002, 3100,
-                                     4000, 4200, 4300, 3027])
+                                     4000, 4200, 4300, 3027, 5000, 5100, 5200, 5208, 5300, 5308,
+                                     5401, 5404, 5204, 6000, 6100, 6104, 6001, 7001, 7101, 7002,
+                                     7102, 7027, 7127, 7201, 7202, 7301, 7302, 7204])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
@@ -69,7 +71,7 @@ def test_sparsemv_variants_agree(hp, gpu, variant):
     x0 = prob.x
     _, it0, nr0, _ = hp.HPCCG(M, prob.b, x0, max_iter=60)
     assert it == it0
-    if variant in (1, 2, 1001, 1002, 2001, 2002, 3001, 3002):
+    if variant in (1, 2, 1001, 1002, 2001, 2002, 3001, 3002, 5401, 5404, 5204, 6104, 6001):
         assert check_trace(tr, M.last_trace(), RTRANS_RTOL_1GPU) > 10
     else:
         assert nr == nr0
@@ -107,7 +109,8 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # and the LDS kernels (same rows per thread), fused or not, give the same bits
-    for v, fuse in itertools.product((2000, 2100, 2200, 2308, 3000, 3100, 4200, 4300), (0, 1)):
+    for v, fuse in itertools.product((2000, 2100, 2200, 2308, 3000, 3100, 4200, 4300, 5200, 5300, 6000, 6100,
+                                      7001, 7102), (0, 1)):
         M.set_option("spmv_variant", v)
         M.set_option("fuse_p", fuse)
         M.set_option("redund", 1 - fuse)
@@ -432,6 +435,8 @@ def test_sell_c_fallback_for_many_offsets(hp, gpu):
     assert M.get_option("spmv_variant") < 3000  # no SELL-512-C for this image
     with pytest.raises(hp.HPCCGError, match="SELL-512-C"):
         M.set_option("spmv_variant", 3000)
+    with pytest.raises(hp.HPCCGError, match="SELL-512-V"):
+        M.set_option("spmv_variant", 6000)
     b = 1.0 + (np.arange(n) % 5)
     x = np.zeros(n)
     _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=30)
@@ -466,3 +471,62 @@ def test_tiny_and_thin_grids(hp, gpu, dims, s7):
             # 3x2x1: whether rtrans and p.Ap both underflow to 0 (-> NaN) in
             # the noise regime depends on the summation order
             assert np.max(np.abs(x - prob.xexact)) <= 1e-12
+
+
+def _banded(n, vals_of):
+    """Symmetric 5-band matrix with the given off-diagonal value per (i, j)."""
+    rp = [0]
+    cols, vals = [], []
+    for i in range(n):
+        row = [(i, 0.0)]
+        for j in (i - 7, i - 1, i + 1, i + 7):
+            if 0 <= j < n:
+                row.append((j, vals_of(min(i, j), max(i, j))))
+        row[0] = (i, 4.5 + 2.0 * sum(abs(v) for _, v in row[1:]))  # well conditioned
+        cols += [c for c, _ in row]
+        vals += [v for _, v in row]
+        rp.append(len(cols))
+    return np.array(rp, np.int64), np.array(cols, np.int32), np.array(vals, np.float64)
+
+
+def _solve_all(hp, M, b, variants, max_iter=40):
+    out = {}
+    for v in variants:
+        M.set_option("spmv_variant", v)
+        x = np.zeros(len(b))
+        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=max_iter)
+        out[v] = (it, nr, M.last_trace().tobytes(), x.tobytes())
+    return out
+
+
+def test_sell_v_value_dictionary_edges(hp, gpu):
+    """SELL-512-V codes (offset, value) pairs: keys are the value's bits, so a
+    stored -0.0 and +0.0 are different entries, and tiny/huge magnitudes keep
+    their exact bits. Same solve bits as the SELL-512 kernels."""
+    n = 3000
+    pick = [-1.0, -0.0, 0.0, -1e-300, -3.0e5, -2.0 ** -1074, -0.25]
+    rp, cols, vals = _banded(n, lambda i, j: pick[(i * 3 + j) % len(pick)])
+    M = hp.Matrix.from_csr(rp, cols, vals)
+    assert M.get_option("spmv_variant") >= 5000  # fits: few distinct values per slice
+    b = 1.0 + (np.arange(n) % 7)
+    out = _solve_all(hp, M, b, (1000, 3000, 6000, 6100, 7001, 7102))
+    assert all(o == out[1000] for o in out.values())
+    A = oracle.CSR(rp, cols, vals, np.zeros(n), b, np.zeros(n))
+    ref = oracle.hpccg(A, max_iter=40)
+    assert check_trace(np.frombuffer(out[6000][2]), ref["trace"], RTRANS_RTOL_1GPU) >= 5
+
+
+def test_sell_v_fallback_for_many_values(hp, gpu):
+    """Few offsets but a different value on every row: SELL-512-C fits, the
+    (offset, value) dictionary of SELL-512-V does not (> 255 pairs per
+    slice), and the library keeps the C kernels."""
+    n = 4096
+    rp, cols, vals = _banded(n, lambda i, j: -1.0 - ((i * 131 + j) % 1000) / 1000.0)
+    M = hp.Matrix.from_csr(rp, cols, vals)
+    assert 3000 <= M.get_option("spmv_variant") < 5000
+    for v in (5200, 6000):
+        with pytest.raises(hp.HPCCGError, match="SELL-512-V"):
+            M.set_option("spmv_variant", v)
+    b = 1.0 + (np.arange(n) % 5)
+    out = _solve_all(hp, M, b, (1000, 3000, 3100))
+    assert all(o == out[1000] for o in out.values())
