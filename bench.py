@@ -97,6 +97,22 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=15.0):
                       f"OpenMP {threads} threads on the GPU box host"}
 
 
+def matrix_format(v):
+    """Matrix image a SpMV variant streams (hpccg_solver.cpp slot_bytes) and
+    its bytes per stored slot."""
+    if v >= 7000:
+        return "SELL-512-V4 (1-byte (offset, value) codes, 4-slot chunks)", 1.0
+    if v >= 5000:
+        return "SELL-512-V (1-byte (offset, value) codes)", 1.0
+    if v >= 4000:
+        return "SELL-512-C + LDS x windows (8 B value + 1-byte offset code)", 9.0
+    if v >= 3000:
+        return "SELL-512-C (8 B value + 1-byte offset code)", 9.0
+    if v >= 2000:
+        return "SELL-512-L (8 B value + 16-bit window index)", 10.0
+    return "SELL-512 (8 B value + int32 column)", 12.0
+
+
 def pmc_traffic(tag, fused_p):
     """HBM bytes per SpMV launch from the committed rocprofv3 PMC summary of
     the same kernel configuration (profiles/pmc_<tag>.json), else None."""
@@ -130,6 +146,10 @@ def main():
                     help="MB of the matrix image streamed with default-policy loads (-1 default)")
     ap.add_argument("--rev-update", type=int, default=-1,
                     help="update kernel walks slices backwards (-1 default)")
+    ap.add_argument("--value-codes", type=int, default=0,
+                    help="1: headline with SELL-512-V (values from a per-slice dictionary); default 0 "
+                         "streams every stored value and reports SELL-512-V as a secondary figure")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the SELL-512-V secondary run")
     ap.add_argument("--event-steps", type=int, default=1,
                     help="timed steps launched eagerly with hipEvents around every SpMV (the "
                          "roofline's kernel time); the other timed steps replay hipGraphs")
@@ -173,6 +193,8 @@ def main():
         M.set_option("rev_update", args.rev_update)
     if args.resident_mb >= 0:
         M.set_option("resident_mb", args.resident_mb)
+    if args.value_codes:
+        M.set_option("value_codes", 1)
     b, x0, _ = M.vectors()
     nrow = n * n * n
     x = torch.zeros(nrow, dtype=torch.float64, device=f"cuda:{local_rank}")
@@ -251,6 +273,41 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     iter_bytes = 12.0 * info["nnz"] + 116.0 * nrow  # unfused reference sequence, SURVEY 8(d)
 
+    # Secondary figure (not `value`): the same solves with SELL-512-V, whose
+    # per-slice (offset, value) dictionary replaces the streamed values.
+    secondary = None
+    if not args.value_codes and not args.no_secondary and M.get_option("value_codes_available"):
+        keep_variant = M.get_option("spmv_variant")
+        M.set_option("value_codes", 1)
+        step(False)  # warm-up: graph build for the new kernel
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        it2 = 0
+        for i in range(args.steps):
+            it2 += step(i < args.event_steps)[1]
+            if i < args.event_steps:
+                kt2 = M.kernel_times()
+        torch.cuda.synchronize()
+        barrier()
+        el2 = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el2], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = t.item()
+        xerr2 = (x - 1.0).abs().max().item()
+        secondary = {
+            "format": "SELL-512-V (1-byte codes of per-slice (column - row, value) pairs; lossless, "
+                      "bitwise-equal results; not the headline: it does not stream the stored values)",
+            "value": round(it2 / el2 * world, 3),
+            "spmv_variant": M.get_option("spmv_variant"),
+            "spmv_avg_us": round(kt2["spmv_ms"] / max(1, kt2["spmv_launches"]) * 1e3, 2)
+            if args.event_steps > 0 else None,
+            "x_minus_xexact_inf": xerr2,
+        }
+        M.set_option("value_codes", 0)
+        M.set_option("spmv_variant", keep_variant)
+
     if rank == 0:
         out = {
             "metric": "CG iterations/sec + effective SpMV GB/s (% HBM peak), 27-pt nx=ny=nz=200",
@@ -272,8 +329,10 @@ def main():
                 "max_iter": args.max_iter, "parallelism": f"z-slab x{world} (RCCL)",
                 "nnz_per_gpu": info["nnz"], "sell_slots_per_gpu": info["slots"],
                 "spmv_variant": M.get_option("spmv_variant"),
+                "matrix_format": matrix_format(M.get_option("spmv_variant"))[0],
+                "matrix_bytes_per_slot": matrix_format(M.get_option("spmv_variant"))[1],
                 "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "x_defer", "rev_update",
-                                                         "resident_mb", "overlap")},
+                                                         "resident_mb", "overlap", "value_codes")},
             },
             "cg_iterations_per_s_global": round(it_per_s, 3),
             "spmv_effective_gbs": round(achieved, 1),
@@ -292,6 +351,7 @@ def main():
                 "avg_launch_us": round(spmv_avg_s * 1e6, 2),
                 "timing": timing_src,
             },
+            "value_coded_secondary": secondary,
             "update_kernel_avg_us": round(upd_ms / upd_n * 1e3, 2) if upd_n else None,
             "check": {"x_minus_xexact_inf": chk[0].item(), "final_normr_over_initial": chk[1].item(),
                       "niters_per_solve": it},

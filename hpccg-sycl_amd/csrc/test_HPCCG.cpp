@@ -130,6 +130,7 @@ int main(int argc, char* argv[])
             die("generate_matrix");
         if (hpccg_hip_matrix_create(A, &M)) die("matrix upload");
     }
+    if (env_int("HPCCG_VALUE_CODES", 0) && hpccg_hip_set_option(M, "value_codes", 1)) die("value_codes");
     times[6] = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
 
     int niters = 0;

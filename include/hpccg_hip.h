@@ -136,7 +136,12 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  * every 8 iterations, default), "rev_update" (1 = the update kernel walks each
  * XCD's slices backwards, default), "resident_mb" (non-temporal SpMV kernels:
  * this many MB of leading slices per XCD use default-policy loads so they can
- * stay in the Infinity Cache; -1 auto = 128 for images up to 400 MB, else 0).
+ * stay in the Infinity Cache; -1 auto = 128 for images up to 400 MB, else 0),
+ * "value_codes" (1 = choose a SELL-512-V kernel when every slice has at most
+ * 255 distinct (column - row, value) pairs: values come from a per-slice
+ * dictionary, ~1 B per stored entry instead of 9; default 0 = every stored
+ * value is streamed from HBM each iteration; get: 1 if a V kernel is in use;
+ * "value_codes_available" (get only) 1 if the V image was built).
  * None of them
  * changes a computed value: fuse_p/fold on and off are bitwise equal. */
 int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value);

@@ -507,6 +507,8 @@ def test_sell_v_value_dictionary_edges(hp, gpu):
     pick = [-1.0, -0.0, 0.0, -1e-300, -3.0e5, -2.0 ** -1074, -0.25]
     rp, cols, vals = _banded(n, lambda i, j: pick[(i * 3 + j) % len(pick)])
     M = hp.Matrix.from_csr(rp, cols, vals)
+    assert M.get_option("value_codes") == 0  # opt-in
+    M.set_option("value_codes", 1)
     assert M.get_option("spmv_variant") >= 5000  # fits: few distinct values per slice
     b = 1.0 + (np.arange(n) % 7)
     out = _solve_all(hp, M, b, (1000, 3000, 6000, 6100, 7001, 7102))
@@ -523,6 +525,8 @@ def test_sell_v_fallback_for_many_values(hp, gpu):
     n = 4096
     rp, cols, vals = _banded(n, lambda i, j: -1.0 - ((i * 131 + j) % 1000) / 1000.0)
     M = hp.Matrix.from_csr(rp, cols, vals)
+    assert M.get_option("value_codes_available") == 0
+    M.set_option("value_codes", 1)
     assert 3000 <= M.get_option("spmv_variant") < 5000
     for v in (5200, 6000):
         with pytest.raises(hp.HPCCGError, match="SELL-512-V"):
@@ -530,3 +534,23 @@ def test_sell_v_fallback_for_many_values(hp, gpu):
     b = 1.0 + (np.arange(n) % 5)
     out = _solve_all(hp, M, b, (1000, 3000, 3100))
     assert all(o == out[1000] for o in out.values())
+
+
+@pytest.mark.parametrize("dims,s7", [((40, 36, 44), False), ((64, 64, 64), True)])
+def test_value_codes_opt_in_bitwise(hp, gpu, dims, s7):
+    """value_codes is off by default (the stored values stream from HBM); on,
+    the generated stencil picks a SELL-512-V kernel and the solve gives the
+    same bits as the default kernel."""
+    M = hp.Matrix.generate(*dims, use_7pt=s7)
+    assert M.get_option("value_codes") == 0 and M.get_option("spmv_variant") < 5000
+    assert M.get_option("value_codes_available") == 1
+    b, _, _ = M.vectors()
+    import torch
+    outs = []
+    for vc in (0, 1, 0):
+        M.set_option("value_codes", vc)
+        assert M.get_option("value_codes") == vc
+        x = torch.zeros(dims[0] * dims[1] * dims[2], dtype=torch.float64, device=gpu)
+        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=80, device=True)
+        outs.append((it, nr, M.last_trace().tobytes(), host(x).tobytes()))
+    assert outs[0] == outs[1] == outs[2]
