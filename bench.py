@@ -100,6 +100,8 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=15.0):
 def matrix_format(v):
     """Matrix image a SpMV variant streams (hpccg_solver.cpp slot_bytes) and
     its bytes per stored slot."""
+    if v >= 8000:
+        return "SELL-512-P (8 B value per slot + 1-byte row-pattern id per row)", 8.0
     if v >= 7000:
         return "SELL-512-V4 (1-byte (offset, value) codes, 4-slot chunks)", 1.0
     if v >= 5000:
@@ -345,7 +347,9 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(f"spmv_{args.stencil}pt_{n}", fused_p),
-                "kernel": "k_spmv (SELL-512 SpMV + p.Ap%s)" % (" + p = r + beta p" if fused_p else ""),
+                "kernel": "SpMV variant %d, %s + p.Ap%s" % (M.get_option("spmv_variant"),
+                                                           matrix_format(M.get_option("spmv_variant"))[0],
+                                                           " + p = r + beta p" if fused_p else ""),
                 "bytes_formula": "12 nnz + 20 n (SpMV) + 16 n (ddot p.Ap)" + (" + 24 n (waxpby p)" if fused_p else ""),
                 "bytes_per_launch": spmv_bytes,
                 "avg_launch_us": round(spmv_avg_s * 1e6, 2),

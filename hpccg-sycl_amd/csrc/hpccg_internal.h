@@ -78,6 +78,12 @@ struct CgArgs {
     const int* ccount;            // SELL-512-C / -V: per slice, codes in use (dictionary entries to load)
     const unsigned int* vbase4;   // SELL-512-V4: [nslices + 1] first chunk of each slice (4 slots x 512 rows)
     const unsigned char* vcodes4; // SELL-512-V4: the V codes, a row's 4 codes of a chunk contiguous
+    const unsigned char* prow;    // SELL-512-P: per row, its pattern id within the slice
+    const int* pcount;            // SELL-512-P: per slice, patterns
+    const int* pbase;             // SELL-512-P: per slice, first entry of its pattern table
+    const int* ptab_g;            // SELL-512-P: pattern tables, column - row per slot (kPatPad = padding)
+    const int* ptab_l;            // SELL-512-P: pattern tables, LDS position - lane per slot
+    int pat_max;                  // SELL-512-P: largest table (ints) over slices: dynamic LDS
     const int* win_ptr;    // [nslices + 1] into the window arrays
     const int* win_start;  // first local column of the window
     const int* win_len;    // entries
@@ -141,6 +147,18 @@ void launch_build_c(const unsigned int* slice_base, int nslices, const int* cols
                     const int* win_ptr, const int* win_start, const int* win_off, const int* win_len,
                     unsigned char* codes, int* cdict, double* cval, int* ldsc, int* ccount, int* ok,
                     hipStream_t s);
+// SELL-512-P (per-row pattern ids over the SELL-512-C codes): pass 1 writes
+// prow, prep[s * kMaxPat + id] (representative lane), pcount; ok[0] = 0 when a
+// slice does not fit. Pass 2 writes the tables at pbase (host prefix sum of
+// pcount * width): tab_g from cdict, tab_l from ldsc (may be null).
+constexpr int kMaxPat = 256;
+constexpr int kPatCap = 2048;          // table entries per slice at most (LDS ints)
+constexpr int kPatPad = -2147483647 - 1;  // padding slot
+void launch_build_p(const unsigned int* slice_base, int nslices, const unsigned char* codes, unsigned char* prow,
+                    int* prep, int* pcount, int* ok, hipStream_t s);
+void launch_fill_p(const unsigned int* slice_base, int nslices, const unsigned char* codes, const int* prep,
+                   const int* pcount, const int* pbase, const int* cdict, const int* ldsc, int* tab_g, int* tab_l,
+                   hipStream_t s);
 // SELL-512-V4 regrouping of the V codes (vbase4 in chunks of 4 slots).
 void launch_interleave_v4(const unsigned int* slice_base, const unsigned int* vbase4, int nslices,
                           const unsigned char* codes, unsigned char* out, hipStream_t s);

@@ -1022,6 +1022,98 @@ __global__ __launch_bounds__(256) void k_build_c(const unsigned int* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------
+// SELL-512-P: per-row pattern ids over the SELL-512-C codes. Rows of a slice
+// whose code sequences (slot 0..w-1) are equal share one pattern; a stencil
+// slice has a handful (interior, x/y/z faces, edges). The SpMV streams the
+// values (8 B per slot) and one byte per row; the offsets come from a
+// per-slice table in LDS. Pass 1 (one block of 512 lanes per slice): hash
+// each lane's code sequence, one representative lane per pattern (the lowest),
+// ids in representative order, every lane verified against its
+// representative. ok[0] = 0 when a slice has more than kMaxPat patterns, a
+// table over kPatCap entries, or a hash collision.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kSliceRows) void k_build_p(const unsigned int* __restrict__ slice_base, int nslices,
+                                                        const unsigned char* __restrict__ codes,
+                                                        unsigned char* __restrict__ prow, int* __restrict__ prep,
+                                                        int* __restrict__ pcount, int* ok)
+{
+    typedef unsigned long long u64;
+    constexpr int kH = 1024;
+    constexpr u64 kEmpty = ~0ull;
+    __shared__ u64 keys[kH];
+    __shared__ int rep[kH];
+    __shared__ short rid[kSliceRows];  // pattern id of a representative lane, else -1
+    __shared__ int cnt;
+    const int s = blockIdx.x;
+    if (s >= nslices) return;
+    for (int h = threadIdx.x; h < kH; h += kSliceRows) {
+        keys[h] = kEmpty;
+        rep[h] = INT_MAX;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x;
+    const size_t e0 = (size_t)slice_base[s] * kSliceRows;
+    const int w = (int)(slice_base[s + 1] - slice_base[s]);
+    u64 hsh = 0xcbf29ce484222325ull ^ (u64)w;
+    for (int j = 0; j < w; j++) {
+        hsh = (hsh ^ codes[e0 + (size_t)j * kSliceRows + lane]) * 0x100000001b3ull;
+        hsh ^= hsh >> 31;
+    }
+    if (hsh == kEmpty) hsh = 0;
+    int h = (int)((hsh * 0x9E3779B97F4A7C15ull) >> 54);
+    for (int probe = 0; probe < kH; probe++) {
+        const u64 old = atomicCAS(&keys[h], kEmpty, hsh);
+        if (old == kEmpty || old == hsh) break;
+        h = (h + 1) & (kH - 1);
+    }
+    atomicMin(&rep[h], lane);
+    __syncthreads();
+    rid[lane] = rep[h] == lane ? 1 : -1;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // ids in lane order of the representatives
+        int n = 0;
+        for (int l = 0; l < kSliceRows; l++)
+            if (rid[l] > 0) {
+                if (n < kMaxPat) prep[(size_t)s * kMaxPat + n] = l;
+                rid[l] = (short)n++;
+            }
+        cnt = n;
+        pcount[s] = n;
+        if (n > kMaxPat || n * w > kPatCap) ok[0] = 0;
+    }
+    __syncthreads();
+    if (cnt > kMaxPat || cnt * w > kPatCap) return;
+    const int r = rep[h];
+    for (int j = 0; j < w; j++)
+        if (codes[e0 + (size_t)j * kSliceRows + lane] != codes[e0 + (size_t)j * kSliceRows + r]) ok[0] = 0;
+    prow[(size_t)s * kSliceRows + lane] = (unsigned char)rid[r];
+}
+
+// Pass 2: the pattern tables, slice s at pbase[s]: entry (id, j) = the
+// offset of slot j of pattern id -- column - row (tab_g, gathering kernels)
+// or the LDS position relative to the row's lane (tab_l) -- or kPatPad.
+__global__ __launch_bounds__(256) void k_fill_p(const unsigned int* __restrict__ slice_base, int nslices,
+                                                const unsigned char* __restrict__ codes,
+                                                const int* __restrict__ prep, const int* __restrict__ pcount,
+                                                const int* __restrict__ pbase, const int* __restrict__ cdict,
+                                                const int* __restrict__ ldsc, int* __restrict__ tab_g,
+                                                int* __restrict__ tab_l)
+{
+    const int s = blockIdx.x;
+    if (s >= nslices) return;
+    const size_t e0 = (size_t)slice_base[s] * kSliceRows;
+    const int w = (int)(slice_base[s + 1] - slice_base[s]);
+    const int n = pcount[s] * w;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int id = i / w, j = i % w;
+        const unsigned c = codes[e0 + (size_t)j * kSliceRows + prep[(size_t)s * kMaxPat + id]];
+        const size_t o = (size_t)pbase[s] + i;
+        tab_g[o] = c == kCodePad ? kPatPad : cdict[(size_t)s * kCodes + c];
+        if (tab_l) tab_l[o] = c == kCodePad ? kPatPad : ldsc[(size_t)s * kCodes + c];
+    }
+}
+
 template <int kRpt, int kW, int kMinW, bool kNT, bool kFuse>
 __global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, bool prologue)
 {
@@ -1223,7 +1315,9 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
         lds_prefetch<kRpt, false, kCode, kVal, kPre>(vp, cp, wdt, vpre, cpre);
     if constexpr (kCode)
     {
-        const int nc = a.ccount[s];  // codes in use; kCodePad has value 0
+        // C: the whole dictionary (no dependent count load ahead of the staging);
+        // V: the codes in use, kCodePad has value 0
+        const int nc = kVal ? a.ccount[s] : kCodes;
         for (int i = threadIdx.x; i < nc; i += kSliceRows / kRpt) {
             sldsc[i] = a.ldsc[(size_t)s * kCodes + i];
             if constexpr (kVal) sval[i] = a.cval[(size_t)s * kCodes + i];
@@ -1288,6 +1382,237 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lds(CgArgs a, bool p
     } else {
         pv = ld<kRpt>(p + row);
     }
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += pv.v[i] * o.v[i];
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
+}
+
+// ---------------------------------------------------------------------------
+// SELL-512-P SpMV kernels: values streamed as in SELL-512 (8 B per slot), one
+// pattern-id byte per row, the slice's pattern table (kPatCap ints) in LDS.
+// k_spmv_lp reads x from the staged windows (the SELL-512-L staging, p update
+// fused as in k_spmv_lds); k_spmv_pp gathers x from global memory. Same
+// products in the same slot order as SELL-512, same p.Ap tree per kRpt.
+// ---------------------------------------------------------------------------
+template <int kRpt>
+__device__ __forceinline__ void ld_pids(const unsigned char* __restrict__ p, int (&pid)[kRpt])
+{
+    if constexpr (kRpt == 1) {
+        pid[0] = p[0];
+    } else {
+        static_assert(kRpt == 2, "1 or 2 rows per thread");
+        const unsigned t = *reinterpret_cast<const unsigned short*>(p);
+        pid[0] = t & 0xFFu;
+        pid[1] = t >> 8;
+    }
+}
+
+template <int kRpt, bool kNT, int kU>
+__device__ __forceinline__ void lp_stream(const double* __restrict__ vp, int j0, int wdt, const int (&pr)[kRpt],
+                                          const double* xs, const int* spat, double (&sum)[kRpt])
+{
+    const int lrow = threadIdx.x * kRpt;
+#pragma unroll kU
+    for (int j = j0; j < wdt; j++) {
+        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            const int c = spat[pr[i] + j];
+            const double xv = c != kPatPad ? xs[lrow + i + c] : 0.0;
+            sum[i] = sum[i] + v.v[i] * xv;
+        }
+    }
+}
+
+// Dynamic LDS: the windows (a.lds_doubles doubles), then the pattern table
+// (a.pat_max ints, the largest over slices).
+template <int kRpt, bool kNT, bool kFuse, int kPre, int kU = 3>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lp(CgArgs a, bool prologue)
+{
+    extern __shared__ __attribute__((aligned(16))) double xs[];
+    int* const spat = reinterpret_cast<int*>(xs + a.lds_doubles);
+    int k = 0;
+    double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
+    if (!prologue) {
+        k = a.kst[0];
+        if (kFuse) rr = cur_rr(a);
+        const bool run = cg_run(a, k, kFuse, rr);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = rr;
+            if (run)
+                stamp(a, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = spmv_slice(a);
+    if (s < 0) return;
+    double* __restrict__ p = cur_p(a, k);
+    const double* __restrict__ xext = p - a.ghost_lo;
+    const size_t base = (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
+    const int wdt = (int)(a.slice_base[s + 1] - a.slice_base[s]);
+    const double* __restrict__ vp = a.vals + base;
+    const bool nt = kNT && (xcd_slice(a.sgrid) % (a.sgrid / kNumXcd)) >= a.nt_split;
+    int pid[kRpt];
+    ld_pids<kRpt>(a.prow + (size_t)s * kSliceRows + threadIdx.x * kRpt, pid);
+    constexpr int kP = kPre > 0 ? kPre : 1;
+    Rows<kRpt> vpre[kP];
+#pragma unroll
+    for (int j = 0; j < kPre; j++)
+        if (j < wdt) vpre[j] = nt ? ld_m<kRpt, true>(vp + (size_t)j * kSliceRows) : ld_m<kRpt, false>(vp + (size_t)j * kSliceRows);
+    {
+        const int np = a.pcount[s] * wdt;
+        const int* __restrict__ tab = a.ptab_l + a.pbase[s];
+        for (int i = threadIdx.x; i < np; i += kSliceRows / kRpt) spat[i] = tab[i];
+    }
+    double beta = 0.0;
+    const double* __restrict__ pold = a.r;
+    if constexpr (kFuse) {
+        beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
+        pold = (k == 1) ? a.r : cur_p(a, k - 1);
+    }
+    const int w0 = a.win_ptr[s], w1 = a.win_ptr[s + 1];
+    for (int w = w0; w < w1; w++) {
+        const int st0 = a.win_start[w], len = a.win_len[w], off = a.win_off[w];
+        for (int i = threadIdx.x; i < len; i += kSliceRows / kRpt) {
+            if constexpr (kFuse) {
+                const int l = st0 + i - a.ghost_lo;
+                xs[off + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + beta * pold[l] : xext[st0 + i];
+            } else {
+                xs[off + i] = xext[st0 + i];
+            }
+        }
+    }
+    __syncthreads();
+    int pr[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) pr[i] = pid[i] * wdt;
+    double sum[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+    const int lrow = threadIdx.x * kRpt;
+#pragma unroll
+    for (int j = 0; j < kPre; j++) {
+        if (j < wdt) {
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) {
+                const int c = spat[pr[i] + j];
+                const double xv = c != kPatPad ? xs[lrow + i + c] : 0.0;
+                sum[i] = sum[i] + vpre[j].v[i] * xv;
+            }
+        }
+    }
+    if (nt)
+        lp_stream<kRpt, true, kU>(vp, kPre, wdt, pr, xs, spat, sum);
+    else
+        lp_stream<kRpt, false, kU>(vp, kPre, wdt, pr, xs, spat, sum);
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    Rows<kRpt> o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+    st_rows<kRpt>(a.Ap, row, a.n, o);
+    if (prologue) return;
+    Rows<kRpt> pv;
+    if constexpr (kFuse) {
+        const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+        const Rows<kRpt> yv = ld<kRpt>(pold + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + beta * yv.v[i];
+        st_rows<kRpt>(p, row, a.n, pv);
+    } else {
+        pv = ld<kRpt>(p + row);
+    }
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += pv.v[i] * o.v[i];
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
+}
+
+// Dynamic LDS: the pattern table (a.pat_max ints). kW > 0: uniform width,
+// slot loop fully unrolled.
+template <int kRpt, bool kNT, bool kFuse, int kW = 0>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_pp(CgArgs a, bool prologue)
+{
+    extern __shared__ int spat[];
+    int k = 0;
+    double rr = 0.0;
+    if (!prologue) {
+        k = a.kst[0];
+        if (kFuse) rr = cur_rr(a);
+        const bool run = cg_run(a, k, kFuse, rr);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = rr;
+            if (run)
+                stamp(a, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = spmv_slice(a);
+    if (s < 0) return;
+    const int wdt = kW > 0 ? kW : (int)(a.slice_base[s + 1] - a.slice_base[s]);
+    int pid[kRpt];
+    ld_pids<kRpt>(a.prow + (size_t)s * kSliceRows + threadIdx.x * kRpt, pid);
+    {
+        const int np = a.pcount[s] * wdt;
+        const int* __restrict__ tab = a.ptab_g + a.pbase[s];
+        for (int i = threadIdx.x; i < np; i += kSliceRows / kRpt) spat[i] = tab[i];
+    }
+    __syncthreads();
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    double* __restrict__ p = cur_p(a, k);
+    const size_t base = (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
+    const double* __restrict__ vp = a.vals + base;
+    double beta = 0.0;
+    const double* pold = a.r;
+    if constexpr (kFuse) {
+        beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
+        pold = (k == 1) ? a.r : cur_p(a, k - 1);
+    }
+    const double* __restrict__ xext = p - a.ghost_lo;
+    int pr[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) pr[i] = pid[i] * wdt;
+    double sum[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+#pragma unroll(kW > 0 ? kW : 3)
+    for (int j = 0; j < wdt; j++) {
+        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            const int off = spat[pr[i] + j];
+            double xv = 0.0;
+            if (off != kPatPad) {
+                const int col = row + i + off;
+                if constexpr (kFuse) xv = a.r[col - a.ghost_lo] + beta * pold[col - a.ghost_lo];
+                else xv = xext[col];
+            }
+            sum[i] = sum[i] + v.v[i] * xv;
+        }
+    }
+    Rows<kRpt> pv;
+    if constexpr (kFuse) {
+        const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+        const Rows<kRpt> yv = ld<kRpt>(pold + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + beta * yv.v[i];
+        st_rows<kRpt>(p, row, a.n, pv);
+    } else {
+        pv = ld<kRpt>(p + row);
+    }
+    Rows<kRpt> o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+    st_rows<kRpt>(a.Ap, row, a.n, o);
+    if (prologue) return;
     double d = 0.0;
 #pragma unroll
     for (int i = 0; i < kRpt; i++)
@@ -1754,6 +2079,23 @@ void launch_interleave_v4(const unsigned int* slice_base, const unsigned int* vb
     hipLaunchKernelGGL(k_interleave_v4, dim3(nslices), dim3(256), 0, s, slice_base, vbase4, nslices, codes, out);
 }
 
+void launch_build_p(const unsigned int* slice_base, int nslices, const unsigned char* codes, unsigned char* prow,
+                    int* prep, int* pcount, int* ok, hipStream_t s)
+{
+    if (nslices <= 0) return;
+    hipLaunchKernelGGL(k_build_p, dim3(nslices), dim3(kSliceRows), 0, s, slice_base, nslices, codes, prow, prep,
+                       pcount, ok);
+}
+
+void launch_fill_p(const unsigned int* slice_base, int nslices, const unsigned char* codes, const int* prep,
+                   const int* pcount, const int* pbase, const int* cdict, const int* ldsc, int* tab_g, int* tab_l,
+                   hipStream_t s)
+{
+    if (nslices <= 0) return;
+    hipLaunchKernelGGL(k_fill_p, dim3(nslices), dim3(256), 0, s, slice_base, nslices, codes, prep, pcount, pbase,
+                       cdict, ldsc, tab_g, tab_l);
+}
+
 void launch_build_c(const unsigned int* slice_base, int nslices, const int* cols, const double* vals,
                     const int* win_ptr, const int* win_start, const int* win_off, const int* win_len,
                     unsigned char* codes, int* cdict, double* cval, int* ldsc, int* ccount, int* ok,
@@ -1787,6 +2129,15 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
 //   width, 2 rows/thread, nt -- within ~3 % of the matrix-streaming ceiling)
 //   2000 / 2001 / 2002 / 2100: SELL-512-L (x windows staged in LDS, 16-bit
 //   slice-local indices) with 2 / 1 / 4 rows per thread, nt; 2100 = 2 rows, no nt
+//   3xxx / 4xxx: SELL-512-C (1-byte offset codes), plain gather / LDS windows
+//   5xxx / 6xxx / 7xxx: SELL-512-V (codes of (offset, value) pairs; opt-in)
+//   8000 / 8200 / 8208 / 8300 / 8201: SELL-512-P with LDS windows (per-row
+//   pattern ids; prefetch 0 / 4 / 8 slots, 8300 no nt, 8201 1 row/thread);
+//   8216 / 8219 / 8226: prefetch 8 / 8 / 4, stream unrolled 6 / 9 / 6;
+//   8308 / 8316 / 8326: no nt, prefetch 8 / 8 / 4, unrolled 3 / 6 / 6
+//   8507 / 8527 / 8607: plain SELL-512-P, uniform width 7 / 27 / 7 fully
+//   unrolled (8607 no nt)
+//   8500 / 8501 / 8600: SELL-512-P, plain gather (2 rows nt, 1 row nt, 2 rows)
 //   9999: diagnostic matrix stream without the gather (not an SpMV)
 #define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
     do {                                                                                            \
@@ -1830,6 +2181,27 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
                                smem, s, a, prologue);                                              \
     } while (0)
 #define HPCCG_SPMV_LDS(RPT, NT, PRE) HPCCG_SPMV_LDSX(RPT, NT, PRE, 0)
+#define HPCCG_SPMV_LPU(RPT, NT, PRE, U)                                                            \
+    do {                                                                                           \
+        const size_t smem = (size_t)a.lds_doubles * sizeof(double) + (size_t)a.pat_max * sizeof(int); \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_lp<RPT, NT, true, PRE, U>), dim3(a.sgrid), dim3(kSliceRows / RPT), smem, \
+                               s, a, prologue);                                                    \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_lp<RPT, NT, false, PRE, U>), dim3(a.sgrid), dim3(kSliceRows / RPT), \
+                               smem, s, a, prologue);                                              \
+    } while (0)
+#define HPCCG_SPMV_LP(RPT, NT, PRE) HPCCG_SPMV_LPU(RPT, NT, PRE, 3)
+#define HPCCG_SPMV_PPW(RPT, NT, W)                                                                 \
+    do {                                                                                           \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_pp<RPT, NT, true, W>), dim3(a.sgrid), dim3(kSliceRows / RPT),         \
+                               (size_t)a.pat_max * sizeof(int), s, a, prologue);                   \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_pp<RPT, NT, false, W>), dim3(a.sgrid), dim3(kSliceRows / RPT),        \
+                               (size_t)a.pat_max * sizeof(int), s, a, prologue);                   \
+    } while (0)
+#define HPCCG_SPMV_PP(RPT, NT) HPCCG_SPMV_PPW(RPT, NT, 0)
 bool spmv_variant_ok(int v)
 {
     switch (v) {
@@ -1841,6 +2213,8 @@ bool spmv_variant_ok(int v)
     case 6000: case 6100: case 6104: case 6001:
     case 7001: case 7101: case 7002: case 7102: case 7027: case 7127: case 7007: case 7107:
     case 7201: case 7202: case 7301: case 7302: case 7204:
+    case 8000: case 8200: case 8208: case 8300: case 8201: case 8500: case 8501: case 8600:
+    case 8216: case 8219: case 8226: case 8308: case 8316: case 8326: case 8507: case 8527: case 8607:
         return true;
     default:
         return false;
@@ -1902,6 +2276,23 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 7301: HPCCG_SPMV_V4P(1, false, 0, 8); break;
     case 7302: HPCCG_SPMV_V4P(2, false, 0, 8); break;
     case 7204: HPCCG_SPMV_V4P(2, true, 0, 4); break;
+    case 8000: HPCCG_SPMV_LP(2, true, 0); break;
+    case 8200: HPCCG_SPMV_LP(2, true, 4); break;
+    case 8208: HPCCG_SPMV_LP(2, true, 8); break;
+    case 8300: HPCCG_SPMV_LP(2, false, 4); break;
+    case 8201: HPCCG_SPMV_LP(1, true, 4); break;
+    case 8216: HPCCG_SPMV_LPU(2, true, 8, 6); break;
+    case 8219: HPCCG_SPMV_LPU(2, true, 8, 9); break;
+    case 8226: HPCCG_SPMV_LPU(2, true, 4, 6); break;
+    case 8308: HPCCG_SPMV_LP(2, false, 8); break;
+    case 8316: HPCCG_SPMV_LPU(2, false, 8, 6); break;
+    case 8326: HPCCG_SPMV_LPU(2, false, 4, 6); break;
+    case 8507: HPCCG_SPMV_PPW(2, true, 7); break;
+    case 8527: HPCCG_SPMV_PPW(2, true, 27); break;
+    case 8607: HPCCG_SPMV_PPW(2, false, 7); break;
+    case 8500: HPCCG_SPMV_PP(2, true); break;
+    case 8501: HPCCG_SPMV_PP(1, true); break;
+    case 8600: HPCCG_SPMV_PP(2, false); break;
     case 3000: HPCCG_SPMV_C(2, true); break;
     case 3001: HPCCG_SPMV_C(1, true); break;
     case 3002: HPCCG_SPMV_C(4, true); break;
@@ -1920,6 +2311,10 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
 #undef HPCCG_SPMV_V
 #undef HPCCG_SPMV_V4
 #undef HPCCG_SPMV_V4P
+#undef HPCCG_SPMV_LP
+#undef HPCCG_SPMV_LPU
+#undef HPCCG_SPMV_PP
+#undef HPCCG_SPMV_PPW
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)
 {

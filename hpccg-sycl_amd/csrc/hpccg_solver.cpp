@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -229,6 +230,11 @@ struct hpccg_hip_matrix {
     int *d_cdict = nullptr, *d_ldsc = nullptr, *d_ccount = nullptr;
     // SELL-512-V (per-slice dictionary of (offset, value) pairs + 1-byte codes)
     int has_v = 0, has_v_lds = 0;
+    // SELL-512-P (per-row pattern ids over the C codes, pattern tables per slice)
+    int has_p = 0, has_p_lds = 0;
+    unsigned char* d_prow = nullptr;
+    int *d_prep = nullptr, *d_pcount = nullptr, *d_pbase = nullptr, *d_ptab_g = nullptr, *d_ptab_l = nullptr;
+    int pat_max = 0;  // largest pattern table over slices (ints)
     int value_codes = 0;  // opt-in: let choose_variant pick SELL-512-V
     unsigned char* d_vcodes = nullptr;
     int *d_vdict = nullptr, *d_vldsc = nullptr, *d_vcount = nullptr;
@@ -288,7 +294,8 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_gen_x0,     M->d_gen_xexact, M->d_lcols, M->d_win_ptr, M->d_win_start,
                     M->d_win_len,    M->d_win_off, M->d_send_idx, M->d_send_buf, M->d_ccodes, M->d_cdict, M->d_ldsc,
                     M->d_vcodes,     M->d_vdict,   M->d_vval,  M->d_vldsc, M->d_vbase4, M->d_vcodes4,
-                    M->d_ccount,     M->d_vcount};
+                    M->d_ccount,     M->d_vcount,  M->d_prow,  M->d_prep,  M->d_pcount, M->d_pbase,
+                    M->d_ptab_g,     M->d_ptab_l};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -569,10 +576,69 @@ int build_code_image(hpccg_hip_matrix* M, bool with_vals, unsigned char** codes,
     return 0;
 }
 
+// SELL-512-P from the SELL-512-C codes: pattern ids per row, tables per slice.
+int build_p_image(hpccg_hip_matrix* M)
+{
+    const int S = M->nslices;
+    if (!M->has_c || S < 1) return 0;
+    HIP_TRY(hipMalloc(&M->d_prow, (size_t)S * kSliceRows));
+    HIP_TRY(hipMalloc(&M->d_prep, sizeof(int) * (size_t)S * kMaxPat));
+    HIP_TRY(hipMalloc(&M->d_pcount, sizeof(int) * S));
+    int* d_ok = nullptr;
+    HIP_TRY(hipMalloc(&d_ok, sizeof(int)));
+    const int one = 1;
+    HIP_TRY(hipMemcpyAsync(d_ok, &one, sizeof one, hipMemcpyHostToDevice, M->stream));
+    launch_build_p(M->d_slice_base, S, M->d_ccodes, M->d_prow, M->d_prep, M->d_pcount, d_ok, M->stream);
+    HIP_TRY(hipGetLastError());
+    int ok = 0;
+    std::vector<int> cnt(S);
+    std::vector<unsigned int> sb(S + 1);
+    HIP_TRY(hipMemcpyAsync(&ok, d_ok, sizeof ok, hipMemcpyDeviceToHost, M->stream));
+    HIP_TRY(hipMemcpyAsync(cnt.data(), M->d_pcount, sizeof(int) * S, hipMemcpyDeviceToHost, M->stream));
+    HIP_TRY(hipMemcpyAsync(sb.data(), M->d_slice_base, sizeof(unsigned int) * sb.size(), hipMemcpyDeviceToHost,
+                           M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    (void)hipFree(d_ok);
+    std::vector<int> base(S + 1, 0);
+    M->pat_max = 0;
+    for (int i = 0; i < S && ok; i++) {
+        M->pat_max = std::max<int>(M->pat_max, cnt[i] * (int)(sb[i + 1] - sb[i]));
+        const long long e = (long long)base[i] + (long long)cnt[i] * (sb[i + 1] - sb[i]);
+        if (e > INT_MAX) ok = 0;
+        else base[i + 1] = (int)e;
+    }
+    if (ok) {
+        HIP_TRY(hipMalloc(&M->d_pbase, sizeof(int) * base.size()));
+        HIP_TRY(hipMemcpy(M->d_pbase, base.data(), sizeof(int) * base.size(), hipMemcpyHostToDevice));
+        const size_t ne = std::max(1, base[S]);
+        HIP_TRY(hipMalloc(&M->d_ptab_g, sizeof(int) * ne));
+        if (M->has_c_lds) HIP_TRY(hipMalloc(&M->d_ptab_l, sizeof(int) * ne));
+        launch_fill_p(M->d_slice_base, S, M->d_ccodes, M->d_prep, M->d_pcount, M->d_pbase, M->d_cdict,
+                      M->has_c_lds ? M->d_ldsc : nullptr, M->d_ptab_g, M->d_ptab_l, M->stream);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(M->stream));
+    }
+    (void)hipFree(M->d_prep);  // representatives: build only
+    M->d_prep = nullptr;
+    M->has_p = ok;
+    // the LDS kernels keep the table after the windows in one dynamic allocation
+    M->has_p_lds = ok && M->has_c_lds && (size_t)M->lds_doubles * 8 + (size_t)M->pat_max * 4 <= 65536;
+    if (!ok) {
+        for (int** q : {&M->d_pcount, &M->d_pbase, &M->d_ptab_g, &M->d_ptab_l}) {
+            if (*q) (void)hipFree(*q);
+            *q = nullptr;
+        }
+        (void)hipFree(M->d_prow);
+        M->d_prow = nullptr;
+    }
+    return 0;
+}
+
 int build_c_image(hpccg_hip_matrix* M)
 {
     TRY(build_code_image(M, false, &M->d_ccodes, &M->d_cdict, nullptr, &M->d_ldsc, &M->d_ccount, &M->has_c,
                          &M->has_c_lds));
+    TRY(build_p_image(M));
     TRY(build_code_image(M, true, &M->d_vcodes, &M->d_vdict, &M->d_vval, &M->d_vldsc, &M->d_vcount, &M->has_v,
                          &M->has_v_lds));
     if (!M->has_v || M->nslices < 1) return 0;
@@ -655,6 +721,8 @@ const char* variant_unavailable(const hpccg_hip_matrix* M, int v)
     if (v >= 4000 && v < 5000 && !M->has_c_lds) return "the SELL-512-C LDS image";
     if (v >= 5000 && v < 6000 && !M->has_v_lds) return "the SELL-512-V LDS image";
     if (v >= 6000 && v < 8000 && !M->has_v) return "the SELL-512-V image";
+    if (v >= 8000 && v < 8500 && !M->has_p_lds) return "the SELL-512-P LDS image";
+    if (v >= 8500 && v < 9000 && !M->has_p) return "the SELL-512-P image";
     return nullptr;
 }
 
@@ -673,6 +741,16 @@ int choose_variant(const hpccg_hip_matrix* M)
     // ("value_codes"): it stops reading every stored value from HBM per
     // iteration, which the headline bench keeps.
     if (M->value_codes && M->has_v) return (double)M->nslots4 > 100e6 ? 7201 : 7301;
+    // SELL-512-P (8 B value per slot + 1 B pattern id per row) wherever a
+    // slice's row patterns fit: in-CG SpMV 200^3 377 vs 408 us (8226 vs 4200),
+    // 100^3 53.4 vs 58.2 us (8300), 7-pt 256^3 252 vs 277 us (8500 vs 3000).
+    // Non-temporal value loads once the image outgrows the 256 MB Infinity Cache.
+    const bool big_p = (double)M->nslots * 8.0 > 256e6;
+    if (lds && M->has_p_lds) return big_p ? 8226 : 8300;
+    if (!lds && M->has_p) {
+        if (M->uniform && M->width == 7 && big_p) return 8507;  // 7-pt 256^3: 248 vs 253 us
+        return big_p ? 8500 : 8600;
+    }
     if (lds) return M->has_c_lds ? 4200 : (big ? 2200 : 2300);
     if (M->has_c) return big ? 3000 : 3100;
     return big ? 1000 : 0;
@@ -688,6 +766,7 @@ double slot_bytes(const hpccg_hip_matrix* M)
     if (v >= 7000 && v < 8000) return (double)M->nslots4 / std::max<long long>(1, M->nslots);
     if (variant_is_v(v)) return 1.0;
     if ((v >= 3000 && v < 5000)) return 9.0;
+    if (v >= 8000 && v < 9000) return 8.0 + (double)M->nslices * kSliceRows / std::max<long long>(1, M->nslots);
     if (v >= 2000 && v < 3000) return 10.0;
     return 12.0;
 }
@@ -712,7 +791,7 @@ bool fuse_p_effective(const hpccg_hip_matrix* M)
 {
     if (M->spmv_variant == 9999) return false;
     const int v = M->spmv_variant;
-    const bool lds = (v >= 2000 && v < 3000) || (v >= 4000 && v < 6000);
+    const bool lds = (v >= 2000 && v < 3000) || (v >= 4000 && v < 6000) || (v >= 8000 && v < 8500);
     if (M->nranks != 1 && !lds) return false;
     if (M->fuse_p < 0) return lds;
     return M->fuse_p != 0;
@@ -797,6 +876,12 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.ccount = v ? M->d_vcount : M->d_ccount;
     a.vbase4 = M->d_vbase4;
     a.vcodes4 = M->d_vcodes4;
+    a.prow = M->d_prow;
+    a.pcount = M->d_pcount;
+    a.pbase = M->d_pbase;
+    a.ptab_g = M->d_ptab_g;
+    a.ptab_l = M->d_ptab_l;
+    a.pat_max = std::max(1, M->pat_max);
     a.win_ptr = M->d_win_ptr;
     a.win_start = M->d_win_start;
     a.win_len = M->d_win_len;

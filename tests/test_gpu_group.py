@@ -60,7 +60,7 @@ def test_group_kernel_variants_bitwise(hp, gpu):
     Ms = hp.group_generate(24, 20, 9, 3)
     ref = None
     import itertools
-    for v, fold, fuse, defer, ovl in itertools.product((1000, 0, 2000, 2100, 4200, 5200, 7201), (0, 1, 2), (0, 1), (0, 1),
+    for v, fold, fuse, defer, ovl in itertools.product((1000, 0, 2000, 2100, 4200, 5200, 7201, 8200, 8500), (0, 1, 2), (0, 1), (0, 1),
                                                       (0, 1)):
         for M in Ms:
             M.set_option("spmv_variant", v)
@@ -71,7 +71,7 @@ def test_group_kernel_variants_bitwise(hp, gpu):
         if v >= 2000 and fuse:
             assert Ms[1].get_option("overlap") == ovl
         # p = r + beta p inside the SpMV: LDS kernels only on multiple ranks
-        lds = 2000 <= v < 3000 or 4000 <= v < 6000
+        lds = 2000 <= v < 3000 or 4000 <= v < 6000 or 8000 <= v < 8500
         assert Ms[1].get_option("fuse_p") == (fuse if lds else 0)
         niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
         got = (niters, normr, Ms[0].last_trace().tobytes(), b"".join(x.tobytes() for x in xs))

@@ -56,7 +56,8 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
                                      2002, 2100, 2200, 2208, 2300, 2308, 3000, 3001, 3002, 3100,
                                      4000, 4200, 4300, 3027, 5000, 5100, 5200, 5208, 5300, 5308,
                                      5401, 5404, 5204, 6000, 6100, 6104, 6001, 7001, 7101, 7002,
-                                     7102, 7027, 7127, 7201, 7202, 7301, 7302, 7204])
+                                     7102, 7027, 7127, 7201, 7202, 7301, 7302, 7204, 8000, 8200,
+                                     8208, 8300, 8201, 8500, 8501, 8600])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
@@ -71,7 +72,7 @@ def test_sparsemv_variants_agree(hp, gpu, variant):
     x0 = prob.x
     _, it0, nr0, _ = hp.HPCCG(M, prob.b, x0, max_iter=60)
     assert it == it0
-    if variant in (1, 2, 1001, 1002, 2001, 2002, 3001, 3002, 5401, 5404, 5204, 6104, 6001):
+    if variant in (1, 2, 1001, 1002, 2001, 2002, 3001, 3002, 5401, 5404, 5204, 6104, 6001, 8201, 8501):
         assert check_trace(tr, M.last_trace(), RTRANS_RTOL_1GPU) > 10
     else:
         assert nr == nr0
@@ -110,7 +111,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # and the LDS kernels (same rows per thread), fused or not, give the same bits
     for v, fuse in itertools.product((2000, 2100, 2200, 2308, 3000, 3100, 4200, 4300, 5200, 5300, 6000, 6100,
-                                      7001, 7102), (0, 1)):
+                                      7001, 7102, 8000, 8200, 8300, 8500, 8600), (0, 1)):
         M.set_option("spmv_variant", v)
         M.set_option("fuse_p", fuse)
         M.set_option("redund", 1 - fuse)
@@ -527,7 +528,8 @@ def test_sell_v_fallback_for_many_values(hp, gpu):
     M = hp.Matrix.from_csr(rp, cols, vals)
     assert M.get_option("value_codes_available") == 0
     M.set_option("value_codes", 1)
-    assert 3000 <= M.get_option("spmv_variant") < 5000
+    v = M.get_option("spmv_variant")
+    assert 3000 <= v < 5000 or 8000 <= v < 9000  # SELL-512-C or -P, not -V
     for v in (5200, 6000):
         with pytest.raises(hp.HPCCGError, match="SELL-512-V"):
             M.set_option("spmv_variant", v)
@@ -542,7 +544,7 @@ def test_value_codes_opt_in_bitwise(hp, gpu, dims, s7):
     the generated stencil picks a SELL-512-V kernel and the solve gives the
     same bits as the default kernel."""
     M = hp.Matrix.generate(*dims, use_7pt=s7)
-    assert M.get_option("value_codes") == 0 and M.get_option("spmv_variant") < 5000
+    assert M.get_option("value_codes") == 0 and M.get_option("spmv_variant") >= 8000  # SELL-512-P
     assert M.get_option("value_codes_available") == 1
     b, _, _ = M.vectors()
     import torch
@@ -554,3 +556,56 @@ def test_value_codes_opt_in_bitwise(hp, gpu, dims, s7):
         _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=80, device=True)
         outs.append((it, nr, M.last_trace().tobytes(), host(x).tobytes()))
     assert outs[0] == outs[1] == outs[2]
+
+
+def _random_patterns(n, seed, noffs=10, band=None):
+    """Symmetric matrix whose rows each keep a random subset of `noffs`
+    offsets: few distinct offsets per slice (SELL-512-C fits), hundreds of
+    distinct row patterns per 512-row slice."""
+    rng = np.random.default_rng(seed)
+    offs = [1, 2, 3, 5, 8, 13, 21, 34, 55, 89][:noffs]
+    nb = [set() for _ in range(n)]
+    for i in range(n):
+        for o in offs:
+            if rng.random() < 0.5 and i + o < n:
+                nb[i].add(i + o)
+                nb[i + o].add(i)
+    rp = [0]
+    cols, vals = [], []
+    for i in range(n):
+        row = [i] + sorted(nb[i])
+        cols += row
+        vals += [2.0 + len(row)] + [-1.0] * (len(row) - 1)
+        rp.append(len(cols))
+    return np.array(rp, np.int64), np.array(cols, np.int32), np.array(vals, np.float64)
+
+
+def test_sell_p_fallback_for_many_patterns(hp, gpu):
+    """Rows with random subsets of 10 offsets: SELL-512-C fits (<= 20 offsets
+    per slice) but a slice has far more than 256 row patterns, so the
+    library keeps the C kernels and refuses the P variants; same bits."""
+    n = 3000
+    rp, cols, vals = _random_patterns(n, 7)
+    M = hp.Matrix.from_csr(rp, cols, vals)
+    assert 3000 <= M.get_option("spmv_variant") < 5000
+    for v in (8200, 8500):
+        with pytest.raises(hp.HPCCGError, match="SELL-512-P"):
+            M.set_option("spmv_variant", v)
+    b = 1.0 + (np.arange(n) % 5)
+    out = _solve_all(hp, M, b, (1000, 3000, 3100))
+    assert all(o == out[1000] for o in out.values())
+
+
+def test_sell_p_few_patterns_irregular(hp, gpu):
+    """Rows with random subsets of 3 offsets (at most 8 patterns per slice,
+    irregular order): the P kernels fit and give the SELL-512 bits, and the
+    solve tracks the oracle."""
+    n = 5000
+    rp, cols, vals = _random_patterns(n, 11, noffs=3)
+    M = hp.Matrix.from_csr(rp, cols, vals)
+    b = 1.0 + (np.arange(n) % 7)
+    out = _solve_all(hp, M, b, (1000, 8500, 8600) + ((8200, 8300) if M.get_option("lds_doubles") else ()))
+    assert all(o == out[1000] for o in out.values())
+    A = oracle.CSR(rp, cols, vals, np.zeros(n), b, np.zeros(n))
+    ref = oracle.hpccg(A, max_iter=40)
+    assert check_trace(np.frombuffer(out[1000][2]), ref["trace"], RTRANS_RTOL_1GPU) >= 5
