@@ -375,6 +375,13 @@ def main():
                                  "halo": times_acc[5] / args.steps},
             "cpu_baseline": None,
         }
+        rf = out["roofline"]
+        if rf["traffic"]:
+            # the bytes the chip moved (PMC) over the same launch time: the
+            # credited formula counts 12 B per nonzero and unfused vector passes,
+            # more than SELL-512-P + fusion stream, so frac can pass 1.0
+            rf["traffic_gbs"] = round(rf["traffic"] / spmv_avg_s / 1e9, 1)
+            rf["traffic_frac"] = round(rf["traffic_gbs"] / HBM_PEAK_GBS, 4)
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(n, n, n, use_7pt)

@@ -15,11 +15,22 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+FORMATS = {
+    "k_spmv": "SELL-512 (8 B value + int32 column per slot)",
+    "k_spmv_c": "SELL-512-C (8 B value + 1-byte offset code per slot)",
+    "k_spmv_lds": "SELL-512-L/-C with x from LDS windows",
+    "k_spmv_lp": "SELL-512-P (8 B value per slot + 1-byte row-pattern id per row), x from LDS windows",
+    "k_spmv_pp": "SELL-512-P (8 B value per slot + 1-byte row-pattern id per row), x gathered",
+    "k_spmv_v4": "SELL-512-V (1-byte (offset, value) codes in 4-slot chunks)",
+}
 
 
 def newest(pattern):
@@ -80,28 +91,28 @@ def main():
         fetch_factor = stream_read / (f_stream * 1024.0)
     else:  # no width-27 image to stream: the factor the 27-pt calibrations measure (2.0)
         stream_read, f_stream, w_stream, fetch_factor = None, None, None, 2.0
-    SPMV = ("k_spmv<", "k_spmv_lds<", "k_spmv_c<")
+    SPMV = ("k_spmv<", "k_spmv_lds<", "k_spmv_c<", "k_spmv_lp<", "k_spmv_pp<", "k_spmv_v4<")
     f_spmv, kname = pick(fetch, SPMV, "FETCH_SIZE")
     w_spmv, _ = pick(write, SPMV, "WRITE_SIZE")
     spmv_read = f_spmv * 1024.0 * fetch_factor
     spmv_write = w_spmv * 1024.0
-    import re
     targs = re.search(r"k_spmv\w*<([^>]*)>", kname).group(1).split(",")
-    # k_spmv<kRpt, kW, kMinW, kNT, kFuse>, k_spmv_lds<kRpt, kNT, kFuse, kPre, kCode>,
-    # k_spmv_c<kRpt, kNT, kFuse>
-    fuse_p = (targs[2] if ("k_spmv_lds" in kname or "k_spmv_c" in kname) else targs[-1]).strip() == "true"
+    # k_spmv<kRpt, kW, kMinW, kNT, kFuse>; every other SpMV kernel (k_spmv_lds,
+    # k_spmv_c, k_spmv_lp, k_spmv_pp, k_spmv_v4) has kFuse third
+    fuse_p = (targs[-1] if "k_spmv<" in kname else targs[2]).strip() == "true"
     algo = 12.0 * nnz + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fuse_p else 0.0)
 
     avg_ns = None
     calls = -1
+    # the kernel the PMC passes measured (the stats run may also hold other
+    # SpMV kernels, e.g. bench's SELL-512-V secondary figure)
     for row in csv.DictReader(open(stats)):
-        if any(nd in row["Name"] for nd in SPMV) and int(row["Calls"]) > calls:
+        if row["Name"] == kname and int(row["Calls"]) > calls:
             avg_ns, calls = float(row["AverageNs"]), int(row["Calls"])
     out = {
         "tag": tag,
         "problem": f"{stencil}-pt {n}^3, SELL-512 width {width} ({slots} slots, nnz {nnz}); "
-                   "k_spmv_lds<..., true> streams the SELL-512-C image (8 B value + 1 B offset code "
-                   "per slot, x from LDS windows)",
+                   + FORMATS.get(re.search(r"(k_spmv\w*)<", kname).group(1), kname),
         "kernel": kname,
         "fuse_p": fuse_p,
         "bytes_formula": "12 nnz + 20 n + 16 n" + (" + 24 n" if fuse_p else ""),
