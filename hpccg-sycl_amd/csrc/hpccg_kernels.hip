@@ -1711,6 +1711,37 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
     }
 }
 
+// x += alpha_j p_j for j = j0..j1 in order (HPCCG.cpp:383, one rounding per
+// term as in the reference); alpha_kcur comes from the caller (the update's own
+// alpha, not yet in ahist for the reader). Four p loads are issued before their
+// adds, so a long ring does not serialise one HBM latency per term.
+template <int kRpt>
+__device__ __forceinline__ void x_accumulate(const CgArgs& a, int row, int j0, int j1, int kcur, double alpha_kcur,
+                                             Rows<kRpt>& xn)
+{
+    constexpr int kB = 4;
+    int j = j0;
+    for (; j + kB - 1 <= j1; j += kB) {
+        Rows<kRpt> pj[kB];
+        double aj[kB];
+#pragma unroll
+        for (int b = 0; b < kB; b++) {
+            pj[b] = ld<kRpt>(cur_p(a, j + b) + row);
+            aj[b] = (j + b == kcur) ? alpha_kcur : a.ahist[j + b];
+        }
+#pragma unroll
+        for (int b = 0; b < kB; b++)
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) xn.v[i] = xn.v[i] + aj[b] * pj[b].v[i];
+    }
+    for (; j <= j1; j++) {
+        const double aj = (j == kcur) ? alpha_kcur : a.ahist[j];
+        const Rows<kRpt> pj = ld<kRpt>(cur_p(a, j) + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) xn.v[i] = xn.v[i] + aj * pj.v[i];
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Fused update + r.r partial.
 // prologue: r = b + (-1)*Ap                (HPCCG.cpp:352)
@@ -1746,12 +1777,7 @@ __device__ __forceinline__ double update_slice(const CgArgs& a, int s, int lt, i
             // deferred x update (HPCCG.cpp:383 for iterations k-nring+1 .. k): the same
             // x + alpha_j p_j roundings in the same order, one pass over x
             Rows<kRpt> xn = ld<kRpt>(a.x + row);
-            for (int j = k - a.nring + 1; j <= k; j++) {
-                const double aj = (j == k) ? alpha : a.ahist[j];
-                const Rows<kRpt> pj = ld<kRpt>(cur_p(a, j) + row);
-#pragma unroll
-                for (int i = 0; i < kRpt; i++) xn.v[i] = xn.v[i] + aj * pj.v[i];
-            }
+            x_accumulate<kRpt>(a, row, k - a.nring + 1, k, k, alpha, xn);
             st_rows<kRpt>(a.x, row, a.n, xn);
         }
     }
@@ -1927,12 +1953,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_xflush(CgArgs a)
     if (s >= a.nslices) return;
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     Rows<kRpt> xn = ld<kRpt>(a.x + row);
-    for (int j = first; j <= niters; j++) {
-        const double aj = a.ahist[j];
-        const Rows<kRpt> pj = ld<kRpt>(cur_p(a, j) + row);
-#pragma unroll
-        for (int i = 0; i < kRpt; i++) xn.v[i] = xn.v[i] + aj * pj.v[i];
-    }
+    x_accumulate<kRpt>(a, row, first, niters, -1, 0.0, xn);
     st_rows<kRpt>(a.x, row, a.n, xn);
 }
 

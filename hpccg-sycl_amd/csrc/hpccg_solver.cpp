@@ -244,11 +244,13 @@ struct hpccg_hip_matrix {
     int *d_win_ptr = nullptr, *d_win_start = nullptr, *d_win_len = nullptr, *d_win_off = nullptr;
     // workspace (padded to a multiple of kSliceRows rows)
     size_t npad = 0;
-    double* d_pbuf = nullptr;  // kXDefer ring buffers of [ghost_lo_pad | npad | ghost_hi_pad]
+    double* d_pbuf = nullptr;  // ring_alloc buffers of [ghost_lo_pad | npad | ghost_hi_pad]
+    int ring_alloc = 0;        // p ring buffers allocated
     double* d_p = nullptr;     // local rows of ring buffer 0
     long long pstride = 0;     // doubles between ring buffers
     double* d_ahist = nullptr;
-    int x_defer = 1;           // batched x update every kXDefer iterations
+    int x_defer = 1;           // batched x update every x_ring iterations
+    int x_ring = kXRingDefault; // p ring length with x_defer (2..kXRingMax)
     int rev_update = 1;        // update kernel walks slices backwards (reads the SpMV's latest writes first)
     long long resident_mb = -1; // NT kernels: MB of leading slices on default-policy loads (-1 auto)
     int redund = 0;            // consumers complete the dots themselves, no finalize kernels (measured slower)
@@ -658,6 +660,21 @@ int build_c_image(hpccg_hip_matrix* M)
     return 0;
 }
 
+// The p ring: nbuf buffers of pstride doubles, local rows 512-row aligned.
+int alloc_ring(hpccg_hip_matrix* M, int nbuf)
+{
+    if (M->d_pbuf) (void)hipFree(M->d_pbuf);
+    M->d_pbuf = nullptr;
+    M->ring_alloc = 0;
+    const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
+    const size_t ptotal = (size_t)M->pstride * nbuf;
+    HIP_TRY(hipMalloc(&M->d_pbuf, sizeof(double) * ptotal));
+    HIP_TRY(hipMemset(M->d_pbuf, 0, sizeof(double) * ptotal));
+    M->d_p = M->d_pbuf + glo_pad;
+    M->ring_alloc = nbuf;
+    return 0;
+}
+
 int alloc_workspace(hpccg_hip_matrix* M)
 {
     M->npad = (size_t)M->nslices * kSliceRows;
@@ -666,10 +683,7 @@ int alloc_workspace(hpccg_hip_matrix* M)
     const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
     const size_t ghi_pad = ((size_t)M->ghost_hi + 2 + kSliceRows - 1) / kSliceRows * kSliceRows;
     M->pstride = (long long)(glo_pad + M->npad + ghi_pad);
-    const size_t ptotal = (size_t)M->pstride * kXDefer;
-    HIP_TRY(hipMalloc(&M->d_pbuf, sizeof(double) * ptotal));
-    HIP_TRY(hipMemset(M->d_pbuf, 0, sizeof(double) * ptotal));
-    M->d_p = M->d_pbuf + glo_pad;
+    TRY(alloc_ring(M, M->x_ring));
     double** vecs[] = {&M->d_r, &M->d_Ap, &M->d_x, &M->d_b};
     for (double** v : vecs) {
         HIP_TRY(hipMalloc(v, sizeof(double) * M->npad));
@@ -797,15 +811,16 @@ bool fuse_p_effective(const hpccg_hip_matrix* M)
     return M->fuse_p != 0;
 }
 
-// fold auto (measured, profiles/r01_final_*): completing p.Ap inside the SpMV
-// saves the k_finalize launch (~7 us incl. its boundary) but holds each
-// block's LDS for the publish round trip. 100^3 (1954 slices): 13062 vs 12475
-// it/s; 200^3 (15625 slices): 1943 vs 1954. r.r in the update kernel: slower
-// at both (every block of a short kernel waits for its ticket).
+// fold auto (measured): completing p.Ap inside the SpMV saves the k_finalize
+// launch (7-14 us incl. its boundary) but holds each block's wave 0 for the
+// publish round trip. 100^3 (1954 slices): 13062 vs 12475 it/s (C format);
+// SELL-512-P: 7-pt 256^3 (32768 slices) 2326-2432 vs 2275-2410, 200^3 (15625)
+// 2277-2293 vs 2279-2286 (even). r.r in the update kernel: slower at every
+// size (every block of a short kernel waits for its ticket).
 int fold_effective(const hpccg_hip_matrix* M)
 {
     if (M->fold >= 0 && M->fold <= 3) return M->fold;
-    return M->nslices <= 8192 ? 2 : 0;
+    return 2;
 }
 
 // Redundant dot completion (k_update_g + cur_rr): single rank, group sums that
@@ -846,7 +861,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
         const double sl = (double)resident_mb_effective(M) * 1e6 / std::max(1.0, per_slice);
         a.nt_split = (int)std::min<double>(M->grid / kNumXcd, sl / kNumXcd);
     }
-    a.nring = a.xdefer ? kXDefer : (a.fuse_p ? 2 : 1);
+    a.nring = a.xdefer ? M->x_ring : (a.fuse_p ? 2 : 1);
     a.ahist = M->d_ahist;
     a.fold = fold_effective(M);
     a.redund = redund_effective(M, max_iter) ? 1 : 0;
@@ -2149,6 +2164,14 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->fuse_p = (int)value;
     } else if (!std::strcmp(key, "x_defer")) {
         M->x_defer = (int)value;
+    } else if (!std::strcmp(key, "x_ring")) {
+        if (value < 2 || value > kXRingMax) return set_err(HPCCG_HIP_EINVAL, "x_ring must be 2..%d", kXRingMax);
+        if (value > M->ring_alloc) {
+            HIP_TRY(hipSetDevice(M->device));
+            HIP_TRY(hipStreamSynchronize(M->stream));
+            TRY(alloc_ring(M, (int)value));
+        }
+        M->x_ring = (int)value;
     } else if (!std::strcmp(key, "rev_update")) {
         M->rev_update = (int)value;
     } else if (!std::strcmp(key, "redund")) {
@@ -2259,6 +2282,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "fuse_p")) *value = fuse_p_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "fold")) *value = fold_effective(M);
     else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
+    else if (!std::strcmp(key, "x_ring")) *value = M->x_ring;
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "resident_mb")) *value = resident_mb_effective(M);
     else if (!std::strcmp(key, "redund")) *value = redund_effective(M, 2) ? 1 : 0;  // off unless set

@@ -83,7 +83,7 @@ def test_sparsemv_variants_agree(hp, gpu, variant):
 @pytest.mark.parametrize("dims", [(24, 20, 18), (13, 7, 5), (40, 40, 40)])
 def test_fusion_options_bitwise_equal(hp, gpu, dims):
     """fuse_p (p update inside the SpMV gather), fold (last-block dot
-    completion) and x_defer (x updated every 8 iterations) change only where
+    completion) and x_defer (x updated every x_ring iterations) change only where
     work happens, never a value: every combination, eager and graph launches,
     gives bitwise the same solve."""
     prob = hp.generate_matrix(*dims)
@@ -99,7 +99,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         M.set_option("redund", red)  # consumers complete the dots themselves (fold unused then)
         M.set_option("rev_update", (fuse + fold + defer) % 2)  # slice order: no value changes
         x = prob.x
-        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)  # 119 iterations: 7 pending x updates
+        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)  # 119 iterations: x updates left for k_xflush
         assert M.get_option("fuse_p") == fuse
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # one dot folded, the other finalized by its own kernel
@@ -117,6 +117,18 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         M.set_option("redund", 1 - fuse)
         M.set_option("resident_mb", fuse)  # 1 MB on default-policy loads: no value changes
         assert M.get_option("fuse_p") == fuse
+        x = prob.x
+        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
+        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    # the x-deferral depth (p ring length) only moves when x is written:
+    # rings of 2 .. 64, 119 iterations leave 1 .. 55 updates for k_xflush
+    M.set_option("spmv_variant", 8200)
+    M.set_option("redund", 0)
+    M.set_option("x_defer", 1)
+    for ring, graph in ((2, 1), (5, 0), (16, 1), (32, 1), (64, 0), (8, 1)):
+        M.set_option("x_ring", ring)
+        M.set_option("use_graph", graph)
+        assert M.get_option("x_ring") == ring
         x = prob.x
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
