@@ -144,6 +144,8 @@ def main():
     ap.add_argument("--redund", type=int, default=-1,
                     help="consumers complete the dot products themselves (-1 default)")
     ap.add_argument("--x-defer", type=int, default=-1, help="batched x update (-1 default)")
+    ap.add_argument("--update-slices", type=int, default=-1,
+                    help="slices per loop-update workgroup: 1, 2, 4, 8 (-1 default)")
     ap.add_argument("--x-ring", type=int, default=-1,
                     help="x-update deferral depth = p ring length (-1 default)")
     ap.add_argument("--resident-mb", type=int, default=-1,
@@ -193,6 +195,8 @@ def main():
         M.set_option("graph_chunk", args.graph_chunk)
     if args.x_defer >= 0:
         M.set_option("x_defer", args.x_defer)
+    if args.update_slices > 0:
+        M.set_option("update_slices", args.update_slices)
     if args.x_ring > 0:
         M.set_option("x_ring", args.x_ring)
     if args.rev_update >= 0:
@@ -337,7 +341,7 @@ def main():
                 "spmv_variant": M.get_option("spmv_variant"),
                 "matrix_format": matrix_format(M.get_option("spmv_variant"))[0],
                 "matrix_bytes_per_slot": matrix_format(M.get_option("spmv_variant"))[1],
-                "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update",
+                "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "update_slices", "x_defer", "x_ring", "rev_update",
                                                          "resident_mb", "overlap", "value_codes")},
             },
             "cg_iterations_per_s_global": round(it_per_s, 3),

@@ -363,29 +363,31 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
     if (a.nranks > 1) stamp(a, which == kRR ? kStampArRR : kStampArPAP);
 }
 
-// bs valid in thread 0. Only wave 0 takes part in the hand-off: the other waves
-// of the block return right away (the publish round trip then holds one wave,
-// not the block).
-template <int kThreads>
-__device__ __forceinline__ void complete_dot(const CgArgs& a, int s, double bs, int which, int kfinal)
+// Partials of slices s0 .. s0 + cnt - 1 (one group: s0 % kGroup + cnt <=
+// kGroup), the partial of slice s0 + j in lane j of wave 0; called by wave 0
+// only. The lanes publish their partials together, lane 0 takes one ticket of
+// cnt arrivals on the group; the group's last arriver then sums the group and
+// takes a ticket on the top counter, whose last arriver forms the total.
+__device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, int s0, int cnt, double bs, int which,
+                                                   int kfinal)
 {
     const int ng = ngroups_of(a);
     double* gp = a.partial + a.nslices + which * ng;       // group sums of this dot
     unsigned* gt = a.tickets + which * (ng + 1);          // group tickets, then the top one
+    const int lane = threadIdx.x;
     if (!fold_of(a, which)) {
-        if (threadIdx.x == 0) a.partial[s] = bs;
+        if (lane < cnt) a.partial[s0 + lane] = bs;
         return;
     }
-    if (threadIdx.x >= kWave) return;
-    const int lane = threadIdx.x;
-    const int g = s / kGroup;
+    const int g = s0 / kGroup;
     int role = 0;
+    if (lane < cnt) st_sc1(a.partial + s0 + lane, bs);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
-        st_sc1(a.partial + s, bs);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned glen = (unsigned)min(kGroup, a.nslices - g * kGroup);
-        const unsigned t = __hip_atomic_fetch_add(gt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        role = (t == glen - 1u) ? 1 : 0;
+        const unsigned t =
+            __hip_atomic_fetch_add(gt + g, (unsigned)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        role = (t + (unsigned)cnt == glen) ? 1 : 0;
         if (role) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -414,6 +416,16 @@ __device__ __forceinline__ void complete_dot(const CgArgs& a, int s, double bs, 
         finish_dot(a, tot, which, kfinal);
         __hip_atomic_store(gt + ng, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
     }
+}
+
+// bs valid in thread 0. Only wave 0 takes part in the hand-off: the other waves
+// of the block return right away (the publish round trip then holds one wave,
+// not the block).
+template <int kThreads>
+__device__ __forceinline__ void complete_dot(const CgArgs& a, int s, double bs, int which, int kfinal)
+{
+    if (threadIdx.x >= kWave) return;
+    complete_dot_lanes(a, s, 1, bs, which, kfinal);
 }
 
 // ---------------------------------------------------------------------------
@@ -1816,6 +1828,79 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
     complete_dot<kSliceRows / kRpt>(a, s, bs, kRR, kPrologue ? 1 : k + 1);
 }
 
+// The loop update over kM consecutive slices per workgroup (a.um = kM): the
+// same per-slice values, partials and partial tree as k_update (each slice's
+// block_sum shape), but one publish round trip and one ticket per kM slices,
+// so folding r.r into the update costs a quarter of the tickets at kM = 4.
+template <int kRpt, int kM>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_update_m(CgArgs a)
+{
+    constexpr int kThreads = kSliceRows / kRpt;
+    constexpr int kWaves = kThreads / kWave;
+    static_assert(kGroup % kM == 0, "a workgroup's slices stay in one group");
+    __shared__ double wsum[kM][kWaves];
+    const int k = a.kst[0];
+    const bool run = cg_run(a, k, false);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (run)
+            stamp(a, kStampUpdate);
+        else
+            mark_end(a);
+    }
+    if (!run) return;
+    const int S = a.rev ? xcd_slice_rev(a.umgrid) : xcd_slice(a.umgrid);
+    const int s0 = S * kM;
+    if (s0 >= a.nslices) return;
+    const int cnt = min(kM, a.nslices - s0);
+    const double alpha = a.g[kRR] / a.g[kPAP];
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ahist[k] = alpha;
+    double d[kM];
+    if (a.xdefer && k % a.nring != 0) {
+        // r = r - alpha Ap only (x deferred): every slice's loads first
+        Rows<kRpt> apv[kM], rv[kM];
+#pragma unroll
+        for (int j = 0; j < kM; j++) {
+            const int row = (s0 + j) * kSliceRows + threadIdx.x * kRpt;
+            if (j < cnt) {
+                apv[j] = ld<kRpt>(a.Ap + row);
+                rv[j] = ld<kRpt>(a.r + row);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kM; j++) {
+            d[j] = 0.0;
+            if (j < cnt) {
+                const int row = (s0 + j) * kSliceRows + threadIdx.x * kRpt;
+                Rows<kRpt> rn;
+#pragma unroll
+                for (int i = 0; i < kRpt; i++) rn.v[i] = rv[j].v[i] + (-alpha) * apv[j].v[i];
+                st_rows<kRpt>(a.r, row, a.n, rn);
+#pragma unroll
+                for (int i = 0; i < kRpt; i++)
+                    if (row + i < a.n) d[j] += rn.v[i] * rn.v[i];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kM; j++)
+            d[j] = j < cnt ? update_slice<kRpt, false>(a, s0 + j, threadIdx.x, k, alpha) : 0.0;
+    }
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+#pragma unroll
+    for (int j = 0; j < kM; j++) {
+        const double v = wave_sum(d[j]);
+        if (lane == 0) wsum[j][w] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x >= kWave) return;
+    double bs = 0.0;  // block_sum's order: 0 + wave 0 + wave 1 + ...
+    if (lane < cnt) {
+#pragma unroll
+        for (int i = 0; i < kWaves; i++) bs += wsum[lane][i];
+    }
+    complete_dot_lanes(a, s0, cnt, bs, kRR, k + 1);
+}
+
 // ---------------------------------------------------------------------------
 // Redundant dot completion (single rank, a.redund): no finalize kernels and no
 // tickets between workgroups. The update runs one workgroup per 64-slice group
@@ -2353,6 +2438,12 @@ void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)
     }
     if (prologue)
         hipLaunchKernelGGL((k_update<kRpt, true>), dim3(a.grid), dim3(kBlock), 0, s, a);
+    else if (a.um == 2)
+        hipLaunchKernelGGL((k_update_m<kRpt, 2>), dim3(a.umgrid), dim3(kBlock), 0, s, a);
+    else if (a.um == 4)
+        hipLaunchKernelGGL((k_update_m<kRpt, 4>), dim3(a.umgrid), dim3(kBlock), 0, s, a);
+    else if (a.um == 8)
+        hipLaunchKernelGGL((k_update_m<kRpt, 8>), dim3(a.umgrid), dim3(kBlock), 0, s, a);
     else
         hipLaunchKernelGGL((k_update<kRpt, false>), dim3(a.grid), dim3(kBlock), 0, s, a);
 }

@@ -254,6 +254,7 @@ struct hpccg_hip_matrix {
     int rev_update = 1;        // update kernel walks slices backwards (reads the SpMV's latest writes first)
     long long resident_mb = -1; // NT kernels: MB of leading slices on default-policy loads (-1 auto)
     int redund = 0;            // consumers complete the dots themselves, no finalize kernels (measured slower)
+    int update_slices = 1;     // slices per loop-update workgroup (1, 2, 4, 8)
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_partial = nullptr;
     unsigned int* d_tickets = nullptr;
@@ -869,6 +870,9 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     {
         const int ng = (M->nslices + 63) / 64;
         a.ugrid = std::max(kNumXcd, (ng + kNumXcd - 1) / kNumXcd * kNumXcd);
+        a.um = M->update_slices;
+        const int nb = (M->nslices + a.um - 1) / a.um;
+        a.umgrid = std::max(kNumXcd, (nb + kNumXcd - 1) / kNumXcd * kNumXcd);
     }
     a.tickets = M->d_tickets;
     a.Ap = M->d_Ap;
@@ -2176,6 +2180,10 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->rev_update = (int)value;
     } else if (!std::strcmp(key, "redund")) {
         M->redund = (int)value;
+    } else if (!std::strcmp(key, "update_slices")) {
+        if (value != 1 && value != 2 && value != 4 && value != 8)
+            return set_err(HPCCG_HIP_EINVAL, "update_slices must be 1, 2, 4 or 8");
+        M->update_slices = (int)value;
     } else if (!std::strcmp(key, "overlap")) {
         M->overlap = (int)value;
     } else if (!std::strcmp(key, "graph_chunk")) {
@@ -2283,6 +2291,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "fold")) *value = fold_effective(M);
     else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
     else if (!std::strcmp(key, "x_ring")) *value = M->x_ring;
+    else if (!std::strcmp(key, "update_slices")) *value = M->update_slices;
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "resident_mb")) *value = resident_mb_effective(M);
     else if (!std::strcmp(key, "redund")) *value = redund_effective(M, 2) ? 1 : 0;  // off unless set

@@ -132,6 +132,17 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         x = prob.x
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    # several slices per update workgroup: same partials and tree, r.r folded or not,
+    # x deferred or not, slice count not a multiple of the slices per workgroup
+    for um, fold, defer in itertools.product((2, 4, 8), (1, 2), (1, 0)):
+        M.set_option("update_slices", um)
+        M.set_option("fold", fold)
+        M.set_option("x_defer", defer)
+        assert M.get_option("update_slices") == um
+        x = prob.x
+        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
+        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    M.set_option("update_slices", 1)
     assert all(r == results[0] for r in results)
 
 
