@@ -103,8 +103,9 @@ inline __host__ __device__ bool fold_of(const CgArgs& a, int which)
 constexpr unsigned short kLdsPad = 0xFFFF;
 constexpr int kLdsMaxDoubles = 8192;  // 64 KiB of LDS per block at most
 constexpr int kLdsMaxWindows = 16;
-// p ring length = x-update deferral depth (option x_ring). 32 vs 8, in-CG
-// update kernel: 7-pt 256^3 92.8 vs 102.7 us, 200^3 45.4 vs 46.6 us.
+// p ring length = x-update deferral depth (option x_ring) for images well
+// beyond the Infinity Cache. 32 vs 8, in-CG update kernel: 7-pt 256^3 92.8 vs
+// 102.7 us, 200^3 45.4 vs 46.6 us.
 constexpr int kXRingDefault = 32;
 constexpr int kXRingMax = 64;
 

@@ -250,7 +250,7 @@ struct hpccg_hip_matrix {
     long long pstride = 0;     // doubles between ring buffers
     double* d_ahist = nullptr;
     int x_defer = 1;           // batched x update every x_ring iterations
-    int x_ring = kXRingDefault; // p ring length with x_defer (2..kXRingMax)
+    int x_ring = -1;           // p ring length with x_defer (2..kXRingMax; -1 auto, x_ring_effective)
     int rev_update = 1;        // update kernel walks slices backwards (reads the SpMV's latest writes first)
     long long resident_mb = -1; // NT kernels: MB of leading slices on default-policy loads (-1 auto)
     int redund = 0;            // consumers complete the dots themselves, no finalize kernels (measured slower)
@@ -661,16 +661,30 @@ int build_c_image(hpccg_hip_matrix* M)
     return 0;
 }
 
+// x_ring auto: the long ring where the matrix image is far beyond the 256 MB
+// Infinity Cache (7-pt 256^3 update 93 vs 103 us with 32 vs 8); near it, the 32
+// p buffers cycled through the cache evict the image (100^3: 14290 vs 14160
+// it/s with 8 vs 32).
+int x_ring_effective(const hpccg_hip_matrix* M)
+{
+    if (M->x_ring > 0) return M->x_ring;
+    return (double)M->nslots * 8.0 > 512e6 ? kXRingDefault : 8;
+}
+
 // The p ring: nbuf buffers of pstride doubles, local rows 512-row aligned.
 int alloc_ring(hpccg_hip_matrix* M, int nbuf)
 {
-    if (M->d_pbuf) (void)hipFree(M->d_pbuf);
-    M->d_pbuf = nullptr;
-    M->ring_alloc = 0;
+    // the new ring first: on failure the matrix keeps its old one
     const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
     const size_t ptotal = (size_t)M->pstride * nbuf;
-    HIP_TRY(hipMalloc(&M->d_pbuf, sizeof(double) * ptotal));
-    HIP_TRY(hipMemset(M->d_pbuf, 0, sizeof(double) * ptotal));
+    double* buf = nullptr;
+    HIP_TRY(hipMalloc(&buf, sizeof(double) * ptotal));
+    if (hipMemset(buf, 0, sizeof(double) * ptotal) != hipSuccess) {
+        (void)hipFree(buf);
+        return set_err(HPCCG_HIP_EHIP, "hipMemset of the p ring failed");
+    }
+    if (M->d_pbuf) (void)hipFree(M->d_pbuf);
+    M->d_pbuf = buf;
     M->d_p = M->d_pbuf + glo_pad;
     M->ring_alloc = nbuf;
     return 0;
@@ -684,7 +698,7 @@ int alloc_workspace(hpccg_hip_matrix* M)
     const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
     const size_t ghi_pad = ((size_t)M->ghost_hi + 2 + kSliceRows - 1) / kSliceRows * kSliceRows;
     M->pstride = (long long)(glo_pad + M->npad + ghi_pad);
-    TRY(alloc_ring(M, M->x_ring));
+    TRY(alloc_ring(M, x_ring_effective(M)));
     double** vecs[] = {&M->d_r, &M->d_Ap, &M->d_x, &M->d_b};
     for (double** v : vecs) {
         HIP_TRY(hipMalloc(v, sizeof(double) * M->npad));
@@ -862,7 +876,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
         const double sl = (double)resident_mb_effective(M) * 1e6 / std::max(1.0, per_slice);
         a.nt_split = (int)std::min<double>(M->grid / kNumXcd, sl / kNumXcd);
     }
-    a.nring = a.xdefer ? M->x_ring : (a.fuse_p ? 2 : 1);
+    a.nring = a.xdefer ? x_ring_effective(M) : (a.fuse_p ? 2 : 1);
     a.ahist = M->d_ahist;
     a.fold = fold_effective(M);
     a.redund = redund_effective(M, max_iter) ? 1 : 0;
@@ -2169,13 +2183,19 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "x_defer")) {
         M->x_defer = (int)value;
     } else if (!std::strcmp(key, "x_ring")) {
-        if (value < 2 || value > kXRingMax) return set_err(HPCCG_HIP_EINVAL, "x_ring must be 2..%d", kXRingMax);
-        if (value > M->ring_alloc) {
+        if (value != -1 && (value < 2 || value > kXRingMax))
+            return set_err(HPCCG_HIP_EINVAL, "x_ring must be -1 (auto) or 2..%d", kXRingMax);
+        const int prev = M->x_ring;
+        M->x_ring = (int)value;
+        if (x_ring_effective(M) > M->ring_alloc) {
             HIP_TRY(hipSetDevice(M->device));
             HIP_TRY(hipStreamSynchronize(M->stream));
-            TRY(alloc_ring(M, (int)value));
+            const int rc = alloc_ring(M, x_ring_effective(M));
+            if (rc) {
+                M->x_ring = prev;
+                return rc;
+            }
         }
-        M->x_ring = (int)value;
     } else if (!std::strcmp(key, "rev_update")) {
         M->rev_update = (int)value;
     } else if (!std::strcmp(key, "redund")) {
@@ -2290,7 +2310,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "fuse_p")) *value = fuse_p_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "fold")) *value = fold_effective(M);
     else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
-    else if (!std::strcmp(key, "x_ring")) *value = M->x_ring;
+    else if (!std::strcmp(key, "x_ring")) *value = x_ring_effective(M);
     else if (!std::strcmp(key, "update_slices")) *value = M->update_slices;
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "resident_mb")) *value = resident_mb_effective(M);

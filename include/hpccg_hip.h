@@ -134,7 +134,8 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  * block of the producing kernel completes a dot product: 0 neither, 1 both,
  * 2 p.Ap only, 3 r.r only; -1 auto (default): 2), "x_defer" (1 = x += alpha p batched
  * every x_ring iterations, default), "x_ring" (p ring length = x deferral
- * depth, 2..64, default 32; a longer ring allocates more p buffers),
+ * depth, 2..64; -1 auto (default): 32 for matrix images over 512 MB, else 8;
+ * a longer ring allocates more p buffers),
  * "update_slices" (1, 2, 4 or 8 slices per loop-update workgroup, default 1), "rev_update" (1 = the update kernel walks each
  * XCD's slices backwards, default), "resident_mb" (non-temporal SpMV kernels:
  * this many MB of leading slices per XCD use default-policy loads so they can

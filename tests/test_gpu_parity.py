@@ -125,10 +125,10 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     M.set_option("spmv_variant", 8200)
     M.set_option("redund", 0)
     M.set_option("x_defer", 1)
-    for ring, graph in ((2, 1), (5, 0), (16, 1), (32, 1), (64, 0), (8, 1)):
+    for ring, graph in ((2, 1), (5, 0), (16, 1), (32, 1), (64, 0), (8, 1), (-1, 1)):
         M.set_option("x_ring", ring)
         M.set_option("use_graph", graph)
-        assert M.get_option("x_ring") == ring
+        assert M.get_option("x_ring") == (ring if ring > 0 else 8)  # auto: 8 for a small image
         x = prob.x
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
