@@ -667,7 +667,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_c(CgArgs a, bool pro
     double sum[kRpt];
 #pragma unroll
     for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
-#pragma unroll(kW > 0 ? kW : 3)
+#pragma unroll kW > 0 ? kW : 3
     for (int j = 0; j < w; j++) {
         unsigned c[kRpt];
         ld_codes<kRpt, kNT>(cp + (size_t)j * kSliceRows, c);
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_v4(CgArgs a, bool pr
 #pragma unroll
     for (int q = 0; q < kPre; q++)
         if (q < nch) chunk(cpre[q]);
-#pragma unroll(kW > 0 ? (kW + kVC - 1) / kVC : 2)
+#pragma unroll kW > 0 ? (kW + kVC - 1) / kVC : 2
     for (int q = kPre; q < nch; q++) {
         unsigned cw[kRpt];
         ld_chunk<kRpt, kNT>(cp + (size_t)q * (kSliceRows * kVC), cw);
@@ -1259,7 +1259,7 @@ __device__ __forceinline__ void lds_stream(const double* __restrict__ vp,
                                            double (&sum)[kRpt])
 {
     const int lrow = threadIdx.x * kRpt;
-#pragma unroll(kVal ? 4 : 3)
+#pragma unroll kVal ? 4 : 3
     for (int j = j0; j < wdt; j++) {
         unsigned c[kRpt];
         ld_idx<kRpt, kNT, kCode>(cp + (size_t)j * kSliceRows, c);
@@ -1595,7 +1595,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_pp(CgArgs a, bool pr
     double sum[kRpt];
 #pragma unroll
     for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
-#pragma unroll(kW > 0 ? kW : 3)
+#pragma unroll kW > 0 ? kW : 3
     for (int j = 0; j < wdt; j++) {
         const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
 #pragma unroll

@@ -66,7 +66,7 @@ public:
         if (write_file) {
             std::time_t now = std::time(nullptr);
             std::tm* t = std::localtime(&now);
-            char stamp[32];
+            char stamp[96];
             std::snprintf(stamp, sizeof stamp, "%04d_%02d_%02d__%02d_%02d_%02d", t->tm_year + 1900,
                           t->tm_mon + 1, t->tm_mday, t->tm_hour, t->tm_min, t->tm_sec);
             std::ofstream f("./" + name_ + "-" + version_ + "_" + stamp + ".yaml");
