@@ -78,6 +78,19 @@ def test_group_kernel_variants_bitwise(hp, gpu):
         if ref is None:
             ref = got
         assert got == ref, (v, fold, fuse, defer, ovl)
+    # several slices per update workgroup (r.r folded or not) and the x ring length
+    for v, um, ring, fold in ((8200, 4, 5, 1), (8226, 8, 16, 3), (8500, 2, -1, 2), (8200, 1, 32, 0)):
+        for M in Ms:
+            M.set_option("spmv_variant", v)
+            M.set_option("fuse_p", 1)
+            M.set_option("overlap", 1)
+            M.set_option("x_defer", 1)
+            M.set_option("update_slices", um)
+            M.set_option("x_ring", ring)
+            M.set_option("fold", fold)
+        niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
+        got = (niters, normr, Ms[0].last_trace().tobytes(), b"".join(x.tobytes() for x in xs))
+        assert got == ref, (v, um, ring, fold)
     assert Ms[0].get_option("lds_doubles") > 0
 
 
