@@ -100,6 +100,8 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=15.0):
 def matrix_format(v):
     """Matrix image a SpMV variant streams (hpccg_solver.cpp slot_bytes) and
     its bytes per stored slot."""
+    if 8700 <= v < 8900:
+        return "SELL-512-A (8 B value per offset-aligned slot, holes 0.0; x read at per-slice offsets)", 8.0
     if v >= 8000:
         return "SELL-512-P (8 B value per slot + 1-byte row-pattern id per row)", 8.0
     if v >= 7000:
@@ -115,9 +117,21 @@ def matrix_format(v):
     return "SELL-512 (8 B value + int32 column)", 12.0
 
 
-def pmc_traffic(tag, fused_p):
+def spmv_kernel_family(v):
+    """Kernel template a SpMV variant launches (hpccg_kernels.hip launch_cg_spmv)."""
+    if 8700 <= v < 8900:
+        return "k_spmv_pa"
+    if 8500 <= v < 8700:
+        return "k_spmv_pp"
+    if 8000 <= v < 8500:
+        return "k_spmv_lp"
+    return None
+
+
+def pmc_traffic(tag, fused_p, variant):
     """HBM bytes per SpMV launch from the committed rocprofv3 PMC summary of
     the same kernel configuration (profiles/pmc_<tag>.json), else None."""
+    import re
     path = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
     if not os.path.exists(path):
         return None
@@ -125,6 +139,10 @@ def pmc_traffic(tag, fused_p):
         d = json.load(f)
     if bool(d.get("fuse_p", False)) != bool(fused_p):
         return None
+    fam = spmv_kernel_family(variant)
+    m = re.search(r"(k_spmv\w*)<", d.get("kernel", ""))
+    if fam is not None and (m is None or m.group(1) != fam):
+        return None  # the summary measured another kernel
     return d.get("spmv_hbm_bytes_per_launch")
 
 
@@ -354,7 +372,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(f"spmv_{args.stencil}pt_{n}", fused_p),
+                "traffic": pmc_traffic(f"spmv_{args.stencil}pt_{n}", fused_p,
+                                       M.get_option("spmv_variant")),
                 "kernel": "SpMV variant %d, %s + p.Ap%s" % (M.get_option("spmv_variant"),
                                                            matrix_format(M.get_option("spmv_variant"))[0],
                                                            " + p = r + beta p" if fused_p else ""),

@@ -85,6 +85,9 @@ struct CgArgs {
     const int* pbase;             // SELL-512-P: per slice, first entry of its pattern table
     const int* ptab_g;            // SELL-512-P: pattern tables, column - row per slot (kPatPad = padding)
     const int* ptab_l;            // SELL-512-P: pattern tables, LDS position - lane per slot
+    const double* aval;           // SELL-512-A: values in offset-aligned slots (holes 0.0)
+    const int* aoff;              // SELL-512-A: per slice, kAMax offsets (column - row), ascending
+    const unsigned int* abase;    // SELL-512-A: [nslices + 1] first slot row of each slice
     int pat_max;                  // SELL-512-P: largest table (ints) over slices: dynamic LDS
     const int* win_ptr;    // [nslices + 1] into the window arrays
     const int* win_start;  // first local column of the window
@@ -165,6 +168,15 @@ void launch_build_p(const unsigned int* slice_base, int nslices, const unsigned 
 void launch_fill_p(const unsigned int* slice_base, int nslices, const unsigned char* codes, const int* prep,
                    const int* pcount, const int* pbase, const int* cdict, const int* ldsc, int* tab_g, int* tab_l,
                    hipStream_t s);
+// SELL-512-A (offset-aligned slots) from the SELL-512-C codes: slot j of slice
+// s holds, for every row, the entry at the slice's j-th smallest offset (0.0
+// where the row has none). abase from the host prefix of ccount. aoff[s *
+// kAMax + j] = offset. ok[0] = 0 when a slice has more than kAMax offsets or a
+// row's entries are not in ascending offset order; maxabs = max |offset|.
+constexpr int kAMax = 32;
+void launch_build_a(const unsigned int* slice_base, int nslices, const unsigned char* codes, const double* vals,
+                    const int* cdict, const int* ccount, const unsigned int* abase, double* aval, int* aoff,
+                    int* ok, int* maxabs, hipStream_t s);
 // SELL-512-V4 regrouping of the V codes (vbase4 in chunks of 4 slots).
 void launch_interleave_v4(const unsigned int* slice_base, const unsigned int* vbase4, int nslices,
                           const unsigned char* codes, unsigned char* out, hipStream_t s);

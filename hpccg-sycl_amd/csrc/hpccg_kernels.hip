@@ -1126,6 +1126,60 @@ __global__ __launch_bounds__(256) void k_fill_p(const unsigned int* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// SELL-512-A: offset-aligned slots. Slot j of slice s holds, for every row,
+// its entry at the slice's j-th smallest (column - row) offset, 0.0 where the
+// row has none. A row's entries keep their order (required ascending), and a
+// hole adds 0 * x = +-0, which never changes a sum that starts at +0.0: the
+// row sums are the reference's bits. Every row of a slice then reads x at the
+// same offsets, so a thread's two rows take one 16-byte x load per slot and
+// the offsets are per-slice scalars. One block of 512 lanes per slice.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kSliceRows) void k_build_a(const unsigned int* __restrict__ slice_base, int nslices,
+                                                        const unsigned char* __restrict__ codes,
+                                                        const double* __restrict__ vals,
+                                                        const int* __restrict__ cdict, const int* __restrict__ ccount,
+                                                        const unsigned int* __restrict__ abase,
+                                                        double* __restrict__ aval, int* __restrict__ aoff, int* ok,
+                                                        int* maxabs)
+{
+    __shared__ int soff[kAMax];
+    __shared__ int srank[kAMax];
+    const int s = blockIdx.x;
+    if (s >= nslices) return;
+    const int K = ccount[s];
+    const int lane = threadIdx.x;
+    if (K > kAMax) {
+        if (lane == 0) ok[0] = 0;
+        return;
+    }
+    if (lane < K) soff[lane] = cdict[(size_t)s * kCodes + lane];
+    __syncthreads();
+    if (lane < K) {
+        const int o = soff[lane];
+        int r = 0;
+        for (int c = 0; c < K; c++) r += soff[c] < o ? 1 : 0;
+        srank[lane] = r;
+        aoff[(size_t)s * kAMax + r] = o;
+        atomicMax(maxabs, o < 0 ? -o : o);
+    } else if (lane < kAMax) {
+        aoff[(size_t)s * kAMax + lane] = 0;
+    }
+    __syncthreads();
+    const size_t e0 = (size_t)slice_base[s] * kSliceRows;
+    const int w = (int)(slice_base[s + 1] - slice_base[s]);
+    double* out = aval + (size_t)abase[s] * kSliceRows + lane;
+    int prev = -1;
+    for (int j = 0; j < w; j++) {
+        const unsigned c = codes[e0 + (size_t)j * kSliceRows + lane];
+        if (c == kCodePad) continue;
+        const int r = srank[c];
+        if (r <= prev) ok[0] = 0;  // entries out of offset order: no A image
+        prev = r;
+        out[(size_t)r * kSliceRows] = vals[e0 + (size_t)j * kSliceRows + lane];
+    }
+}
+
 template <int kRpt, int kW, int kMinW, bool kNT, bool kFuse>
 __global__ __launch_bounds__(kSliceRows / kRpt, kMinW) void k_spmv(CgArgs a, bool prologue)
 {
@@ -1625,6 +1679,105 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_pp(CgArgs a, bool pr
     for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
     st_rows<kRpt>(a.Ap, row, a.n, o);
     if (prologue) return;
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += pv.v[i] * o.v[i];
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
+}
+
+// kRpt consecutive doubles from an 8-byte aligned address: one 16-byte load
+// for two rows (global loads need only dword alignment on gfx950).
+template <int kRpt>
+__device__ __forceinline__ Rows<kRpt> ld_rows_u(const double* __restrict__ p)
+{
+    Rows<kRpt> o;
+    if constexpr (kRpt == 2) {
+        typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
+        const d2u t = *reinterpret_cast<const d2u*>(p);
+        o.v[0] = t.x;
+        o.v[1] = t.y;
+    } else {
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) o.v[i] = p[i];
+    }
+    return o;
+}
+
+// SELL-512-A SpMV: per slot one value load and one x load per thread at the
+// slice's offset for that slot. Holes read x inside the zeroed guard zones of
+// the p buffers (and of r) or at a real neighbour; their value is 0.0.
+// kW > 0: uniform width, slot loop fully unrolled. kFuse (single rank, never
+// the prologue): x = r + beta*p_{k-1} formed per load, k_p_update's exact
+// expression, so every row sum is unchanged; the thread's own rows of p_k
+// are stored for the update kernel and the next iteration.
+template <int kRpt, bool kNT, int kW = 0, bool kFuse = false>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_pa(CgArgs a, bool prologue)
+{
+    int k = 0;
+    double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
+    if (!prologue) {
+        k = a.kst[0];
+        if (kFuse) rr = cur_rr(a);
+        const bool run = cg_run(a, k, kFuse, rr);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = rr;
+            if (run)
+                stamp(a, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = spmv_slice(a);
+    if (s < 0) return;
+    const int wdt = kW > 0 ? kW : (int)(a.abase[s + 1] - a.abase[s]);
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    double* __restrict__ p = cur_p(a, k);
+    const double* __restrict__ xr = p - a.ghost_lo + row;  // x of column row + off at xr[off]
+    double beta = 0.0;
+    const double* __restrict__ rr_ = a.r - a.ghost_lo + row;
+    const double* __restrict__ py = rr_;
+    if constexpr (kFuse) {
+        beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
+        py = ((k == 1) ? a.r : cur_p(a, k - 1)) - a.ghost_lo + row;
+    }
+    const double* __restrict__ vp = a.aval + (size_t)a.abase[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
+    const int* __restrict__ off = a.aoff + (size_t)s * kAMax;
+    double sum[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+#pragma unroll kW > 0 ? kW : 4
+    for (int j = 0; j < wdt; j++) {
+        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+        Rows<kRpt> xv;
+        if constexpr (kFuse) {
+            const Rows<kRpt> rv = ld_rows_u<kRpt>(rr_ + off[j]);
+            const Rows<kRpt> yv = ld_rows_u<kRpt>(py + off[j]);
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) xv.v[i] = rv.v[i] + beta * yv.v[i];
+        } else {
+            xv = ld_rows_u<kRpt>(xr + off[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xv.v[i];
+    }
+    Rows<kRpt> o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+    st_rows<kRpt>(a.Ap, row, a.n, o);
+    if (prologue) return;
+    Rows<kRpt> pv;
+    if constexpr (kFuse) {
+        const Rows<kRpt> rv = ld<kRpt>(rr_ + a.ghost_lo);
+        const Rows<kRpt> yv = ld<kRpt>(py + a.ghost_lo);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + beta * yv.v[i];
+        st_rows<kRpt>(p, row, a.n, pv);
+    } else {
+        pv = ld<kRpt>(p + row);
+    }
     double d = 0.0;
 #pragma unroll
     for (int i = 0; i < kRpt; i++)
@@ -2193,6 +2346,15 @@ void launch_build_p(const unsigned int* slice_base, int nslices, const unsigned 
                        pcount, ok);
 }
 
+void launch_build_a(const unsigned int* slice_base, int nslices, const unsigned char* codes, const double* vals,
+                    const int* cdict, const int* ccount, const unsigned int* abase, double* aval, int* aoff,
+                    int* ok, int* maxabs, hipStream_t s)
+{
+    if (nslices <= 0) return;
+    hipLaunchKernelGGL(k_build_a, dim3(nslices), dim3(kSliceRows), 0, s, slice_base, nslices, codes, vals, cdict,
+                       ccount, abase, aval, aoff, ok, maxabs);
+}
+
 void launch_fill_p(const unsigned int* slice_base, int nslices, const unsigned char* codes, const int* prep,
                    const int* pcount, const int* pbase, const int* cdict, const int* ldsc, int* tab_g, int* tab_l,
                    hipStream_t s)
@@ -2244,6 +2406,9 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
 //   8507 / 8527 / 8607: plain SELL-512-P, uniform width 7 / 27 / 7 fully
 //   unrolled (8607 no nt)
 //   8500 / 8501 / 8600: SELL-512-P, plain gather (2 rows nt, 1 row nt, 2 rows)
+//   8700 / 8707 / 8727 / 8800 / 8807: SELL-512-A (offset-aligned slots, one
+//   16-byte x load per thread and slot), nt dynamic width / 7 / 27, no nt
+//   dynamic / 7
 //   9999: diagnostic matrix stream without the gather (not an SpMV)
 #define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
     do {                                                                                            \
@@ -2298,6 +2463,15 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
                                smem, s, a, prologue);                                              \
     } while (0)
 #define HPCCG_SPMV_LP(RPT, NT, PRE) HPCCG_SPMV_LPU(RPT, NT, PRE, 3)
+#define HPCCG_SPMV_PA(RPT, NT, W)                                                                  \
+    do {                                                                                           \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_pa<RPT, NT, W, true>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, \
+                               s, a, prologue);                                                    \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_pa<RPT, NT, W, false>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, \
+                               s, a, prologue);                                                    \
+    } while (0)
 #define HPCCG_SPMV_PPW(RPT, NT, W)                                                                 \
     do {                                                                                           \
         if (a.fuse_p && !prologue)                                                                 \
@@ -2321,6 +2495,7 @@ bool spmv_variant_ok(int v)
     case 7201: case 7202: case 7301: case 7302: case 7204:
     case 8000: case 8200: case 8208: case 8300: case 8201: case 8500: case 8501: case 8600:
     case 8216: case 8219: case 8226: case 8308: case 8316: case 8326: case 8507: case 8527: case 8607:
+    case 8700: case 8707: case 8727: case 8800: case 8807:
         return true;
     default:
         return false;
@@ -2394,6 +2569,11 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 8316: HPCCG_SPMV_LPU(2, false, 8, 6); break;
     case 8326: HPCCG_SPMV_LPU(2, false, 4, 6); break;
     case 8507: HPCCG_SPMV_PPW(2, true, 7); break;
+    case 8700: HPCCG_SPMV_PA(2, true, 0); break;
+    case 8707: HPCCG_SPMV_PA(2, true, 7); break;
+    case 8727: HPCCG_SPMV_PA(2, true, 27); break;
+    case 8800: HPCCG_SPMV_PA(2, false, 0); break;
+    case 8807: HPCCG_SPMV_PA(2, false, 7); break;
     case 8527: HPCCG_SPMV_PPW(2, true, 27); break;
     case 8607: HPCCG_SPMV_PPW(2, false, 7); break;
     case 8500: HPCCG_SPMV_PP(2, true); break;

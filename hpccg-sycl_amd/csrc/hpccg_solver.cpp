@@ -235,6 +235,13 @@ struct hpccg_hip_matrix {
     unsigned char* d_prow = nullptr;
     int *d_prep = nullptr, *d_pcount = nullptr, *d_pbase = nullptr, *d_ptab_g = nullptr, *d_ptab_l = nullptr;
     int pat_max = 0;  // largest pattern table over slices (ints)
+    // SELL-512-A (offset-aligned slots, holes 0.0; per-slice offset lists)
+    int has_a = 0;
+    int a_width = 0;  // slots per slice when uniform (every slice padded to the widest), else 0
+    double* d_aval = nullptr;
+    int* d_aoff = nullptr;
+    unsigned int* d_abase = nullptr;
+    long long p_guard = 0;  // zeroed doubles on each side of every p buffer (A kernels read holes there)
     int value_codes = 0;  // opt-in: let choose_variant pick SELL-512-V
     unsigned char* d_vcodes = nullptr;
     int *d_vdict = nullptr, *d_vldsc = nullptr, *d_vcount = nullptr;
@@ -256,6 +263,7 @@ struct hpccg_hip_matrix {
     int redund = 0;            // consumers complete the dots themselves, no finalize kernels (measured slower)
     int update_slices = 1;     // slices per loop-update workgroup (1, 2, 4, 8)
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
+    double* d_rbuf = nullptr;  // r with p_guard zeroed doubles on each side (fused SELL-512-A reads holes there)
     double* d_partial = nullptr;
     unsigned int* d_tickets = nullptr;
     int ntickets = 0;
@@ -290,7 +298,7 @@ int free_matrix(hpccg_hip_matrix* M)
     if (!M) return 0;
     (void)hipSetDevice(M->device);
     if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
-    void* ptrs[] = {M->d_slice_base, M->d_cols,    M->d_vals,  M->d_pbuf,  M->d_ahist,  M->d_r,
+    void* ptrs[] = {M->d_slice_base, M->d_cols,    M->d_vals,  M->d_pbuf,  M->d_ahist,  M->d_rbuf,
                     M->d_Ap,         M->d_x,       M->d_b,     M->d_partial,      M->d_scal,
                     M->d_tickets,
                     M->d_kst,        M->d_hist,    M->d_stamps, M->d_ddot_partial, M->d_gen_b,
@@ -298,7 +306,7 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_win_len,    M->d_win_off, M->d_send_idx, M->d_send_buf, M->d_ccodes, M->d_cdict, M->d_ldsc,
                     M->d_vcodes,     M->d_vdict,   M->d_vval,  M->d_vldsc, M->d_vbase4, M->d_vcodes4,
                     M->d_ccount,     M->d_vcount,  M->d_prow,  M->d_prep,  M->d_pcount, M->d_pbase,
-                    M->d_ptab_g,     M->d_ptab_l};
+                    M->d_ptab_g,     M->d_ptab_l,  M->d_aval,  M->d_aoff,  M->d_abase};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -637,11 +645,80 @@ int build_p_image(hpccg_hip_matrix* M)
     return 0;
 }
 
+int alloc_ring(hpccg_hip_matrix* M, int nbuf);
+int alloc_r(hpccg_hip_matrix* M);
+int x_ring_effective(const hpccg_hip_matrix* M);
+
+// SELL-512-A from the SELL-512-C codes (k_build_a), then the p ring again
+// with zeroed guard zones of max |offset| + a slice on each side, so a hole's
+// x load stays inside the buffer.
+int build_a_image(hpccg_hip_matrix* M)
+{
+    const int S = M->nslices;
+    if (!M->has_c || S < 1) return 0;
+    std::vector<int> cnt(S);
+    HIP_TRY(hipMemcpy(cnt.data(), M->d_ccount, sizeof(int) * S, hipMemcpyDeviceToHost));
+    std::vector<unsigned int> ab(S + 1, 0);
+    int wmax = 0;
+    for (int i = 0; i < S; i++) {
+        if (cnt[i] > kAMax) return 0;
+        ab[i + 1] = ab[i] + (unsigned)cnt[i];
+        wmax = std::max(wmax, cnt[i]);
+    }
+    // uniform slot count when padding every slice to the widest costs < 4 %
+    // (stencils: only the first and last planes' slices are narrower); the
+    // padding slots are holes at offset 0 (value 0.0, x of the row itself)
+    M->a_width = 0;
+    if ((double)wmax * S <= 1.04 * (double)ab[S]) {
+        for (int i = 0; i <= S; i++) ab[i] = (unsigned)i * (unsigned)wmax;
+        M->a_width = wmax;
+    }
+    HIP_TRY(hipMalloc(&M->d_abase, sizeof(unsigned int) * ab.size()));
+    HIP_TRY(hipMemcpy(M->d_abase, ab.data(), sizeof(unsigned int) * ab.size(), hipMemcpyHostToDevice));
+    const size_t na = std::max<size_t>(1, (size_t)ab[S] * kSliceRows);
+    HIP_TRY(hipMalloc(&M->d_aval, sizeof(double) * na));
+    HIP_TRY(hipMemsetAsync(M->d_aval, 0, sizeof(double) * na, M->stream));
+    HIP_TRY(hipMalloc(&M->d_aoff, sizeof(int) * (size_t)S * kAMax));
+    int* d_flags = nullptr;  // ok, maxabs
+    HIP_TRY(hipMalloc(&d_flags, sizeof(int) * 2));
+    const int init[2] = {1, 0};
+    HIP_TRY(hipMemcpyAsync(d_flags, init, sizeof init, hipMemcpyHostToDevice, M->stream));
+    launch_build_a(M->d_slice_base, S, M->d_ccodes, M->d_vals, M->d_cdict, M->d_ccount, M->d_abase, M->d_aval,
+                   M->d_aoff, d_flags, d_flags + 1, M->stream);
+    HIP_TRY(hipGetLastError());
+    int fl[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(fl, d_flags, sizeof fl, hipMemcpyDeviceToHost, M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    (void)hipFree(d_flags);
+    if (!fl[0]) {
+        for (void** q : {(void**)&M->d_aval, (void**)&M->d_aoff, (void**)&M->d_abase}) {
+            (void)hipFree(*q);
+            *q = nullptr;
+        }
+        return 0;
+    }
+    // A hole of row i at offset o reads column i + o; o is a real offset of
+    // some row of the same slice, so i + o lies within 511 of a valid column:
+    // two slices of zeros on each side cover every hole, whatever max |o|.
+    const long long guard = 2 * kSliceRows;
+    if (guard > M->p_guard) {
+        M->p_guard = guard;
+        const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
+        const size_t ghi_pad = ((size_t)M->ghost_hi + 2 + kSliceRows - 1) / kSliceRows * kSliceRows;
+        M->pstride = (long long)(M->p_guard + glo_pad + M->npad + ghi_pad + M->p_guard);
+        if (M->d_pbuf) TRY(alloc_ring(M, std::max(M->ring_alloc, x_ring_effective(M))));
+        if (M->d_rbuf) TRY(alloc_r(M));
+    }
+    M->has_a = 1;
+    return 0;
+}
+
 int build_c_image(hpccg_hip_matrix* M)
 {
     TRY(build_code_image(M, false, &M->d_ccodes, &M->d_cdict, nullptr, &M->d_ldsc, &M->d_ccount, &M->has_c,
                          &M->has_c_lds));
     TRY(build_p_image(M));
+    TRY(build_a_image(M));
     TRY(build_code_image(M, true, &M->d_vcodes, &M->d_vdict, &M->d_vval, &M->d_vldsc, &M->d_vcount, &M->has_v,
                          &M->has_v_lds));
     if (!M->has_v || M->nslices < 1) return 0;
@@ -685,8 +762,26 @@ int alloc_ring(hpccg_hip_matrix* M, int nbuf)
     }
     if (M->d_pbuf) (void)hipFree(M->d_pbuf);
     M->d_pbuf = buf;
-    M->d_p = M->d_pbuf + glo_pad;
+    M->d_p = M->d_pbuf + M->p_guard + glo_pad;
     M->ring_alloc = nbuf;
+    return 0;
+}
+
+// r = [p_guard zeros | npad rows | p_guard zeros]; only rows < n are ever
+// written. Reallocated (zeroed) when the guard grows: r is recomputed by every
+// solve's prologue.
+int alloc_r(hpccg_hip_matrix* M)
+{
+    const size_t total = M->npad + 2 * (size_t)M->p_guard;
+    double* buf = nullptr;
+    HIP_TRY(hipMalloc(&buf, sizeof(double) * total));
+    if (hipMemset(buf, 0, sizeof(double) * total) != hipSuccess) {
+        (void)hipFree(buf);
+        return set_err(HPCCG_HIP_EHIP, "hipMemset of r failed");
+    }
+    if (M->d_rbuf) (void)hipFree(M->d_rbuf);
+    M->d_rbuf = buf;
+    M->d_r = buf + M->p_guard;
     return 0;
 }
 
@@ -697,9 +792,10 @@ int alloc_workspace(hpccg_hip_matrix* M)
     // p = [ghost_lo | n | ghost_hi]; local rows start 512-row aligned
     const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
     const size_t ghi_pad = ((size_t)M->ghost_hi + 2 + kSliceRows - 1) / kSliceRows * kSliceRows;
-    M->pstride = (long long)(glo_pad + M->npad + ghi_pad);
+    M->pstride = (long long)(M->p_guard + glo_pad + M->npad + ghi_pad + M->p_guard);
     TRY(alloc_ring(M, x_ring_effective(M)));
-    double** vecs[] = {&M->d_r, &M->d_Ap, &M->d_x, &M->d_b};
+    TRY(alloc_r(M));
+    double** vecs[] = {&M->d_Ap, &M->d_x, &M->d_b};
     for (double** v : vecs) {
         HIP_TRY(hipMalloc(v, sizeof(double) * M->npad));
         HIP_TRY(hipMemset(*v, 0, sizeof(double) * M->npad));
@@ -751,8 +847,18 @@ const char* variant_unavailable(const hpccg_hip_matrix* M, int v)
     if (v >= 5000 && v < 6000 && !M->has_v_lds) return "the SELL-512-V LDS image";
     if (v >= 6000 && v < 8000 && !M->has_v) return "the SELL-512-V image";
     if (v >= 8000 && v < 8500 && !M->has_p_lds) return "the SELL-512-P LDS image";
-    if (v >= 8500 && v < 9000 && !M->has_p) return "the SELL-512-P image";
+    if (v >= 8500 && v < 8700 && !M->has_p) return "the SELL-512-P image";
+    if (v >= 8700 && v < 8900 && !M->has_a) return "the SELL-512-A image";
     return nullptr;
+}
+
+// Fixed-width variants (xx07 / xx27, 9999 = 27) unroll the slot loop: every
+// slice must have exactly that many slots (SELL-512-A: that many offsets).
+bool fixed_width_ok(const hpccg_hip_matrix* M, int v)
+{
+    const int w = v == 9999 ? 27 : v % 100;
+    if (v >= 8700 && v < 8900) return M->has_a && M->a_width == w;
+    return M->uniform && M->width == w;
 }
 
 int choose_variant(const hpccg_hip_matrix* M)
@@ -775,6 +881,17 @@ int choose_variant(const hpccg_hip_matrix* M)
     // 100^3 53.4 vs 58.2 us (8300), 7-pt 256^3 252 vs 277 us (8500 vs 3000).
     // Non-temporal value loads once the image outgrows the 256 MB Infinity Cache.
     const bool big_p = (double)M->nslots * 8.0 > 256e6;
+    // SELL-512-A (values in offset-aligned slots, x read directly at the
+    // slice's offsets, p = r + beta*p_{k-1} formed per load on one rank)
+    // everywhere except the 27-pt images beyond the Infinity Cache, where the
+    // LDS windows compute p once per staged entry: 100^3 SpMV 49.7 us and
+    // no k_p_update vs 53.0 (14789 vs 14113 it/s); 7-pt 256^3 2397 vs 2319
+    // it/s (8707 fused); 200^3 fused 423 us, separate p update 365 + 30 us vs
+    // 381 us (8226).
+    if (M->has_a && !(lds && big_p && M->has_p_lds)) {
+        if (!big_p) return 8800;
+        return M->a_width == 7 ? 8707 : 8700;
+    }
     if (lds && M->has_p_lds) return big_p ? 8226 : 8300;
     if (!lds && M->has_p) {
         if (M->uniform && M->width == 7 && big_p) return 8507;  // 7-pt 256^3: 248 vs 253 us
@@ -795,6 +912,7 @@ double slot_bytes(const hpccg_hip_matrix* M)
     if (v >= 7000 && v < 8000) return (double)M->nslots4 / std::max<long long>(1, M->nslots);
     if (variant_is_v(v)) return 1.0;
     if ((v >= 3000 && v < 5000)) return 9.0;
+    if (v >= 8700 && v < 8900) return 8.0;
     if (v >= 8000 && v < 9000) return 8.0 + (double)M->nslices * kSliceRows / std::max<long long>(1, M->nslots);
     if (v >= 2000 && v < 3000) return 10.0;
     return 12.0;
@@ -821,8 +939,9 @@ bool fuse_p_effective(const hpccg_hip_matrix* M)
     if (M->spmv_variant == 9999) return false;
     const int v = M->spmv_variant;
     const bool lds = (v >= 2000 && v < 3000) || (v >= 4000 && v < 6000) || (v >= 8000 && v < 8500);
+    const bool aligned = v >= 8700 && v < 8900;  // SELL-512-A: x = r + beta*p per coalesced load
     if (M->nranks != 1 && !lds) return false;
-    if (M->fuse_p < 0) return lds;
+    if (M->fuse_p < 0) return lds || aligned;
     return M->fuse_p != 0;
 }
 
@@ -914,6 +1033,9 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.pbase = M->d_pbase;
     a.ptab_g = M->d_ptab_g;
     a.ptab_l = M->d_ptab_l;
+    a.aval = M->d_aval;
+    a.aoff = M->d_aoff;
+    a.abase = M->d_abase;
     a.pat_max = std::max(1, M->pat_max);
     a.win_ptr = M->d_win_ptr;
     a.win_start = M->d_win_start;
@@ -2221,7 +2343,7 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         const int w = v % 100;  // 27 / 7 for the fixed-width variants
         if (!spmv_variant_ok(v) || v == 9999)
             return set_err(HPCCG_HIP_EINVAL, "unknown spmv variant %lld", value);
-        if ((w == 27 || w == 7) && !(M->uniform && M->width == w))
+        if ((w == 27 || w == 7) && !fixed_width_ok(M, v))
             return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform width-%d SELL image", v, w);
         if (const char* why = variant_unavailable(M, v))
             return set_err(HPCCG_HIP_EINVAL, "variant %d needs %s (not built)", v, why);
@@ -2276,7 +2398,7 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_
     if (!spmv_variant_ok(variant)) return set_err(HPCCG_HIP_EINVAL, "unknown variant %d", variant);
     if (const char* why = variant_unavailable(M, variant))
         return set_err(HPCCG_HIP_EINVAL, "variant %d needs %s", variant, why);
-    if ((w == 27 || w == 7 || variant == 9999) && !(M->uniform && M->width == (variant == 9999 ? 27 : w)))
+    if ((w == 27 || w == 7 || variant == 9999) && !fixed_width_ok(M, variant))
         return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform SELL image of that width", variant);
     HIP_TRY(hipSetDevice(M->device));
     TRY(ensure_hist(M, 2));

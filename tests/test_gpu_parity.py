@@ -57,7 +57,7 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
                                      4000, 4200, 4300, 3027, 5000, 5100, 5200, 5208, 5300, 5308,
                                      5401, 5404, 5204, 6000, 6100, 6104, 6001, 7001, 7101, 7002,
                                      7102, 7027, 7127, 7201, 7202, 7301, 7302, 7204, 8000, 8200,
-                                     8208, 8300, 8201, 8500, 8501, 8600])
+                                     8208, 8300, 8201, 8500, 8501, 8600, 8700, 8727, 8800])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
@@ -111,7 +111,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # and the LDS kernels (same rows per thread), fused or not, give the same bits
     for v, fuse in itertools.product((2000, 2100, 2200, 2308, 3000, 3100, 4200, 4300, 5200, 5300, 6000, 6100,
-                                      7001, 7102, 8000, 8200, 8300, 8500, 8600), (0, 1)):
+                                      7001, 7102, 8000, 8200, 8300, 8500, 8600, 8700, 8800), (0, 1)):
         M.set_option("spmv_variant", v)
         M.set_option("fuse_p", fuse)
         M.set_option("redund", 1 - fuse)
@@ -567,7 +567,7 @@ def test_value_codes_opt_in_bitwise(hp, gpu, dims, s7):
     the generated stencil picks a SELL-512-V kernel and the solve gives the
     same bits as the default kernel."""
     M = hp.Matrix.generate(*dims, use_7pt=s7)
-    assert M.get_option("value_codes") == 0 and M.get_option("spmv_variant") >= 8000  # SELL-512-P
+    assert M.get_option("value_codes") == 0 and M.get_option("spmv_variant") >= 8000  # SELL-512-P / -A
     assert M.get_option("value_codes_available") == 1
     b, _, _ = M.vectors()
     import torch
@@ -581,7 +581,7 @@ def test_value_codes_opt_in_bitwise(hp, gpu, dims, s7):
     assert outs[0] == outs[1] == outs[2]
 
 
-def _random_patterns(n, seed, noffs=10, band=None):
+def _random_patterns(n, seed, noffs=10, band=None, diag_first=True):
     """Symmetric matrix whose rows each keep a random subset of `noffs`
     offsets: few distinct offsets per slice (SELL-512-C fits), hundreds of
     distinct row patterns per 512-row slice."""
@@ -596,9 +596,9 @@ def _random_patterns(n, seed, noffs=10, band=None):
     rp = [0]
     cols, vals = [], []
     for i in range(n):
-        row = [i] + sorted(nb[i])
+        row = [i] + sorted(nb[i]) if diag_first else sorted(nb[i] | {i})
         cols += row
-        vals += [2.0 + len(row)] + [-1.0] * (len(row) - 1)
+        vals += [2.0 + len(row) if c == i else -1.0 for c in row]
         rp.append(len(cols))
     return np.array(rp, np.int64), np.array(cols, np.int32), np.array(vals, np.float64)
 
@@ -610,7 +610,7 @@ def test_sell_p_fallback_for_many_patterns(hp, gpu):
     n = 3000
     rp, cols, vals = _random_patterns(n, 7)
     M = hp.Matrix.from_csr(rp, cols, vals)
-    assert 3000 <= M.get_option("spmv_variant") < 5000
+    assert 3000 <= M.get_option("spmv_variant") < 5000  # diagonal first: no SELL-512-A either
     for v in (8200, 8500):
         with pytest.raises(hp.HPCCGError, match="SELL-512-P"):
             M.set_option("spmv_variant", v)
@@ -632,3 +632,31 @@ def test_sell_p_few_patterns_irregular(hp, gpu):
     A = oracle.CSR(rp, cols, vals, np.zeros(n), b, np.zeros(n))
     ref = oracle.hpccg(A, max_iter=40)
     assert check_trace(np.frombuffer(out[1000][2]), ref["trace"], RTRANS_RTOL_1GPU) >= 5
+
+
+def test_sell_a_holes_fused_and_refused(hp, gpu):
+    """SELL-512-A stores, per slice, one slot per distinct (column - row)
+    offset in ascending order, 0.0 where a row has no entry. Rows with random
+    offset subsets (many holes, x read past both ends of the vector for the
+    first and last slices) give the SELL-512 bits with the p update separate
+    or formed per load; a matrix whose rows are not in ascending column order
+    (diagonal first) gets no A image, since its sums would round in another
+    order."""
+    n = 2600  # 5 full slices + a ragged one
+    rp, cols, vals = _random_patterns(n, 5, noffs=10, diag_first=False)
+    M = hp.Matrix.from_csr(rp, cols, vals)
+    b = 1.0 + (np.arange(n) % 3)
+    out = {}
+    for v, fuse in ((1000, 0), (8700, 0), (8700, 1), (8800, 0), (8800, 1)):
+        M.set_option("spmv_variant", v)
+        M.set_option("fuse_p", fuse)
+        assert M.get_option("fuse_p") == fuse
+        x = np.zeros(n)
+        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=70)
+        out[(v, fuse)] = (it, nr, M.last_trace().tobytes(), x.tobytes())
+    assert all(o == out[(1000, 0)] for o in out.values())
+    rp, cols, vals = _banded(1500, lambda i, j: -1.0)
+    M = hp.Matrix.from_csr(rp, cols, vals)
+    assert not 8700 <= M.get_option("spmv_variant") < 8900
+    with pytest.raises(hp.HPCCGError, match="SELL-512-A"):
+        M.set_option("spmv_variant", 8700)
