@@ -88,6 +88,10 @@ struct CgArgs {
     const double* aval;           // SELL-512-A: values in offset-aligned slots (holes 0.0)
     const int* aoff;              // SELL-512-A: per slice, kAMax offsets (column - row), ascending
     const unsigned int* abase;    // SELL-512-A: [nslices + 1] first slot row of each slice
+    const int* alds;              // SELL-512-A LDS: per slice, kAMax LDS positions (minus the lane's row)
+    const int* awin;              // SELL-512-A LDS: per slice, kAWin windows (first row - slice row, length, LDS base)
+    const int* awn;               // SELL-512-A LDS: windows per slice
+    int alds_doubles;             // SELL-512-A LDS: dynamic LDS per block (largest window total)
     int pat_max;                  // SELL-512-P: largest table (ints) over slices: dynamic LDS
     const int* win_ptr;    // [nslices + 1] into the window arrays
     const int* win_start;  // first local column of the window
@@ -174,6 +178,12 @@ void launch_fill_p(const unsigned int* slice_base, int nslices, const unsigned c
 // kAMax + j] = offset. ok[0] = 0 when a slice has more than kAMax offsets or a
 // row's entries are not in ascending offset order; maxabs = max |offset|.
 constexpr int kAMax = 32;
+// SELL-512-A LDS windows: a slice's offsets cut where two neighbours are more
+// than a slice apart; each window stages every row of the slice at every
+// offset of its range (holes included), at most kAWin windows and kALdsMax
+// doubles per slice.
+constexpr int kAWin = 8;
+constexpr int kALdsMax = 8192;
 void launch_build_a(const unsigned int* slice_base, int nslices, const unsigned char* codes, const double* vals,
                     const int* cdict, const int* ccount, const unsigned int* abase, double* aval, int* aoff,
                     int* ok, int* maxabs, hipStream_t s);

@@ -1786,6 +1786,121 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_pa(CgArgs a, bool pr
     complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
 }
 
+// SELL-512-A with x from LDS windows: the windows of the slice (one per
+// z-plane for the 27-pt stencil, holes included) are staged first, with
+// kFuse p_k = r + beta*p_{k-1} computed per staged own row (k_p_update's
+// exact expression; ghost rows come from the halo as in k_spmv_lp). Slot j
+// then reads xs[lane row + alds[j]]: one per-slice scalar per slot, no index
+// or pattern stream, no table lookup. kPre value slots are loaded before the
+// staging barrier. kW > 0: uniform width, slot loop fully unrolled.
+template <int kRpt, bool kNT, bool kFuse, int kPre, int kW = 0>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_la(CgArgs a, bool prologue)
+{
+    extern __shared__ __attribute__((aligned(16))) double xs[];
+    int k = 0;
+    double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
+    if (!prologue) {
+        k = a.kst[0];
+        if (kFuse) rr = cur_rr(a);
+        const bool run = cg_run(a, k, kFuse, rr);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = rr;
+            if (run)
+                stamp(a, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    const int s = spmv_slice(a);
+    if (s < 0) return;
+    double* __restrict__ p = cur_p(a, k);
+    const int wdt = kW > 0 ? kW : (int)(a.abase[s + 1] - a.abase[s]);
+    const double* __restrict__ vp = a.aval + (size_t)a.abase[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
+    const bool nt = kNT && (xcd_slice(a.sgrid) % (a.sgrid / kNumXcd)) >= a.nt_split;
+    constexpr int kP = kPre > 0 ? kPre : 1;
+    Rows<kRpt> vpre[kP];
+#pragma unroll
+    for (int j = 0; j < kPre; j++)
+        if (j < wdt)
+            vpre[j] = nt ? ld_m<kRpt, true>(vp + (size_t)j * kSliceRows) : ld_m<kRpt, false>(vp + (size_t)j * kSliceRows);
+    double beta = 0.0;
+    const double* __restrict__ pold = a.r;
+    if constexpr (kFuse) {
+        beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
+        pold = (k == 1) ? a.r : cur_p(a, k - 1);
+    }
+    const int srow = s * kSliceRows;
+    {
+        const int nw = a.awn[s];
+        const int* __restrict__ win = a.awin + (size_t)s * kAWin * 3;
+        for (int w = 0; w < nw; w++) {
+            // offsets are in the [ghost_lo | n | ghost_hi] column numbering
+            const int st0 = srow + win[3 * w] - a.ghost_lo, len = win[3 * w + 1], base = win[3 * w + 2];
+            for (int i = threadIdx.x; i < len; i += kSliceRows / kRpt) {
+                const int l = st0 + i;  // local row (< 0 / >= n: ghosts, guard or padding zeros)
+                if constexpr (kFuse)
+                    xs[base + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + beta * pold[l] : p[l];
+                else
+                    xs[base + i] = p[l];
+            }
+        }
+    }
+    __syncthreads();
+    const int* __restrict__ cl = a.alds + (size_t)s * kAMax;
+    const int lrow = threadIdx.x * kRpt;
+    double sum[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < kPre; j++) {
+        if (j < wdt) {
+            const int c = lrow + cl[j];
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + vpre[j].v[i] * xs[c + i];
+        }
+    }
+    if (nt) {
+#pragma unroll kW > 0 ? kW : 6
+        for (int j = kPre; j < wdt; j++) {
+            const Rows<kRpt> v = ld_m<kRpt, true>(vp + (size_t)j * kSliceRows);
+            const int c = lrow + cl[j];
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xs[c + i];
+        }
+    } else {
+#pragma unroll kW > 0 ? kW : 6
+        for (int j = kPre; j < wdt; j++) {
+            const Rows<kRpt> v = ld_m<kRpt, false>(vp + (size_t)j * kSliceRows);
+            const int c = lrow + cl[j];
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xs[c + i];
+        }
+    }
+    const int row = srow + lrow;
+    Rows<kRpt> o;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+    st_rows<kRpt>(a.Ap, row, a.n, o);
+    if (prologue) return;
+    Rows<kRpt> pv;
+    if constexpr (kFuse) {
+        const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+        const Rows<kRpt> yv = ld<kRpt>(pold + row);
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + beta * yv.v[i];
+        st_rows<kRpt>(p, row, a.n, pv);
+    } else {
+        pv = ld<kRpt>(p + row);
+    }
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += pv.v[i] * o.v[i];
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
+}
+
 // Plain SpMV on arbitrary x (kernel-level C ABI): same body, no dot.
 template <int kRpt>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_plain(CgArgs a, const double* xext,
@@ -2409,6 +2524,9 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
 //   8700 / 8707 / 8727 / 8800 / 8807: SELL-512-A (offset-aligned slots, one
 //   16-byte x load per thread and slot), nt dynamic width / 7 / 27, no nt
 //   dynamic / 7
+//   8900 / 8902 / 8910 / 8927 / 8947: SELL-512-A with LDS windows, nt prefetch
+//   4 / nt prefetch 2 / no nt prefetch 4 / nt prefetch 4 width 27 unrolled /
+//   nt no prefetch width 27
 //   9999: diagnostic matrix stream without the gather (not an SpMV)
 #define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
     do {                                                                                            \
@@ -2472,6 +2590,16 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
             hipLaunchKernelGGL((k_spmv_pa<RPT, NT, W, false>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, \
                                s, a, prologue);                                                    \
     } while (0)
+#define HPCCG_SPMV_LA(RPT, NT, PRE, W)                                                             \
+    do {                                                                                           \
+        const size_t smem = (size_t)a.alds_doubles * sizeof(double);                               \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_la<RPT, NT, true, PRE, W>), dim3(a.sgrid), dim3(kSliceRows / RPT), smem, \
+                               s, a, prologue);                                                    \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_la<RPT, NT, false, PRE, W>), dim3(a.sgrid), dim3(kSliceRows / RPT), \
+                               smem, s, a, prologue);                                              \
+    } while (0)
 #define HPCCG_SPMV_PPW(RPT, NT, W)                                                                 \
     do {                                                                                           \
         if (a.fuse_p && !prologue)                                                                 \
@@ -2496,6 +2624,7 @@ bool spmv_variant_ok(int v)
     case 8000: case 8200: case 8208: case 8300: case 8201: case 8500: case 8501: case 8600:
     case 8216: case 8219: case 8226: case 8308: case 8316: case 8326: case 8507: case 8527: case 8607:
     case 8700: case 8707: case 8727: case 8800: case 8807:
+    case 8900: case 8927: case 8910: case 8902: case 8947:
         return true;
     default:
         return false;
@@ -2570,6 +2699,11 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 8326: HPCCG_SPMV_LPU(2, false, 4, 6); break;
     case 8507: HPCCG_SPMV_PPW(2, true, 7); break;
     case 8700: HPCCG_SPMV_PA(2, true, 0); break;
+    case 8900: HPCCG_SPMV_LA(2, true, 4, 0); break;
+    case 8902: HPCCG_SPMV_LA(2, true, 2, 0); break;
+    case 8910: HPCCG_SPMV_LA(2, false, 4, 0); break;
+    case 8927: HPCCG_SPMV_LA(2, true, 4, 27); break;
+    case 8947: HPCCG_SPMV_LA(2, true, 0, 27); break;
     case 8707: HPCCG_SPMV_PA(2, true, 7); break;
     case 8727: HPCCG_SPMV_PA(2, true, 27); break;
     case 8800: HPCCG_SPMV_PA(2, false, 0); break;

@@ -238,6 +238,9 @@ struct hpccg_hip_matrix {
     // SELL-512-A (offset-aligned slots, holes 0.0; per-slice offset lists)
     int has_a = 0;
     int a_width = 0;  // slots per slice when uniform (every slice padded to the widest), else 0
+    int has_a_lds = 0;  // SELL-512-A LDS windows (27-pt: one per plane, holes included)
+    int *d_alds = nullptr, *d_awin = nullptr, *d_awn = nullptr;
+    int alds_doubles = 0;
     double* d_aval = nullptr;
     int* d_aoff = nullptr;
     unsigned int* d_abase = nullptr;
@@ -306,7 +309,8 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_win_len,    M->d_win_off, M->d_send_idx, M->d_send_buf, M->d_ccodes, M->d_cdict, M->d_ldsc,
                     M->d_vcodes,     M->d_vdict,   M->d_vval,  M->d_vldsc, M->d_vbase4, M->d_vcodes4,
                     M->d_ccount,     M->d_vcount,  M->d_prow,  M->d_prep,  M->d_pcount, M->d_pbase,
-                    M->d_ptab_g,     M->d_ptab_l,  M->d_aval,  M->d_aoff,  M->d_abase};
+                    M->d_ptab_g,     M->d_ptab_l,  M->d_aval,  M->d_aoff,  M->d_abase,
+                    M->d_alds,       M->d_awin,    M->d_awn};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -649,6 +653,56 @@ int alloc_ring(hpccg_hip_matrix* M, int nbuf);
 int alloc_r(hpccg_hip_matrix* M);
 int x_ring_effective(const hpccg_hip_matrix* M);
 
+// SELL-512-A LDS windows (host, from the per-slice offsets): the ascending
+// offsets are cut where neighbours are more than a slice apart (staging the
+// gap would cost more than a second window); window [o_a, o_b] stages rows
+// s*512 + o_a .. s*512 + 511 + o_b, so every row of the slice finds every
+// offset of the range in it, holes included, and slot j reads LDS position
+// lane row + alds[j]. Padding slots (offset 0, value 0.0) read slot 0's.
+int build_a_windows(hpccg_hip_matrix* M, const std::vector<int>& cnt)
+{
+    const int S = M->nslices;
+    std::vector<int> off((size_t)S * kAMax);
+    HIP_TRY(hipMemcpy(off.data(), M->d_aoff, sizeof(int) * off.size(), hipMemcpyDeviceToHost));
+    std::vector<int> lds((size_t)S * kAMax, 0), win((size_t)S * kAWin * 3, 0), wn(S, 0);
+    int maxd = 0;
+    for (int s = 0; s < S; s++) {
+        const int K = cnt[s];
+        const int* o = &off[(size_t)s * kAMax];
+        int* w = &win[(size_t)s * kAWin * 3];
+        int nw = 0, base = 0;
+        if (K == 0) {  // empty rows only: one window of the slice's own rows
+            w[0] = 0, w[1] = kSliceRows, w[2] = 0;
+            nw = 1, base = kSliceRows;
+        }
+        for (int j = 0; j < K;) {
+            int e = j;
+            while (e + 1 < K && o[e + 1] - o[e] <= kSliceRows) e++;
+            if (nw == kAWin) return 0;
+            w[3 * nw] = o[j];
+            w[3 * nw + 1] = kSliceRows + o[e] - o[j];
+            w[3 * nw + 2] = base;
+            for (int q = j; q <= e; q++) lds[(size_t)s * kAMax + q] = base + o[q] - o[j];
+            base += kSliceRows + o[e] - o[j];
+            nw++;
+            j = e + 1;
+        }
+        if (base > kALdsMax) return 0;
+        for (int q = std::max(K, 1); q < kAMax; q++) lds[(size_t)s * kAMax + q] = lds[(size_t)s * kAMax];
+        wn[s] = nw;
+        maxd = std::max(maxd, base);
+    }
+    HIP_TRY(hipMalloc(&M->d_alds, sizeof(int) * lds.size()));
+    HIP_TRY(hipMalloc(&M->d_awin, sizeof(int) * win.size()));
+    HIP_TRY(hipMalloc(&M->d_awn, sizeof(int) * wn.size()));
+    HIP_TRY(hipMemcpy(M->d_alds, lds.data(), sizeof(int) * lds.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(M->d_awin, win.data(), sizeof(int) * win.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(M->d_awn, wn.data(), sizeof(int) * wn.size(), hipMemcpyHostToDevice));
+    M->alds_doubles = maxd;
+    M->has_a_lds = 1;
+    return 0;
+}
+
 // SELL-512-A from the SELL-512-C codes (k_build_a), then the p ring again
 // with zeroed guard zones of max |offset| + a slice on each side, so a hole's
 // x load stays inside the buffer.
@@ -710,7 +764,7 @@ int build_a_image(hpccg_hip_matrix* M)
         if (M->d_rbuf) TRY(alloc_r(M));
     }
     M->has_a = 1;
-    return 0;
+    return build_a_windows(M, cnt);
 }
 
 int build_c_image(hpccg_hip_matrix* M)
@@ -849,6 +903,7 @@ const char* variant_unavailable(const hpccg_hip_matrix* M, int v)
     if (v >= 8000 && v < 8500 && !M->has_p_lds) return "the SELL-512-P LDS image";
     if (v >= 8500 && v < 8700 && !M->has_p) return "the SELL-512-P image";
     if (v >= 8700 && v < 8900 && !M->has_a) return "the SELL-512-A image";
+    if (v >= 8900 && v < 9000 && !M->has_a_lds) return "the SELL-512-A LDS windows";
     return nullptr;
 }
 
@@ -857,7 +912,7 @@ const char* variant_unavailable(const hpccg_hip_matrix* M, int v)
 bool fixed_width_ok(const hpccg_hip_matrix* M, int v)
 {
     const int w = v == 9999 ? 27 : v % 100;
-    if (v >= 8700 && v < 8900) return M->has_a && M->a_width == w;
+    if (v >= 8700 && v < 9000) return M->has_a && M->a_width == w;
     return M->uniform && M->width == w;
 }
 
@@ -912,7 +967,7 @@ double slot_bytes(const hpccg_hip_matrix* M)
     if (v >= 7000 && v < 8000) return (double)M->nslots4 / std::max<long long>(1, M->nslots);
     if (variant_is_v(v)) return 1.0;
     if ((v >= 3000 && v < 5000)) return 9.0;
-    if (v >= 8700 && v < 8900) return 8.0;
+    if (v >= 8700 && v < 9000) return 8.0;
     if (v >= 8000 && v < 9000) return 8.0 + (double)M->nslices * kSliceRows / std::max<long long>(1, M->nslots);
     if (v >= 2000 && v < 3000) return 10.0;
     return 12.0;
@@ -938,7 +993,8 @@ bool fuse_p_effective(const hpccg_hip_matrix* M)
 {
     if (M->spmv_variant == 9999) return false;
     const int v = M->spmv_variant;
-    const bool lds = (v >= 2000 && v < 3000) || (v >= 4000 && v < 6000) || (v >= 8000 && v < 8500);
+    const bool lds = (v >= 2000 && v < 3000) || (v >= 4000 && v < 6000) || (v >= 8000 && v < 8500) ||
+                     (v >= 8900 && v < 9000);
     const bool aligned = v >= 8700 && v < 8900;  // SELL-512-A: x = r + beta*p per coalesced load
     if (M->nranks != 1 && !lds) return false;
     if (M->fuse_p < 0) return lds || aligned;
@@ -1036,6 +1092,10 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.aval = M->d_aval;
     a.aoff = M->d_aoff;
     a.abase = M->d_abase;
+    a.alds = M->d_alds;
+    a.awin = M->d_awin;
+    a.awn = M->d_awn;
+    a.alds_doubles = std::max(1, M->alds_doubles);
     a.pat_max = std::max(1, M->pat_max);
     a.win_ptr = M->d_win_ptr;
     a.win_start = M->d_win_start;
