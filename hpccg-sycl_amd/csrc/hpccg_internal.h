@@ -51,6 +51,7 @@ struct CgArgs {
     int redund;            // 1: no finalize kernels: consumers sum the producers' partials themselves
     int ugrid;             // k_update_g grid (groups rounded up to a multiple of kNumXcd)
     int um;                // slices per k_update workgroup (1: k_update, else k_update_m)
+    int uearly;            // um = 1: k_update_e (Ap and r loaded before the iteration test)
     int umgrid;            // k_update_m grid (slice blocks of um rounded up to a multiple of kNumXcd)
     int s0, sn0, s1, sn1;  // SpMV launch: slices [s0, s0 + sn0) then [s1, s1 + sn1)
     int sgrid;             // SpMV launch grid (sn0 + sn1 rounded up to a multiple of kNumXcd)

@@ -1495,11 +1495,29 @@ __device__ __forceinline__ void lp_stream(const double* __restrict__ vp, int j0,
 
 // Dynamic LDS: the windows (a.lds_doubles doubles), then the pattern table
 // (a.pat_max ints, the largest over slices).
-template <int kRpt, bool kNT, bool kFuse, int kPre, int kU = 3>
+// kEarly: the slice's pattern ids and first kPre value slots (they depend
+// only on blockIdx) are loaded before the iteration test.
+template <int kRpt, bool kNT, bool kFuse, int kPre, int kU = 3, bool kEarly = false>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lp(CgArgs a, bool prologue)
 {
     extern __shared__ __attribute__((aligned(16))) double xs[];
     int* const spat = reinterpret_cast<int*>(xs + a.lds_doubles);
+    constexpr int kP = kPre > 0 ? kPre : 1;
+    Rows<kRpt> vpre[kP];
+    int pid[kRpt];
+    const int s = spmv_slice(a);
+    const size_t base = s >= 0 ? (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt : 0;
+    const int wdt = s >= 0 ? (int)(a.slice_base[s + 1] - a.slice_base[s]) : 0;
+    const double* __restrict__ vp = a.vals + base;
+    const bool nt = kNT && (xcd_slice(a.sgrid) % (a.sgrid / kNumXcd)) >= a.nt_split;
+    auto load_early = [&]() {
+        ld_pids<kRpt>(a.prow + (size_t)s * kSliceRows + threadIdx.x * kRpt, pid);
+#pragma unroll
+        for (int j = 0; j < kPre; j++)
+            if (j < wdt)
+                vpre[j] = nt ? ld_m<kRpt, true>(vp + (size_t)j * kSliceRows) : ld_m<kRpt, false>(vp + (size_t)j * kSliceRows);
+    };
+    if (kEarly && s >= 0) load_early();
     int k = 0;
     double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
     if (!prologue) {
@@ -1515,21 +1533,10 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_lp(CgArgs a, bool pr
         }
         if (!run) return;
     }
-    const int s = spmv_slice(a);
     if (s < 0) return;
     double* __restrict__ p = cur_p(a, k);
     const double* __restrict__ xext = p - a.ghost_lo;
-    const size_t base = (size_t)a.slice_base[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
-    const int wdt = (int)(a.slice_base[s + 1] - a.slice_base[s]);
-    const double* __restrict__ vp = a.vals + base;
-    const bool nt = kNT && (xcd_slice(a.sgrid) % (a.sgrid / kNumXcd)) >= a.nt_split;
-    int pid[kRpt];
-    ld_pids<kRpt>(a.prow + (size_t)s * kSliceRows + threadIdx.x * kRpt, pid);
-    constexpr int kP = kPre > 0 ? kPre : 1;
-    Rows<kRpt> vpre[kP];
-#pragma unroll
-    for (int j = 0; j < kPre; j++)
-        if (j < wdt) vpre[j] = nt ? ld_m<kRpt, true>(vp + (size_t)j * kSliceRows) : ld_m<kRpt, false>(vp + (size_t)j * kSliceRows);
+    if (!kEarly) load_early();
     {
         const int np = a.pcount[s] * wdt;
         const int* __restrict__ tab = a.ptab_l + a.pbase[s];
@@ -1712,9 +1719,26 @@ __device__ __forceinline__ Rows<kRpt> ld_rows_u(const double* __restrict__ p)
 // the prologue): x = r + beta*p_{k-1} formed per load, k_p_update's exact
 // expression, so every row sum is unchanged; the thread's own rows of p_k
 // are stored for the update kernel and the next iteration.
-template <int kRpt, bool kNT, int kW = 0, bool kFuse = false>
+template <int kRpt, bool kNT, int kW = 0, bool kFuse = false, int kPre = 0>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_pa(CgArgs a, bool prologue)
 {
+    static_assert(kPre == 0 || (kW > 0 && kPre <= kW), "early loads need the uniform width");
+    // kPre > 0: the slice, its first kPre value slots and its offsets depend
+    // only on blockIdx, so they are loaded before the iteration count and
+    // r.r (two dependent scalar loads) decide whether the block runs
+    const int s = spmv_slice(a);
+    constexpr int kP = kPre > 0 ? kPre : 1;
+    Rows<kRpt> vpre[kP];
+    int offp[kPre > 0 ? kW : 1];
+    if constexpr (kPre > 0) {
+        if (s >= 0) {
+            const double* __restrict__ vp0 = a.aval + (size_t)s * kW * kSliceRows + (size_t)threadIdx.x * kRpt;
+#pragma unroll
+            for (int j = 0; j < kPre; j++) vpre[j] = ld_m<kRpt, kNT>(vp0 + (size_t)j * kSliceRows);
+#pragma unroll
+            for (int j = 0; j < kW; j++) offp[j] = a.aoff[(size_t)s * kAMax + j];
+        }
+    }
     int k = 0;
     double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
     if (!prologue) {
@@ -1730,7 +1754,6 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_pa(CgArgs a, bool pr
         }
         if (!run) return;
     }
-    const int s = spmv_slice(a);
     if (s < 0) return;
     const int wdt = kW > 0 ? kW : (int)(a.abase[s + 1] - a.abase[s]);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
@@ -1743,22 +1766,32 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_pa(CgArgs a, bool pr
         beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
         py = ((k == 1) ? a.r : cur_p(a, k - 1)) - a.ghost_lo + row;
     }
-    const double* __restrict__ vp = a.aval + (size_t)a.abase[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
+    // uniform width: slice s starts at slot row s * kW
+    const size_t vb = kW > 0 ? (size_t)s * kW : (size_t)a.abase[s];
+    const double* __restrict__ vp = a.aval + vb * kSliceRows + (size_t)threadIdx.x * kRpt;
     const int* __restrict__ off = a.aoff + (size_t)s * kAMax;
     double sum[kRpt];
 #pragma unroll
     for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
 #pragma unroll kW > 0 ? kW : 4
     for (int j = 0; j < wdt; j++) {
-        const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+        Rows<kRpt> v;
+        int oj;
+        if constexpr (kPre > 0) {
+            v = j < kPre ? vpre[j] : ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+            oj = offp[j];
+        } else {
+            v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+            oj = off[j];
+        }
         Rows<kRpt> xv;
         if constexpr (kFuse) {
-            const Rows<kRpt> rv = ld_rows_u<kRpt>(rr_ + off[j]);
-            const Rows<kRpt> yv = ld_rows_u<kRpt>(py + off[j]);
+            const Rows<kRpt> rv = ld_rows_u<kRpt>(rr_ + oj);
+            const Rows<kRpt> yv = ld_rows_u<kRpt>(py + oj);
 #pragma unroll
             for (int i = 0; i < kRpt; i++) xv.v[i] = rv.v[i] + beta * yv.v[i];
         } else {
-            xv = ld_rows_u<kRpt>(xr + off[j]);
+            xv = ld_rows_u<kRpt>(xr + oj);
         }
 #pragma unroll
         for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xv.v[i];
@@ -2094,6 +2127,55 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_update(CgArgs a)
     const double d = update_slice<kRpt, kPrologue>(a, s, threadIdx.x, k, alpha);
     const double bs = block_sum<kSliceRows / kRpt>(d);
     complete_dot<kSliceRows / kRpt>(a, s, bs, kRR, kPrologue ? 1 : k + 1);
+}
+
+// The loop update with the slice's Ap and r loaded before the iteration test
+// and alpha, which need two and three dependent scalar loads (a.uearly): the
+// same values and the same partial tree as k_update.
+template <int kRpt>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_update_e(CgArgs a)
+{
+    const int s = a.rev ? xcd_slice_rev(a.grid) : xcd_slice(a.grid);
+    const bool have = s < a.nslices;
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    Rows<kRpt> apv, rv;
+    if (have) {
+        apv = ld<kRpt>(a.Ap + row);
+        rv = ld<kRpt>(a.r + row);
+    }
+    const int k = a.kst[0];
+    const bool run = cg_run(a, k, false);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (run)
+            stamp(a, kStampUpdate);
+        else
+            mark_end(a);
+    }
+    if (!run || !have) return;
+    const double alpha = a.g[kRR] / a.g[kPAP];
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ahist[k] = alpha;
+    Rows<kRpt> rn;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
+    if (!a.xdefer) {
+        const Rows<kRpt> xv = ld<kRpt>(a.x + row);
+        const Rows<kRpt> pv = ld<kRpt>(cur_p(a, k) + row);
+        Rows<kRpt> xn;
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) xn.v[i] = xv.v[i] + alpha * pv.v[i];
+        st_rows<kRpt>(a.x, row, a.n, xn);
+    } else if (k % a.nring == 0) {
+        Rows<kRpt> xn = ld<kRpt>(a.x + row);
+        x_accumulate<kRpt>(a, row, k - a.nring + 1, k, k, alpha, xn);
+        st_rows<kRpt>(a.x, row, a.n, xn);
+    }
+    st_rows<kRpt>(a.r, row, a.n, rn);
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += rn.v[i] * rn.v[i];
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kRR, k + 1);
 }
 
 // The loop update over kM consecutive slices per workgroup (a.um = kM): the
@@ -2524,6 +2606,11 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
 //   8700 / 8707 / 8727 / 8800 / 8807: SELL-512-A (offset-aligned slots, one
 //   16-byte x load per thread and slot), nt dynamic width / 7 / 27, no nt
 //   dynamic / 7
+//   8236 / 8246 / 8336: 8226 (nt, prefetch 4 / 8) and 8326 (default policy)
+//   with the pattern ids and the prefetched slots loaded before the run test
+//   8717 / 8817: width 7 unrolled, all 7 value slots and the offsets loaded
+//   before the run test (nt / default policy); 8737 / 8757 / 8837 / 8857:
+//   width 27, 4 / 8 value slots early (nt, nt, default, default)
 //   8900 / 8902 / 8910 / 8927 / 8947: SELL-512-A with LDS windows, nt prefetch
 //   4 / nt prefetch 2 / no nt prefetch 4 / nt prefetch 4 width 27 unrolled /
 //   nt no prefetch width 27
@@ -2570,26 +2657,28 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
                                smem, s, a, prologue);                                              \
     } while (0)
 #define HPCCG_SPMV_LDS(RPT, NT, PRE) HPCCG_SPMV_LDSX(RPT, NT, PRE, 0)
-#define HPCCG_SPMV_LPU(RPT, NT, PRE, U)                                                            \
+#define HPCCG_SPMV_LPE(RPT, NT, PRE, U, E)                                                         \
     do {                                                                                           \
         const size_t smem = (size_t)a.lds_doubles * sizeof(double) + (size_t)a.pat_max * sizeof(int); \
         if (a.fuse_p && !prologue)                                                                 \
-            hipLaunchKernelGGL((k_spmv_lp<RPT, NT, true, PRE, U>), dim3(a.sgrid), dim3(kSliceRows / RPT), smem, \
+            hipLaunchKernelGGL((k_spmv_lp<RPT, NT, true, PRE, U, E>), dim3(a.sgrid), dim3(kSliceRows / RPT), smem, \
                                s, a, prologue);                                                    \
         else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_lp<RPT, NT, false, PRE, U>), dim3(a.sgrid), dim3(kSliceRows / RPT), \
+            hipLaunchKernelGGL((k_spmv_lp<RPT, NT, false, PRE, U, E>), dim3(a.sgrid), dim3(kSliceRows / RPT), \
                                smem, s, a, prologue);                                              \
     } while (0)
+#define HPCCG_SPMV_LPU(RPT, NT, PRE, U) HPCCG_SPMV_LPE(RPT, NT, PRE, U, false)
 #define HPCCG_SPMV_LP(RPT, NT, PRE) HPCCG_SPMV_LPU(RPT, NT, PRE, 3)
-#define HPCCG_SPMV_PA(RPT, NT, W)                                                                  \
+#define HPCCG_SPMV_PAP(RPT, NT, W, PRE)                                                            \
     do {                                                                                           \
         if (a.fuse_p && !prologue)                                                                 \
-            hipLaunchKernelGGL((k_spmv_pa<RPT, NT, W, true>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, \
+            hipLaunchKernelGGL((k_spmv_pa<RPT, NT, W, true, PRE>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, \
                                s, a, prologue);                                                    \
         else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_pa<RPT, NT, W, false>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, \
+            hipLaunchKernelGGL((k_spmv_pa<RPT, NT, W, false, PRE>), dim3(a.sgrid), dim3(kSliceRows / RPT), 0, \
                                s, a, prologue);                                                    \
     } while (0)
+#define HPCCG_SPMV_PA(RPT, NT, W) HPCCG_SPMV_PAP(RPT, NT, W, 0)
 #define HPCCG_SPMV_LA(RPT, NT, PRE, W)                                                             \
     do {                                                                                           \
         const size_t smem = (size_t)a.alds_doubles * sizeof(double);                               \
@@ -2625,6 +2714,8 @@ bool spmv_variant_ok(int v)
     case 8216: case 8219: case 8226: case 8308: case 8316: case 8326: case 8507: case 8527: case 8607:
     case 8700: case 8707: case 8727: case 8800: case 8807:
     case 8900: case 8927: case 8910: case 8902: case 8947:
+    case 8236: case 8246: case 8336:
+    case 8717: case 8737: case 8757: case 8837: case 8857: case 8817:
         return true;
     default:
         return false;
@@ -2699,6 +2790,15 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 8326: HPCCG_SPMV_LPU(2, false, 4, 6); break;
     case 8507: HPCCG_SPMV_PPW(2, true, 7); break;
     case 8700: HPCCG_SPMV_PA(2, true, 0); break;
+    case 8236: HPCCG_SPMV_LPE(2, true, 4, 6, true); break;
+    case 8246: HPCCG_SPMV_LPE(2, true, 8, 6, true); break;
+    case 8336: HPCCG_SPMV_LPE(2, false, 4, 6, true); break;
+    case 8717: HPCCG_SPMV_PAP(2, true, 7, 7); break;
+    case 8817: HPCCG_SPMV_PAP(2, false, 7, 7); break;
+    case 8737: HPCCG_SPMV_PAP(2, true, 27, 4); break;
+    case 8757: HPCCG_SPMV_PAP(2, true, 27, 8); break;
+    case 8837: HPCCG_SPMV_PAP(2, false, 27, 4); break;
+    case 8857: HPCCG_SPMV_PAP(2, false, 27, 8); break;
     case 8900: HPCCG_SPMV_LA(2, true, 4, 0); break;
     case 8902: HPCCG_SPMV_LA(2, true, 2, 0); break;
     case 8910: HPCCG_SPMV_LA(2, false, 4, 0); break;
@@ -2758,6 +2858,8 @@ void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)
         hipLaunchKernelGGL((k_update_m<kRpt, 4>), dim3(a.umgrid), dim3(kBlock), 0, s, a);
     else if (a.um == 8)
         hipLaunchKernelGGL((k_update_m<kRpt, 8>), dim3(a.umgrid), dim3(kBlock), 0, s, a);
+    else if (a.uearly)
+        hipLaunchKernelGGL(k_update_e<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
     else
         hipLaunchKernelGGL((k_update<kRpt, false>), dim3(a.grid), dim3(kBlock), 0, s, a);
 }

@@ -265,6 +265,7 @@ struct hpccg_hip_matrix {
     long long resident_mb = -1; // NT kernels: MB of leading slices on default-policy loads (-1 auto)
     int redund = 0;            // consumers complete the dots themselves, no finalize kernels (measured slower)
     int update_slices = 1;     // slices per loop-update workgroup (1, 2, 4, 8)
+    int update_early = 0;      // loop update loads Ap and r before the iteration test
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_rbuf = nullptr;  // r with p_guard zeroed doubles on each side (fused SELL-512-A reads holes there)
     double* d_partial = nullptr;
@@ -907,11 +908,25 @@ const char* variant_unavailable(const hpccg_hip_matrix* M, int v)
     return nullptr;
 }
 
-// Fixed-width variants (xx07 / xx27, 9999 = 27) unroll the slot loop: every
-// slice must have exactly that many slots (SELL-512-A: that many offsets).
+// Slots per slice a fixed-width variant unrolls (0: any width): xx07 / xx27,
+// 9999 = 27, and the SELL-512-A early-load variants.
+int required_width(int v)
+{
+    switch (v) {
+    case 8717: case 8817: return 7;
+    case 8737: case 8757: case 8837: case 8857: case 9999: return 27;
+    default: break;
+    }
+    const int w = v % 100;
+    return (w == 27 || w == 7) ? w : 0;
+}
+
+// Fixed-width variants unroll the slot loop: every slice must have exactly
+// that many slots (SELL-512-A: that many offsets).
 bool fixed_width_ok(const hpccg_hip_matrix* M, int v)
 {
-    const int w = v == 9999 ? 27 : v % 100;
+    const int w = required_width(v);
+    if (w == 0) return true;
     if (v >= 8700 && v < 9000) return M->has_a && M->a_width == w;
     return M->uniform && M->width == w;
 }
@@ -944,10 +959,14 @@ int choose_variant(const hpccg_hip_matrix* M)
     // it/s (8707 fused); 200^3 fused 423 us, separate p update 365 + 30 us vs
     // 381 us (8226).
     if (M->has_a && !(lds && big_p && M->has_p_lds)) {
-        if (!big_p) return 8800;
+        // width 27: 4 value slots and the offsets loaded before the run
+        // test, 100^3 SpMV 44.6 vs 49.3-50.1 us (15983 vs 14737-14901 it/s)
+        if (!big_p) return M->a_width == 27 ? 8837 : 8800;
         return M->a_width == 7 ? 8707 : 8700;
     }
-    if (lds && M->has_p_lds) return big_p ? 8226 : 8300;
+    // 8236 = 8226 with the pattern ids and the 4 prefetched value slots
+    // loaded before the iteration test: 200^3 2412-2416 vs 2385-2391 it/s
+    if (lds && M->has_p_lds) return big_p ? 8236 : 8300;
     if (!lds && M->has_p) {
         if (M->uniform && M->width == 7 && big_p) return 8507;  // 7-pt 256^3: 248 vs 253 us
         return big_p ? 8500 : 8600;
@@ -1060,6 +1079,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
         const int ng = (M->nslices + 63) / 64;
         a.ugrid = std::max(kNumXcd, (ng + kNumXcd - 1) / kNumXcd * kNumXcd);
         a.um = M->update_slices;
+        a.uearly = M->update_early ? 1 : 0;
         const int nb = (M->nslices + a.um - 1) / a.um;
         a.umgrid = std::max(kNumXcd, (nb + kNumXcd - 1) / kNumXcd * kNumXcd);
     }
@@ -2382,6 +2402,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->rev_update = (int)value;
     } else if (!std::strcmp(key, "redund")) {
         M->redund = (int)value;
+    } else if (!std::strcmp(key, "update_early")) {
+        M->update_early = value != 0;
     } else if (!std::strcmp(key, "update_slices")) {
         if (value != 1 && value != 2 && value != 4 && value != 8)
             return set_err(HPCCG_HIP_EINVAL, "update_slices must be 1, 2, 4 or 8");
@@ -2400,10 +2422,10 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->spmv_variant = choose_variant(M);
     } else if (!std::strcmp(key, "spmv_variant")) {
         const int v = (int)value;
-        const int w = v % 100;  // 27 / 7 for the fixed-width variants
+        const int w = required_width(v);
         if (!spmv_variant_ok(v) || v == 9999)
             return set_err(HPCCG_HIP_EINVAL, "unknown spmv variant %lld", value);
-        if ((w == 27 || w == 7) && !fixed_width_ok(M, v))
+        if (w && !fixed_width_ok(M, v))
             return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform width-%d SELL image", v, w);
         if (const char* why = variant_unavailable(M, v))
             return set_err(HPCCG_HIP_EINVAL, "variant %d needs %s (not built)", v, why);
@@ -2454,11 +2476,11 @@ int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_ite
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_us)
 {
     if (!M || !avg_us || reps < 1) return set_err(HPCCG_HIP_EINVAL, "bad argument");
-    const int w = variant % 100;
+    const int w = required_width(variant);
     if (!spmv_variant_ok(variant)) return set_err(HPCCG_HIP_EINVAL, "unknown variant %d", variant);
     if (const char* why = variant_unavailable(M, variant))
         return set_err(HPCCG_HIP_EINVAL, "variant %d needs %s", variant, why);
-    if ((w == 27 || w == 7 || variant == 9999) && !fixed_width_ok(M, variant))
+    if (w && !fixed_width_ok(M, variant))
         return set_err(HPCCG_HIP_EINVAL, "variant %d needs a uniform SELL image of that width", variant);
     HIP_TRY(hipSetDevice(M->device));
     TRY(ensure_hist(M, 2));
@@ -2494,6 +2516,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
     else if (!std::strcmp(key, "x_ring")) *value = x_ring_effective(M);
     else if (!std::strcmp(key, "update_slices")) *value = M->update_slices;
+    else if (!std::strcmp(key, "update_early")) *value = M->update_early;
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "resident_mb")) *value = resident_mb_effective(M);
     else if (!std::strcmp(key, "redund")) *value = redund_effective(M, 2) ? 1 : 0;  // off unless set

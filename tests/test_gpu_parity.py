@@ -58,7 +58,8 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
                                      5401, 5404, 5204, 6000, 6100, 6104, 6001, 7001, 7101, 7002,
                                      7102, 7027, 7127, 7201, 7202, 7301, 7302, 7204, 8000, 8200,
                                      8208, 8300, 8201, 8500, 8501, 8600, 8700, 8727, 8800,
-                                     8900, 8902, 8910, 8927, 8947])
+                                     8900, 8902, 8910, 8927, 8947, 8737, 8757, 8837, 8857,
+                                     8236, 8246, 8336])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
@@ -145,6 +146,14 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     M.set_option("update_slices", 1)
+    # the one-slice update with Ap and r loaded before its iteration test
+    for ue, fold, defer in itertools.product((1, 0), (1, 2), (1, 0)):
+        M.set_option("update_early", ue)
+        M.set_option("fold", fold)
+        M.set_option("x_defer", defer)
+        x = prob.x
+        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
+        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     assert all(r == results[0] for r in results)
 
 
@@ -662,3 +671,26 @@ def test_sell_a_holes_fused_and_refused(hp, gpu):
     assert not 8700 <= M.get_option("spmv_variant") < 8900
     with pytest.raises(hp.HPCCGError, match="SELL-512-A"):
         M.set_option("spmv_variant", 8700)
+
+
+def test_sell_a_early_loads_7pt(hp, gpu):
+    """The SELL-512-A variants that load a slice's values and offsets before
+    the iteration test (width 7 unrolled, 7-pt stencil) give the SELL-512
+    bits with the p update separate or formed per load; a width-7 variant is
+    refused on a 27-pt image."""
+    dims = (32, 16, 40)  # 40 planes of one slice each, plus the first and last
+    M = hp.Matrix.generate(*dims, use_7pt=True)
+    b, _, _ = M.vectors()
+    import torch
+    n = dims[0] * dims[1] * dims[2]
+    out = {}
+    for v, fuse in ((1000, 0), (8707, 1), (8717, 0), (8717, 1), (8817, 1), (8807, 0)):
+        M.set_option("spmv_variant", v)
+        M.set_option("fuse_p", fuse)
+        x = torch.zeros(n, dtype=torch.float64, device=gpu)
+        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=60, device=True)
+        out[(v, fuse)] = (it, nr, M.last_trace().tobytes(), host(x).tobytes())
+    assert all(o == out[(1000, 0)] for o in out.values())
+    M27 = hp.Matrix.generate(24, 20, 18)
+    with pytest.raises(hp.HPCCGError, match="width"):
+        M27.set_option("spmv_variant", 8717)

@@ -13,6 +13,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=200)
 ap.add_argument("--iters", type=int, default=12)
 ap.add_argument("--stencil", type=int, default=27, choices=[27, 7])
+ap.add_argument("--variant", type=int, default=-1, help="SpMV variant (-1: the library's choice)")
+ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1: default)")
 args = ap.parse_args()
 import torch  # noqa: E402,F401
 hp = load_pkg()
@@ -20,6 +22,10 @@ hp.set_device(0)
 M = hp.Matrix.generate(args.n, args.n, args.n, use_7pt=args.stencil == 7)
 if args.stencil == 27:
     M.diag_spmv(9999, 3)  # known-bytes stream of the uniform width-27 image (FETCH calibration)
+if args.variant >= 0:
+    M.set_option("spmv_variant", args.variant)
+if args.fuse_p >= 0:
+    M.set_option("fuse_p", args.fuse_p)
 b, _, _ = M.vectors()
 x = torch.zeros(args.n ** 3, dtype=torch.float64, device="cuda:0")
 M.set_option("use_graph", 0)
