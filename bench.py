@@ -100,6 +100,11 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=15.0):
 def matrix_format(v):
     """Matrix image a SpMV variant streams (hpccg_solver.cpp slot_bytes) and
     its bytes per stored slot."""
+    if 8960 <= v < 9000:
+        return ("SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared "
+                "by slice pairs"), 8.0
+    if 8900 <= v < 8960:
+        return "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows", 8.0
     if 8700 <= v < 8900:
         return "SELL-512-A (8 B value per offset-aligned slot, holes 0.0; x read at per-slice offsets)", 8.0
     if v >= 8000:
@@ -119,6 +124,10 @@ def matrix_format(v):
 
 def spmv_kernel_family(v):
     """Kernel template a SpMV variant launches (hpccg_kernels.hip launch_cg_spmv)."""
+    if 8960 <= v < 9000:
+        return "k_spmv_la2"
+    if 8900 <= v < 8960:
+        return "k_spmv_la"
     if 8700 <= v < 8900:
         return "k_spmv_pa"
     if 8500 <= v < 8700:

@@ -93,6 +93,11 @@ struct CgArgs {
     const int* awin;              // SELL-512-A LDS: per slice, kAWin windows (first row - slice row, length, LDS base)
     const int* awn;               // SELL-512-A LDS: windows per slice
     int alds_doubles;             // SELL-512-A LDS: dynamic LDS per block (largest window total)
+    const int* alds2;             // SELL-512-A pair windows: per slice, kAMax LDS positions (minus the pair row)
+    const int* awin2;             // per slice pair, kAWin windows (first row - pair row, length, LDS base)
+    const int* awn2;              // windows per slice pair
+    int alds2_doubles;            // dynamic LDS per two-slice block
+    int pgrid;                    // two-slice blocks, rounded up to a multiple of kNumXcd
     int pat_max;                  // SELL-512-P: largest table (ints) over slices: dynamic LDS
     const int* win_ptr;    // [nslices + 1] into the window arrays
     const int* win_start;  // first local column of the window
@@ -185,6 +190,9 @@ constexpr int kAMax = 32;
 // doubles per slice.
 constexpr int kAWin = 8;
 constexpr int kALdsMax = 8192;
+// Two-slice blocks (k_spmv_la2): windows over both slices' offsets, so
+// neighbouring slices share their staged planes.
+constexpr int kALdsMax2 = 12288;
 void launch_build_a(const unsigned int* slice_base, int nslices, const unsigned char* codes, const double* vals,
                     const int* cdict, const int* ccount, const unsigned int* abase, double* aval, int* aoff,
                     int* ok, int* maxabs, hipStream_t s);

@@ -1934,6 +1934,130 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_la(CgArgs a, bool pr
     complete_dot<kSliceRows / kRpt>(a, s, bs, kPAP, 0);
 }
 
+// SELL-512-A LDS windows over slice pairs (single rank): block P owns slices
+// 2P and 2P + 1 with 512 threads (waves 0-3 slice 2P, 4-7 slice 2P + 1, two
+// rows per thread as everywhere). The pair's windows cover both slices, so a
+// stencil plane is staged once for 1024 rows (27-pt 200^3: 4.2 instead of 5.4
+// doubles per row) and the p.Ap hand-off takes one ticket per two slices.
+// Each half forms its slice's partial with block_sum<256>'s shape (wave sums,
+// then the 4 in order), so the dot is bitwise the one-slice kernels'.
+template <bool kNT, bool kFuse, int kPre, int kMinW = 1>
+__global__ __launch_bounds__(kSliceRows, kMinW) void k_spmv_la2(CgArgs a, bool prologue)
+{
+    constexpr int kRpt = 2;
+    constexpr int kHalf = kSliceRows / kRpt;  // threads per slice
+    extern __shared__ __attribute__((aligned(16))) double xs[];
+    __shared__ double wsum[2 * kHalf / kWave];
+    const int P = xcd_slice(a.pgrid);
+    const int half = threadIdx.x / kHalf;
+    const int s = 2 * P + half;
+    const bool have = s < a.nslices;
+    const int lrow = (threadIdx.x % kHalf) * kRpt;  // row within the slice
+    const int wdt = have ? (int)(a.abase[s + 1] - a.abase[s]) : 0;
+    const double* __restrict__ vp = a.aval + (have ? (size_t)a.abase[s] * kSliceRows : 0) + lrow;
+    constexpr int kP = kPre > 0 ? kPre : 1;
+    Rows<kRpt> vpre[kP];
+#pragma unroll
+    for (int j = 0; j < kPre; j++)
+        if (j < wdt) vpre[j] = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+    int k = 0;
+    double rr = 0.0;  // r_{k-1}.r_{k-1}: the fused p update needs it
+    if (!prologue) {
+        k = a.kst[0];
+        if (kFuse) rr = cur_rr(a);
+        const bool run = cg_run(a, k, kFuse, rr);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (kFuse && (k == 1 || run)) a.hist[k - 1] = rr;
+            if (run)
+                stamp(a, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (!run) return;
+    }
+    if (2 * P >= a.nslices) return;
+    double* __restrict__ p = cur_p(a, k);
+    double beta = 0.0;
+    const double* __restrict__ pold = a.r;
+    if constexpr (kFuse) {
+        beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
+        pold = (k == 1) ? a.r : cur_p(a, k - 1);
+    }
+    const int prow0 = 2 * P * kSliceRows;  // first row of the pair
+    {
+        const int nw = a.awn2[P];
+        const int* __restrict__ win = a.awin2 + (size_t)P * kAWin * 3;
+        for (int w = 0; w < nw; w++) {
+            const int st0 = prow0 + win[3 * w] - a.ghost_lo, len = win[3 * w + 1], base = win[3 * w + 2];
+            for (int i = threadIdx.x; i < len; i += kSliceRows) {
+                const int l = st0 + i;  // local row (< 0 / >= n: guard or padding zeros)
+                if constexpr (kFuse)
+                    xs[base + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + beta * pold[l] : p[l];
+                else
+                    xs[base + i] = p[l];
+            }
+        }
+    }
+    __syncthreads();
+    double sum[kRpt];
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) sum[i] = 0.0;
+    const int row = s * kSliceRows + lrow;
+    double d = 0.0;
+    if (have) {
+        const int* __restrict__ cl = a.alds2 + (size_t)s * kAMax;
+        const int prow = half * kSliceRows + lrow;  // row within the pair
+#pragma unroll
+        for (int j = 0; j < kPre; j++) {
+            if (j < wdt) {
+                const int c = prow + cl[j];
+#pragma unroll
+                for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + vpre[j].v[i] * xs[c + i];
+            }
+        }
+#pragma unroll 6
+        for (int j = kPre; j < wdt; j++) {
+            const Rows<kRpt> v = ld_m<kRpt, kNT>(vp + (size_t)j * kSliceRows);
+            const int c = prow + cl[j];
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xs[c + i];
+        }
+        Rows<kRpt> o;
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) o.v[i] = sum[i];
+        st_rows<kRpt>(a.Ap, row, a.n, o);
+        if (!prologue) {
+            Rows<kRpt> pv;
+            if constexpr (kFuse) {
+                const Rows<kRpt> rv = ld<kRpt>(a.r + row);
+                const Rows<kRpt> yv = ld<kRpt>(pold + row);
+#pragma unroll
+                for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + beta * yv.v[i];
+                st_rows<kRpt>(p, row, a.n, pv);
+            } else {
+                pv = ld<kRpt>(p + row);
+            }
+#pragma unroll
+            for (int i = 0; i < kRpt; i++)
+                if (row + i < a.n) d += pv.v[i] * o.v[i];
+        }
+    }
+    if (prologue) return;
+    // per-slice partials with block_sum<256>'s shape
+    const double wv = wave_sum(d);
+    const int lane = threadIdx.x & (kWave - 1);
+    if (lane == 0) wsum[threadIdx.x / kWave] = wv;
+    __syncthreads();
+    if (threadIdx.x >= kWave) return;
+    constexpr int kWh = kHalf / kWave;
+    double bs = 0.0;
+    if (lane < 2) {
+#pragma unroll
+        for (int i = 0; i < kWh; i++) bs += wsum[lane * kWh + i];
+    }
+    complete_dot_lanes(a, 2 * P, min(2, a.nslices - 2 * P), bs, kPAP, 0);
+}
+
 // Plain SpMV on arbitrary x (kernel-level C ABI): same body, no dot.
 template <int kRpt>
 __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_plain(CgArgs a, const double* xext,
@@ -2614,6 +2738,10 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
 //   8900 / 8902 / 8910 / 8927 / 8947: SELL-512-A with LDS windows, nt prefetch
 //   4 / nt prefetch 2 / no nt prefetch 4 / nt prefetch 4 width 27 unrolled /
 //   nt no prefetch width 27
+//   8960 / 8962 / 8970: SELL-512-A pair windows (two slices per 512-thread
+//   block, single rank), nt prefetch 4 / nt prefetch 2 / default policy 4;
+//   8961 / 8963 / 8965: nt prefetch 1 / 3 / 0; 8966 / 8967 / 8968: nt
+//   prefetch 2 / 1 / 4 with at most 64 VGPRs (8 waves per SIMD)
 //   9999: diagnostic matrix stream without the gather (not an SpMV)
 #define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
     do {                                                                                            \
@@ -2689,6 +2817,17 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
             hipLaunchKernelGGL((k_spmv_la<RPT, NT, false, PRE, W>), dim3(a.sgrid), dim3(kSliceRows / RPT), \
                                smem, s, a, prologue);                                              \
     } while (0)
+#define HPCCG_SPMV_LA2W(NT, PRE, MINW)                                                             \
+    do {                                                                                           \
+        const size_t smem = (size_t)a.alds2_doubles * sizeof(double);                              \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_la2<NT, true, PRE, MINW>), dim3(a.pgrid), dim3(kSliceRows), smem, s, a, \
+                               prologue);                                                          \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_la2<NT, false, PRE, MINW>), dim3(a.pgrid), dim3(kSliceRows), smem, s, a, \
+                               prologue);                                                          \
+    } while (0)
+#define HPCCG_SPMV_LA2(NT, PRE) HPCCG_SPMV_LA2W(NT, PRE, 1)
 #define HPCCG_SPMV_PPW(RPT, NT, W)                                                                 \
     do {                                                                                           \
         if (a.fuse_p && !prologue)                                                                 \
@@ -2714,7 +2853,8 @@ bool spmv_variant_ok(int v)
     case 8216: case 8219: case 8226: case 8308: case 8316: case 8326: case 8507: case 8527: case 8607:
     case 8700: case 8707: case 8727: case 8800: case 8807:
     case 8900: case 8927: case 8910: case 8902: case 8947:
-    case 8236: case 8246: case 8336:
+    case 8236: case 8246: case 8336: case 8960: case 8962: case 8970:
+    case 8961: case 8963: case 8965: case 8966: case 8967: case 8968:
     case 8717: case 8737: case 8757: case 8837: case 8857: case 8817:
         return true;
     default:
@@ -2800,6 +2940,15 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 8837: HPCCG_SPMV_PAP(2, false, 27, 4); break;
     case 8857: HPCCG_SPMV_PAP(2, false, 27, 8); break;
     case 8900: HPCCG_SPMV_LA(2, true, 4, 0); break;
+    case 8960: HPCCG_SPMV_LA2(true, 4); break;
+    case 8962: HPCCG_SPMV_LA2(true, 2); break;
+    case 8961: HPCCG_SPMV_LA2(true, 1); break;
+    case 8965: HPCCG_SPMV_LA2(true, 0); break;
+    case 8963: HPCCG_SPMV_LA2(true, 3); break;
+    case 8966: HPCCG_SPMV_LA2W(true, 2, 8); break;
+    case 8967: HPCCG_SPMV_LA2W(true, 1, 8); break;
+    case 8968: HPCCG_SPMV_LA2W(true, 4, 8); break;
+    case 8970: HPCCG_SPMV_LA2(false, 4); break;
     case 8902: HPCCG_SPMV_LA(2, true, 2, 0); break;
     case 8910: HPCCG_SPMV_LA(2, false, 4, 0); break;
     case 8927: HPCCG_SPMV_LA(2, true, 4, 27); break;

@@ -241,6 +241,9 @@ struct hpccg_hip_matrix {
     int has_a_lds = 0;  // SELL-512-A LDS windows (27-pt: one per plane, holes included)
     int *d_alds = nullptr, *d_awin = nullptr, *d_awn = nullptr;
     int alds_doubles = 0;
+    int has_a_lds2 = 0;  // the same over slice pairs (k_spmv_la2, single rank)
+    int *d_alds2 = nullptr, *d_awin2 = nullptr, *d_awn2 = nullptr;
+    int alds2_doubles = 0;
     double* d_aval = nullptr;
     int* d_aoff = nullptr;
     unsigned int* d_abase = nullptr;
@@ -311,7 +314,7 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_vcodes,     M->d_vdict,   M->d_vval,  M->d_vldsc, M->d_vbase4, M->d_vcodes4,
                     M->d_ccount,     M->d_vcount,  M->d_prow,  M->d_prep,  M->d_pcount, M->d_pbase,
                     M->d_ptab_g,     M->d_ptab_l,  M->d_aval,  M->d_aoff,  M->d_abase,
-                    M->d_alds,       M->d_awin,    M->d_awn};
+                    M->d_alds,       M->d_awin,    M->d_awn,   M->d_alds2, M->d_awin2, M->d_awn2};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -654,6 +657,83 @@ int alloc_ring(hpccg_hip_matrix* M, int nbuf);
 int alloc_r(hpccg_hip_matrix* M);
 int x_ring_effective(const hpccg_hip_matrix* M);
 
+// Windows of a group of slices [s0, s0 + ns) over the union of their
+// ascending offsets (cut where neighbours are more than a slice apart):
+// window [o_a, o_b] stages rows s0*512 + o_a .. (s0 + ns)*512 - 1 + o_b, so
+// every row of every slice of the group finds every offset of the range,
+// holes included. lds[s][j] = LDS position of slot j minus the row's index
+// in the group; padding slots (offset 0, value 0.0) read slot 0's. Returns
+// the doubles staged, or -1 when it needs more than kAWin windows.
+int group_windows(const std::vector<int>& off, const std::vector<int>& cnt, int s0, int ns, int* win, int* nwin,
+                  std::vector<int>& lds)
+{
+    std::vector<int> u;
+    for (int t = 0; t < ns; t++)
+        for (int j = 0; j < cnt[s0 + t]; j++) u.push_back(off[(size_t)(s0 + t) * kAMax + j]);
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    const int rows = ns * kSliceRows;
+    int nw = 0, base = 0;
+    std::vector<int> wlo, wbase;
+    if (u.empty()) {  // empty rows only: one window of the group's own rows
+        win[0] = 0, win[1] = rows, win[2] = 0;
+        wlo.push_back(0), wbase.push_back(0);
+        nw = 1, base = rows;
+    }
+    for (size_t j = 0; j < u.size();) {
+        size_t e = j;
+        while (e + 1 < u.size() && u[e + 1] - u[e] <= kSliceRows) e++;
+        if (nw == kAWin) return -1;
+        win[3 * nw] = u[j];
+        win[3 * nw + 1] = rows + u[e] - u[j];
+        win[3 * nw + 2] = base;
+        wlo.push_back(u[j]);
+        wbase.push_back(base);
+        base += rows + u[e] - u[j];
+        nw++;
+        j = e + 1;
+    }
+    for (int t = 0; t < ns; t++) {
+        const int s = s0 + t;
+        int* l = &lds[(size_t)s * kAMax];
+        for (int j = 0; j < cnt[s]; j++) {
+            const int o = off[(size_t)s * kAMax + j];
+            int w = 0;
+            while (w + 1 < nw && wlo[w + 1] <= o) w++;
+            l[j] = wbase[w] + o - wlo[w];
+        }
+        // padding slots read slot 0's position; a slice without entries reads
+        // its own rows in the group's single window (position = group row)
+        if (cnt[s] == 0) l[0] = 0;
+        for (int j = std::max(cnt[s], 1); j < kAMax; j++) l[j] = l[0];
+    }
+    *nwin = nw;
+    return base;
+}
+
+// SELL-512-A pair windows (k_spmv_la2): slices 2P and 2P + 1 share one set.
+int build_a_windows2(hpccg_hip_matrix* M, const std::vector<int>& off, const std::vector<int>& cnt)
+{
+    const int S = M->nslices;
+    const int NP = (S + 1) / 2;
+    std::vector<int> lds((size_t)S * kAMax, 0), win((size_t)NP * kAWin * 3, 0), wn(NP, 0);
+    int maxd = 0;
+    for (int P = 0; P < NP; P++) {
+        const int d = group_windows(off, cnt, 2 * P, std::min(2, S - 2 * P), &win[(size_t)P * kAWin * 3], &wn[P], lds);
+        if (d < 0 || d > kALdsMax2) return 0;
+        maxd = std::max(maxd, d);
+    }
+    HIP_TRY(hipMalloc(&M->d_alds2, sizeof(int) * lds.size()));
+    HIP_TRY(hipMalloc(&M->d_awin2, sizeof(int) * win.size()));
+    HIP_TRY(hipMalloc(&M->d_awn2, sizeof(int) * wn.size()));
+    HIP_TRY(hipMemcpy(M->d_alds2, lds.data(), sizeof(int) * lds.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(M->d_awin2, win.data(), sizeof(int) * win.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(M->d_awn2, wn.data(), sizeof(int) * wn.size(), hipMemcpyHostToDevice));
+    M->alds2_doubles = maxd;
+    M->has_a_lds2 = 1;
+    return 0;
+}
+
 // SELL-512-A LDS windows (host, from the per-slice offsets): the ascending
 // offsets are cut where neighbours are more than a slice apart (staging the
 // gap would cost more than a second window); window [o_a, o_b] stages rows
@@ -701,7 +781,7 @@ int build_a_windows(hpccg_hip_matrix* M, const std::vector<int>& cnt)
     HIP_TRY(hipMemcpy(M->d_awn, wn.data(), sizeof(int) * wn.size(), hipMemcpyHostToDevice));
     M->alds_doubles = maxd;
     M->has_a_lds = 1;
-    return 0;
+    return build_a_windows2(M, off, cnt);
 }
 
 // SELL-512-A from the SELL-512-C codes (k_build_a), then the p ring again
@@ -904,7 +984,9 @@ const char* variant_unavailable(const hpccg_hip_matrix* M, int v)
     if (v >= 8000 && v < 8500 && !M->has_p_lds) return "the SELL-512-P LDS image";
     if (v >= 8500 && v < 8700 && !M->has_p) return "the SELL-512-P image";
     if (v >= 8700 && v < 8900 && !M->has_a) return "the SELL-512-A image";
-    if (v >= 8900 && v < 9000 && !M->has_a_lds) return "the SELL-512-A LDS windows";
+    if (v >= 8900 && v < 8960 && !M->has_a_lds) return "the SELL-512-A LDS windows";
+    if (v >= 8960 && v < 9000 && !M->has_a_lds2) return "the SELL-512-A pair windows";
+    if (v >= 8960 && v < 9000 && M->nranks != 1) return "a single rank (SELL-512-A pair windows)";
     return nullptr;
 }
 
@@ -951,6 +1033,11 @@ int choose_variant(const hpccg_hip_matrix* M)
     // 100^3 53.4 vs 58.2 us (8300), 7-pt 256^3 252 vs 277 us (8500 vs 3000).
     // Non-temporal value loads once the image outgrows the 256 MB Infinity Cache.
     const bool big_p = (double)M->nslots * 8.0 > 256e6;
+    // One rank, 27-pt beyond the Infinity Cache: SELL-512-A pair windows (two
+    // slices per 512-thread block share their staged planes, 4.2 instead of
+    // 5.4 staged doubles per row; one ticket per two slices), 3 value slots
+    // early: 200^3 2461-2468 vs 2330-2387 it/s (8236) on one box.
+    if (lds && big_p && M->has_p_lds && M->nranks == 1 && M->has_a_lds2) return 8963;
     // SELL-512-A (values in offset-aligned slots, x read directly at the
     // slice's offsets, p = r + beta*p_{k-1} formed per load on one rank)
     // everywhere except the 27-pt images beyond the Infinity Cache, where the
@@ -1116,6 +1203,11 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.awin = M->d_awin;
     a.awn = M->d_awn;
     a.alds_doubles = std::max(1, M->alds_doubles);
+    a.alds2 = M->d_alds2;
+    a.awin2 = M->d_awin2;
+    a.awn2 = M->d_awn2;
+    a.alds2_doubles = std::max(1, M->alds2_doubles);
+    a.pgrid = std::max(kNumXcd, ((M->nslices + 1) / 2 + kNumXcd - 1) / kNumXcd * kNumXcd);
     a.pat_max = std::max(1, M->pat_max);
     a.win_ptr = M->d_win_ptr;
     a.win_start = M->d_win_start;
@@ -1538,6 +1630,8 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     for (int r = 0; r < P; r++) {
         HIP_TRY(hipSetDevice(Ms[r]->device));
         TRY(ensure_hist(Ms[r], max_iter));
+        // a variant this matrix cannot run (e.g. a one-rank kernel on a rank of a group)
+        if (variant_unavailable(Ms[r], Ms[r]->spmv_variant)) Ms[r]->spmv_variant = choose_variant(Ms[r]);
     }
     if (P > 1) {
         gev.resize(P + 1);

@@ -97,6 +97,8 @@ def test_group_kernel_variants_bitwise(hp, gpu):
         if got != ref:
             pytest.fail(f"{(v, um, ring, fold)}: niters {got[0]} vs {ref[0]}, normr {got[1]} vs {ref[1]}")
     assert Ms[0].get_option("lds_doubles") > 0
+    with pytest.raises(hp.HPCCGError, match="single rank"):
+        Ms[0].set_option("spmv_variant", 8960)  # pair windows: one rank only
 
 
 def test_group_from_host_csr_equals_device_generator(hp, gpu):

@@ -59,7 +59,8 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
                                      7102, 7027, 7127, 7201, 7202, 7301, 7302, 7204, 8000, 8200,
                                      8208, 8300, 8201, 8500, 8501, 8600, 8700, 8727, 8800,
                                      8900, 8902, 8910, 8927, 8947, 8737, 8757, 8837, 8857,
-                                     8236, 8246, 8336])
+                                     8236, 8246, 8336, 8960, 8962, 8970, 8961, 8963,
+                                     8965, 8966, 8967, 8968])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
@@ -113,7 +114,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     # and the LDS kernels (same rows per thread), fused or not, give the same bits
     for v, fuse in itertools.product((2000, 2100, 2200, 2308, 3000, 3100, 4200, 4300, 5200, 5300, 6000, 6100,
-                                      7001, 7102, 8000, 8200, 8300, 8500, 8600, 8700, 8800, 8900, 8910),
+                                      7001, 7102, 8000, 8200, 8300, 8500, 8600, 8700, 8800, 8900, 8910, 8960),
                                      (0, 1)):
         M.set_option("spmv_variant", v)
         M.set_option("fuse_p", fuse)
@@ -658,7 +659,8 @@ def test_sell_a_holes_fused_and_refused(hp, gpu):
     M = hp.Matrix.from_csr(rp, cols, vals)
     b = 1.0 + (np.arange(n) % 3)
     out = {}
-    for v, fuse in ((1000, 0), (8700, 0), (8700, 1), (8800, 0), (8800, 1), (8900, 0), (8900, 1), (8910, 1)):
+    for v, fuse in ((1000, 0), (8700, 0), (8700, 1), (8800, 0), (8800, 1), (8900, 0), (8900, 1), (8910, 1),
+                    (8960, 0), (8960, 1)):
         M.set_option("spmv_variant", v)
         M.set_option("fuse_p", fuse)
         assert M.get_option("fuse_p") == fuse

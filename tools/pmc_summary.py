@@ -30,6 +30,7 @@ FORMATS = {
     "k_spmv_lp": "SELL-512-P (8 B value per slot + 1-byte row-pattern id per row), x from LDS windows",
     "k_spmv_pp": "SELL-512-P (8 B value per slot + 1-byte row-pattern id per row), x gathered",
     "k_spmv_v4": "SELL-512-V (1-byte (offset, value) codes in 4-slot chunks)",
+    "k_spmv_la2": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice pairs",
     "k_spmv_la": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows",
     "k_spmv_pa": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at per-slice offsets",
 }
@@ -93,7 +94,7 @@ def main():
         fetch_factor = stream_read / (f_stream * 1024.0)
     else:  # no width-27 image to stream: the factor the 27-pt calibrations measure (2.0)
         stream_read, f_stream, w_stream, fetch_factor = None, None, None, 2.0
-    SPMV = ("k_spmv<", "k_spmv_lds<", "k_spmv_c<", "k_spmv_lp<", "k_spmv_pp<", "k_spmv_v4<", "k_spmv_pa<", "k_spmv_la<")
+    SPMV = ("k_spmv<", "k_spmv_lds<", "k_spmv_c<", "k_spmv_lp<", "k_spmv_pp<", "k_spmv_v4<", "k_spmv_pa<", "k_spmv_la<", "k_spmv_la2<")
     f_spmv, kname = pick(fetch, SPMV, "FETCH_SIZE")
     w_spmv, _ = pick(write, SPMV, "WRITE_SIZE")
     spmv_read = f_spmv * 1024.0 * fetch_factor
@@ -106,6 +107,8 @@ def main():
         fuse_p = targs[-1].strip() == "true"
     elif "k_spmv_pa<" in kname:
         fuse_p = targs[3].strip() == "true"
+    elif "k_spmv_la2<" in kname:  # k_spmv_la2<kNT, kFuse, kPre, kMinW>
+        fuse_p = targs[1].strip() == "true"
     else:
         fuse_p = targs[2].strip() == "true"
     algo = 12.0 * nnz + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fuse_p else 0.0)
