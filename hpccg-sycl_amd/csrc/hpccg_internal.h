@@ -98,6 +98,11 @@ struct CgArgs {
     const int* awn2;              // windows per slice pair
     int alds2_doubles;            // dynamic LDS per two-slice block
     int pgrid;                    // two-slice blocks, rounded up to a multiple of kNumXcd
+    const int* alds4;             // the same for groups of four slices (k_spmv_la2<..., 4>)
+    const int* awin4;
+    const int* awn4;
+    int alds4_doubles;
+    int qgrid;
     int pat_max;                  // SELL-512-P: largest table (ints) over slices: dynamic LDS
     const int* win_ptr;    // [nslices + 1] into the window arrays
     const int* win_start;  // first local column of the window
@@ -189,10 +194,11 @@ constexpr int kAMax = 32;
 // offset of its range (holes included), at most kAWin windows and kALdsMax
 // doubles per slice.
 constexpr int kAWin = 8;
-constexpr int kALdsMax = 8192;
+constexpr int kALdsMax = 8000;  // + static LDS within the 64 KB default dynamic limit
 // Two-slice blocks (k_spmv_la2): windows over both slices' offsets, so
 // neighbouring slices share their staged planes.
-constexpr int kALdsMax2 = 12288;
+constexpr int kALdsMax2 = 7936;
+constexpr int kALdsMax4 = 7936;
 void launch_build_a(const unsigned int* slice_base, int nslices, const unsigned char* codes, const double* vals,
                     const int* cdict, const int* ccount, const unsigned int* abase, double* aval, int* aoff,
                     int* ok, int* maxabs, hipStream_t s);

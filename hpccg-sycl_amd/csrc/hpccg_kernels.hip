@@ -1941,16 +1941,21 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_la(CgArgs a, bool pr
 // doubles per row) and the p.Ap hand-off takes one ticket per two slices.
 // Each half forms its slice's partial with block_sum<256>'s shape (wave sums,
 // then the 4 in order), so the dot is bitwise the one-slice kernels'.
-template <bool kNT, bool kFuse, int kPre, int kMinW = 1>
-__global__ __launch_bounds__(kSliceRows, kMinW) void k_spmv_la2(CgArgs a, bool prologue)
+template <bool kNT, bool kFuse, int kPre, int kMinW = 1, int kS = 2>
+__global__ __launch_bounds__(kS * kSliceRows / 2, kMinW) void k_spmv_la2(CgArgs a, bool prologue)
 {
+    static_assert(kS == 2 || kS == 4, "slices per block");
     constexpr int kRpt = 2;
     constexpr int kHalf = kSliceRows / kRpt;  // threads per slice
+    constexpr int kThr = kS * kHalf;
     extern __shared__ __attribute__((aligned(16))) double xs[];
-    __shared__ double wsum[2 * kHalf / kWave];
-    const int P = xcd_slice(a.pgrid);
-    const int half = threadIdx.x / kHalf;
-    const int s = 2 * P + half;
+    __shared__ double wsum[kThr / kWave];
+    const int* __restrict__ g_lds = kS == 2 ? a.alds2 : a.alds4;
+    const int* __restrict__ g_win = kS == 2 ? a.awin2 : a.awin4;
+    const int* __restrict__ g_wn = kS == 2 ? a.awn2 : a.awn4;
+    const int P = xcd_slice(kS == 2 ? a.pgrid : a.qgrid);
+    const int half = threadIdx.x / kHalf;  // slice of the group
+    const int s = kS * P + half;
     const bool have = s < a.nslices;
     const int lrow = (threadIdx.x % kHalf) * kRpt;  // row within the slice
     const int wdt = have ? (int)(a.abase[s + 1] - a.abase[s]) : 0;
@@ -1975,7 +1980,7 @@ __global__ __launch_bounds__(kSliceRows, kMinW) void k_spmv_la2(CgArgs a, bool p
         }
         if (!run) return;
     }
-    if (2 * P >= a.nslices) return;
+    if (kS * P >= a.nslices) return;
     double* __restrict__ p = cur_p(a, k);
     double beta = 0.0;
     const double* __restrict__ pold = a.r;
@@ -1983,13 +1988,13 @@ __global__ __launch_bounds__(kSliceRows, kMinW) void k_spmv_la2(CgArgs a, bool p
         beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
         pold = (k == 1) ? a.r : cur_p(a, k - 1);
     }
-    const int prow0 = 2 * P * kSliceRows;  // first row of the pair
+    const int prow0 = kS * P * kSliceRows;  // first row of the group
     {
-        const int nw = a.awn2[P];
-        const int* __restrict__ win = a.awin2 + (size_t)P * kAWin * 3;
+        const int nw = g_wn[P];
+        const int* __restrict__ win = g_win + (size_t)P * kAWin * 3;
         for (int w = 0; w < nw; w++) {
             const int st0 = prow0 + win[3 * w] - a.ghost_lo, len = win[3 * w + 1], base = win[3 * w + 2];
-            for (int i = threadIdx.x; i < len; i += kSliceRows) {
+            for (int i = threadIdx.x; i < len; i += kThr) {
                 const int l = st0 + i;  // local row (< 0 / >= n: guard or padding zeros)
                 if constexpr (kFuse)
                     xs[base + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + beta * pold[l] : p[l];
@@ -2005,7 +2010,7 @@ __global__ __launch_bounds__(kSliceRows, kMinW) void k_spmv_la2(CgArgs a, bool p
     const int row = s * kSliceRows + lrow;
     double d = 0.0;
     if (have) {
-        const int* __restrict__ cl = a.alds2 + (size_t)s * kAMax;
+        const int* __restrict__ cl = g_lds + (size_t)s * kAMax;
         const int prow = half * kSliceRows + lrow;  // row within the pair
 #pragma unroll
         for (int j = 0; j < kPre; j++) {
@@ -2051,11 +2056,11 @@ __global__ __launch_bounds__(kSliceRows, kMinW) void k_spmv_la2(CgArgs a, bool p
     if (threadIdx.x >= kWave) return;
     constexpr int kWh = kHalf / kWave;
     double bs = 0.0;
-    if (lane < 2) {
+    if (lane < kS) {
 #pragma unroll
         for (int i = 0; i < kWh; i++) bs += wsum[lane * kWh + i];
     }
-    complete_dot_lanes(a, 2 * P, min(2, a.nslices - 2 * P), bs, kPAP, 0);
+    complete_dot_lanes(a, kS * P, min(kS, a.nslices - kS * P), bs, kPAP, 0);
 }
 
 // Plain SpMV on arbitrary x (kernel-level C ABI): same body, no dot.
@@ -2742,6 +2747,8 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
 //   block, single rank), nt prefetch 4 / nt prefetch 2 / default policy 4;
 //   8961 / 8963 / 8965: nt prefetch 1 / 3 / 0; 8966 / 8967 / 8968: nt
 //   prefetch 2 / 1 / 4 with at most 64 VGPRs (8 waves per SIMD)
+//   8980 / 8982 / 8983: four slices per 1024-thread block (quad windows),
+//   nt prefetch 0 / 2 / 3
 //   9999: diagnostic matrix stream without the gather (not an SpMV)
 #define HPCCG_SPMV(RPT, W, MINW, NT)                                                                \
     do {                                                                                            \
@@ -2828,6 +2835,16 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
                                prologue);                                                          \
     } while (0)
 #define HPCCG_SPMV_LA2(NT, PRE) HPCCG_SPMV_LA2W(NT, PRE, 1)
+#define HPCCG_SPMV_LA4(NT, PRE)                                                                    \
+    do {                                                                                           \
+        const size_t smem = (size_t)a.alds4_doubles * sizeof(double);                              \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_la2<NT, true, PRE, 8, 4>), dim3(a.qgrid), dim3(2 * kSliceRows), smem, s, \
+                               a, prologue);                                                       \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_la2<NT, false, PRE, 8, 4>), dim3(a.qgrid), dim3(2 * kSliceRows), smem, \
+                               s, a, prologue);                                                    \
+    } while (0)
 #define HPCCG_SPMV_PPW(RPT, NT, W)                                                                 \
     do {                                                                                           \
         if (a.fuse_p && !prologue)                                                                 \
@@ -2855,6 +2872,7 @@ bool spmv_variant_ok(int v)
     case 8900: case 8927: case 8910: case 8902: case 8947:
     case 8236: case 8246: case 8336: case 8960: case 8962: case 8970:
     case 8961: case 8963: case 8965: case 8966: case 8967: case 8968:
+    case 8980: case 8982: case 8983:
     case 8717: case 8737: case 8757: case 8837: case 8857: case 8817:
         return true;
     default:
@@ -2943,6 +2961,9 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 8960: HPCCG_SPMV_LA2(true, 4); break;
     case 8962: HPCCG_SPMV_LA2(true, 2); break;
     case 8961: HPCCG_SPMV_LA2(true, 1); break;
+    case 8980: HPCCG_SPMV_LA4(true, 0); break;
+    case 8982: HPCCG_SPMV_LA4(true, 2); break;
+    case 8983: HPCCG_SPMV_LA4(true, 3); break;
     case 8965: HPCCG_SPMV_LA2(true, 0); break;
     case 8963: HPCCG_SPMV_LA2(true, 3); break;
     case 8966: HPCCG_SPMV_LA2W(true, 2, 8); break;

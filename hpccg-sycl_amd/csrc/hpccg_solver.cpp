@@ -244,6 +244,9 @@ struct hpccg_hip_matrix {
     int has_a_lds2 = 0;  // the same over slice pairs (k_spmv_la2, single rank)
     int *d_alds2 = nullptr, *d_awin2 = nullptr, *d_awn2 = nullptr;
     int alds2_doubles = 0;
+    int has_a_lds4 = 0;  // and over groups of four slices
+    int *d_alds4 = nullptr, *d_awin4 = nullptr, *d_awn4 = nullptr;
+    int alds4_doubles = 0;
     double* d_aval = nullptr;
     int* d_aoff = nullptr;
     unsigned int* d_abase = nullptr;
@@ -314,7 +317,8 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_vcodes,     M->d_vdict,   M->d_vval,  M->d_vldsc, M->d_vbase4, M->d_vcodes4,
                     M->d_ccount,     M->d_vcount,  M->d_prow,  M->d_prep,  M->d_pcount, M->d_pbase,
                     M->d_ptab_g,     M->d_ptab_l,  M->d_aval,  M->d_aoff,  M->d_abase,
-                    M->d_alds,       M->d_awin,    M->d_awn,   M->d_alds2, M->d_awin2, M->d_awn2};
+                    M->d_alds,       M->d_awin,    M->d_awn,   M->d_alds2, M->d_awin2, M->d_awn2,
+                    M->d_alds4,      M->d_awin4,   M->d_awn4};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -711,27 +715,37 @@ int group_windows(const std::vector<int>& off, const std::vector<int>& cnt, int 
     return base;
 }
 
-// SELL-512-A pair windows (k_spmv_la2): slices 2P and 2P + 1 share one set.
-int build_a_windows2(hpccg_hip_matrix* M, const std::vector<int>& off, const std::vector<int>& cnt)
+// SELL-512-A group windows (k_spmv_la2): slices G*g .. G*g + G - 1 share
+// one set (G = 2 or 4).
+int build_a_windows_g(hpccg_hip_matrix* M, const std::vector<int>& off, const std::vector<int>& cnt, int G,
+                      int cap, int** d_lds, int** d_win, int** d_wn, int* doubles, int* has)
 {
     const int S = M->nslices;
-    const int NP = (S + 1) / 2;
-    std::vector<int> lds((size_t)S * kAMax, 0), win((size_t)NP * kAWin * 3, 0), wn(NP, 0);
+    const int NG = (S + G - 1) / G;
+    std::vector<int> lds((size_t)S * kAMax, 0), win((size_t)NG * kAWin * 3, 0), wn(NG, 0);
     int maxd = 0;
-    for (int P = 0; P < NP; P++) {
-        const int d = group_windows(off, cnt, 2 * P, std::min(2, S - 2 * P), &win[(size_t)P * kAWin * 3], &wn[P], lds);
-        if (d < 0 || d > kALdsMax2) return 0;
+    for (int P = 0; P < NG; P++) {
+        const int d = group_windows(off, cnt, G * P, std::min(G, S - G * P), &win[(size_t)P * kAWin * 3], &wn[P], lds);
+        if (d < 0 || d > cap) return 0;
         maxd = std::max(maxd, d);
     }
-    HIP_TRY(hipMalloc(&M->d_alds2, sizeof(int) * lds.size()));
-    HIP_TRY(hipMalloc(&M->d_awin2, sizeof(int) * win.size()));
-    HIP_TRY(hipMalloc(&M->d_awn2, sizeof(int) * wn.size()));
-    HIP_TRY(hipMemcpy(M->d_alds2, lds.data(), sizeof(int) * lds.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(M->d_awin2, win.data(), sizeof(int) * win.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(M->d_awn2, wn.data(), sizeof(int) * wn.size(), hipMemcpyHostToDevice));
-    M->alds2_doubles = maxd;
-    M->has_a_lds2 = 1;
+    HIP_TRY(hipMalloc(d_lds, sizeof(int) * lds.size()));
+    HIP_TRY(hipMalloc(d_win, sizeof(int) * win.size()));
+    HIP_TRY(hipMalloc(d_wn, sizeof(int) * wn.size()));
+    HIP_TRY(hipMemcpy(*d_lds, lds.data(), sizeof(int) * lds.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(*d_win, win.data(), sizeof(int) * win.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(*d_wn, wn.data(), sizeof(int) * wn.size(), hipMemcpyHostToDevice));
+    *doubles = maxd;
+    *has = 1;
     return 0;
+}
+
+int build_a_windows2(hpccg_hip_matrix* M, const std::vector<int>& off, const std::vector<int>& cnt)
+{
+    TRY(build_a_windows_g(M, off, cnt, 2, kALdsMax2, &M->d_alds2, &M->d_awin2, &M->d_awn2, &M->alds2_doubles,
+                          &M->has_a_lds2));
+    return build_a_windows_g(M, off, cnt, 4, kALdsMax4, &M->d_alds4, &M->d_awin4, &M->d_awn4, &M->alds4_doubles,
+                             &M->has_a_lds4);
 }
 
 // SELL-512-A LDS windows (host, from the per-slice offsets): the ascending
@@ -833,9 +847,10 @@ int build_a_image(hpccg_hip_matrix* M)
         return 0;
     }
     // A hole of row i at offset o reads column i + o; o is a real offset of
-    // some row of the same slice, so i + o lies within 511 of a valid column:
-    // two slices of zeros on each side cover every hole, whatever max |o|.
-    const long long guard = 2 * kSliceRows;
+    // some row of the same slice (of the same group of four slices for the
+    // group windows), so i + o lies within 2047 of a valid column: four
+    // slices of zeros on each side cover every hole, whatever max |o|.
+    const long long guard = 4 * kSliceRows;
     if (guard > M->p_guard) {
         M->p_guard = guard;
         const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
@@ -985,7 +1000,8 @@ const char* variant_unavailable(const hpccg_hip_matrix* M, int v)
     if (v >= 8500 && v < 8700 && !M->has_p) return "the SELL-512-P image";
     if (v >= 8700 && v < 8900 && !M->has_a) return "the SELL-512-A image";
     if (v >= 8900 && v < 8960 && !M->has_a_lds) return "the SELL-512-A LDS windows";
-    if (v >= 8960 && v < 9000 && !M->has_a_lds2) return "the SELL-512-A pair windows";
+    if (v >= 8960 && v < 8980 && !M->has_a_lds2) return "the SELL-512-A pair windows";
+    if (v >= 8980 && v < 9000 && !M->has_a_lds4) return "the SELL-512-A quad windows";
     if (v >= 8960 && v < 9000 && M->nranks != 1) return "a single rank (SELL-512-A pair windows)";
     return nullptr;
 }
@@ -1208,6 +1224,11 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.awn2 = M->d_awn2;
     a.alds2_doubles = std::max(1, M->alds2_doubles);
     a.pgrid = std::max(kNumXcd, ((M->nslices + 1) / 2 + kNumXcd - 1) / kNumXcd * kNumXcd);
+    a.alds4 = M->d_alds4;
+    a.awin4 = M->d_awin4;
+    a.awn4 = M->d_awn4;
+    a.alds4_doubles = std::max(1, M->alds4_doubles);
+    a.qgrid = std::max(kNumXcd, ((M->nslices + 3) / 4 + kNumXcd - 1) / kNumXcd * kNumXcd);
     a.pat_max = std::max(1, M->pat_max);
     a.win_ptr = M->d_win_ptr;
     a.win_start = M->d_win_start;
