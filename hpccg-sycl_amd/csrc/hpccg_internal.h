@@ -103,6 +103,10 @@ struct CgArgs {
     const int* awn4;
     int alds4_doubles;
     int qgrid;
+    // group kernels (pair / quad windows): group ranges [gs0, gs0 + gn0) then
+    // [gs1, gs1 + gn1), as s0/sn0/s1/sn1 for the one-slice kernels; pgrid /
+    // qgrid cover gn0 + gn1. agroup = slices per group of the variant (0: none)
+    int agroup, gs0, gn0, gs1, gn1;
     int pat_max;                  // SELL-512-P: largest table (ints) over slices: dynamic LDS
     const int* win_ptr;    // [nslices + 1] into the window arrays
     const int* win_start;  // first local column of the window

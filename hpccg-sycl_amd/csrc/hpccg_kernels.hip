@@ -1953,9 +1953,10 @@ __global__ __launch_bounds__(kS * kSliceRows / 2, kMinW) void k_spmv_la2(CgArgs 
     const int* __restrict__ g_lds = kS == 2 ? a.alds2 : a.alds4;
     const int* __restrict__ g_win = kS == 2 ? a.awin2 : a.awin4;
     const int* __restrict__ g_wn = kS == 2 ? a.awn2 : a.awn4;
-    const int P = xcd_slice(kS == 2 ? a.pgrid : a.qgrid);
+    int P = xcd_slice(kS == 2 ? a.pgrid : a.qgrid);  // group: all, or the interior / halo runs
+    P = P < a.gn0 ? a.gs0 + P : (P < a.gn0 + a.gn1 ? a.gs1 + (P - a.gn0) : -1);
     const int half = threadIdx.x / kHalf;  // slice of the group
-    const int s = kS * P + half;
+    const int s = P < 0 ? a.nslices : kS * P + half;
     const bool have = s < a.nslices;
     const int lrow = (threadIdx.x % kHalf) * kRpt;  // row within the slice
     const int wdt = have ? (int)(a.abase[s + 1] - a.abase[s]) : 0;
@@ -1980,7 +1981,7 @@ __global__ __launch_bounds__(kS * kSliceRows / 2, kMinW) void k_spmv_la2(CgArgs 
         }
         if (!run) return;
     }
-    if (kS * P >= a.nslices) return;
+    if (P < 0 || kS * P >= a.nslices) return;
     double* __restrict__ p = cur_p(a, k);
     double beta = 0.0;
     const double* __restrict__ pold = a.r;

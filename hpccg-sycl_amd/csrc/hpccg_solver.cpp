@@ -1002,7 +1002,7 @@ const char* variant_unavailable(const hpccg_hip_matrix* M, int v)
     if (v >= 8900 && v < 8960 && !M->has_a_lds) return "the SELL-512-A LDS windows";
     if (v >= 8960 && v < 8980 && !M->has_a_lds2) return "the SELL-512-A pair windows";
     if (v >= 8980 && v < 9000 && !M->has_a_lds4) return "the SELL-512-A quad windows";
-    if (v >= 8960 && v < 9000 && M->nranks != 1) return "a single rank (SELL-512-A pair windows)";
+    if (v >= 8960 && v < 9000 && M->general) return "the slab halo plan (SELL-512-A group windows)";
     return nullptr;
 }
 
@@ -1053,7 +1053,7 @@ int choose_variant(const hpccg_hip_matrix* M)
     // slices per 512-thread block share their staged planes, 4.2 instead of
     // 5.4 staged doubles per row; one ticket per two slices), 3 value slots
     // early: 200^3 2461-2468 vs 2330-2387 it/s (8236) on one box.
-    if (lds && big_p && M->has_p_lds && M->nranks == 1 && M->has_a_lds2) return 8963;
+    if (lds && big_p && M->has_p_lds && !M->general && M->has_a_lds2) return 8963;
     // SELL-512-A (values in offset-aligned slots, x read directly at the
     // slice's offsets, p = r + beta*p_{k-1} formed per load on one rank)
     // everywhere except the 27-pt images beyond the Infinity Cache, where the
@@ -1229,6 +1229,13 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.awn4 = M->d_awn4;
     a.alds4_doubles = std::max(1, M->alds4_doubles);
     a.qgrid = std::max(kNumXcd, ((M->nslices + 3) / 4 + kNumXcd - 1) / kNumXcd * kNumXcd);
+    {
+        const int v = M->spmv_variant;
+        a.agroup = (v >= 8960 && v < 8980) ? 2 : ((v >= 8980 && v < 9000) ? 4 : 0);
+        a.gs0 = 0;
+        a.gn0 = a.agroup ? (M->nslices + a.agroup - 1) / a.agroup : 0;
+        a.gs1 = a.gn1 = 0;
+    }
     a.pat_max = std::max(1, M->pat_max);
     a.win_ptr = M->d_win_ptr;
     a.win_start = M->d_win_start;
@@ -1441,6 +1448,22 @@ CgArgs spmv_range(const CgArgs& a, int s0, int n0, int s1, int n1)
     return b;
 }
 
+// The same for the group kernels, in groups of a.agroup slices.
+CgArgs group_range(const CgArgs& a, int g0, int n0, int g1, int n1)
+{
+    CgArgs b = a;
+    b.gs0 = g0;
+    b.gn0 = n0;
+    b.gs1 = g1;
+    b.gn1 = n1;
+    const int grid = std::max(kNumXcd, (n0 + n1 + kNumXcd - 1) / kNumXcd * kNumXcd);
+    if (a.agroup == 2)
+        b.pgrid = grid;
+    else
+        b.qgrid = grid;
+    return b;
+}
+
 // Multi-rank slab iteration with the halo exchange overlapped (SURVEY 5,
 // "overlap the halo with the interior-row SpMV"): the halo rows of p_k first
 // (k_p_boundary), then the exchange on the second stream while the main stream
@@ -1493,10 +1516,22 @@ int enqueue_spmv_overlapped(const Ranks& R, int slot, int k_host)
         TRY(use_device(R, r));
         const int lo = M->halo_b_lo, hi = M->halo_b_hi, mid = M->nslices - lo - hi;
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
-        launch_cg_spmv(spmv_range(a, lo, mid, 0, 0), M->spmv_variant, false, M->stream);
-        HIP_TRY(hipStreamWaitEvent(M->stream, M->ev_halo, 0));
-        if (lo + hi > 0)
-            launch_cg_spmv(spmv_range(a, 0, lo, M->nslices - hi, hi), M->spmv_variant, false, M->stream);
+        if (a.agroup) {
+            // groups holding a ghost-reading slice run after the halo: the
+            // first ceil(lo / G) and every group from floor((S - hi) / G)
+            const int G = a.agroup, NG = (M->nslices + G - 1) / G;
+            const int glo = std::min(NG, (lo + G - 1) / G);
+            const int ghi0 = std::max(glo, (M->nslices - hi) / G);
+            launch_cg_spmv(group_range(a, glo, ghi0 - glo, 0, 0), M->spmv_variant, false, M->stream);
+            HIP_TRY(hipStreamWaitEvent(M->stream, M->ev_halo, 0));
+            if (glo + (NG - ghi0) > 0)
+                launch_cg_spmv(group_range(a, 0, glo, ghi0, NG - ghi0), M->spmv_variant, false, M->stream);
+        } else {
+            launch_cg_spmv(spmv_range(a, lo, mid, 0, 0), M->spmv_variant, false, M->stream);
+            HIP_TRY(hipStreamWaitEvent(M->stream, M->ev_halo, 0));
+            if (lo + hi > 0)
+                launch_cg_spmv(spmv_range(a, 0, lo, M->nslices - hi, hi), M->spmv_variant, false, M->stream);
+        }
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
         if (!a.redund && !fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
     }

@@ -60,7 +60,7 @@ def test_group_kernel_variants_bitwise(hp, gpu):
     Ms = hp.group_generate(24, 20, 9, 3)
     ref = None
     import itertools
-    for v, fold, fuse, defer, ovl in itertools.product((1000, 0, 2000, 2100, 4200, 5200, 7201, 8200, 8500, 8800, 8900, 8910),
+    for v, fold, fuse, defer, ovl in itertools.product((1000, 0, 2000, 2100, 4200, 5200, 7201, 8200, 8500, 8800, 8900, 8910, 8963, 8983),
                                                        (0, 1, 2), (0, 1), (0, 1),
                                                       (0, 1)):
         for M in Ms:
@@ -97,8 +97,7 @@ def test_group_kernel_variants_bitwise(hp, gpu):
         if got != ref:
             pytest.fail(f"{(v, um, ring, fold)}: niters {got[0]} vs {ref[0]}, normr {got[1]} vs {ref[1]}")
     assert Ms[0].get_option("lds_doubles") > 0
-    with pytest.raises(hp.HPCCGError, match="single rank"):
-        Ms[0].set_option("spmv_variant", 8960)  # pair windows: one rank only
+
 
 
 def test_group_from_host_csr_equals_device_generator(hp, gpu):
