@@ -1941,7 +1941,7 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_spmv_la(CgArgs a, bool pr
 // doubles per row) and the p.Ap hand-off takes one ticket per two slices.
 // Each half forms its slice's partial with block_sum<256>'s shape (wave sums,
 // then the 4 in order), so the dot is bitwise the one-slice kernels'.
-template <bool kNT, bool kFuse, int kPre, int kMinW = 1, int kS = 2>
+template <bool kNT, bool kFuse, int kPre, int kMinW = 1, int kS = 2, int kSU = 1>
 __global__ __launch_bounds__(kS * kSliceRows / 2, kMinW) void k_spmv_la2(CgArgs a, bool prologue)
 {
     static_assert(kS == 2 || kS == 4, "slices per block");
@@ -1995,7 +1995,24 @@ __global__ __launch_bounds__(kS * kSliceRows / 2, kMinW) void k_spmv_la2(CgArgs 
         const int* __restrict__ win = g_win + (size_t)P * kAWin * 3;
         for (int w = 0; w < nw; w++) {
             const int st0 = prow0 + win[3 * w] - a.ghost_lo, len = win[3 * w + 1], base = win[3 * w + 2];
-            for (int i = threadIdx.x; i < len; i += kThr) {
+            int i = threadIdx.x;
+            if constexpr (kSU > 1) {
+                // kSU positions per thread with every load issued before the stores
+                for (; i + (kSU - 1) * kThr < len; i += kSU * kThr) {
+                    double v[kSU];
+#pragma unroll
+                    for (int u = 0; u < kSU; u++) {
+                        const int l = st0 + i + u * kThr;
+                        if constexpr (kFuse)
+                            v[u] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + beta * pold[l] : p[l];
+                        else
+                            v[u] = p[l];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kSU; u++) xs[base + i + u * kThr] = v[u];
+                }
+            }
+            for (; i < len; i += kThr) {
                 const int l = st0 + i;  // local row (< 0 / >= n: guard or padding zeros)
                 if constexpr (kFuse)
                     xs[base + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + beta * pold[l] : p[l];
@@ -2748,6 +2765,8 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
 //   block, single rank), nt prefetch 4 / nt prefetch 2 / default policy 4;
 //   8961 / 8963 / 8965: nt prefetch 1 / 3 / 0; 8966 / 8967 / 8968: nt
 //   prefetch 2 / 1 / 4 with at most 64 VGPRs (8 waves per SIMD)
+//   8972 / 8973: 8963 with 2 / 3 staged positions per thread, loads before
+//   stores; 8974: 8963 with at most 64 VGPRs (8 waves per SIMD)
 //   8980 / 8982 / 8983: four slices per 1024-thread block (quad windows),
 //   nt prefetch 0 / 2 / 3
 //   9999: diagnostic matrix stream without the gather (not an SpMV)
@@ -2836,6 +2855,16 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
                                prologue);                                                          \
     } while (0)
 #define HPCCG_SPMV_LA2(NT, PRE) HPCCG_SPMV_LA2W(NT, PRE, 1)
+#define HPCCG_SPMV_LA2U(NT, PRE, SU)                                                               \
+    do {                                                                                           \
+        const size_t smem = (size_t)a.alds2_doubles * sizeof(double);                              \
+        if (a.fuse_p && !prologue)                                                                 \
+            hipLaunchKernelGGL((k_spmv_la2<NT, true, PRE, SU == 4 ? 8 : 1, 2, SU == 4 ? 1 : SU>), dim3(a.pgrid), dim3(kSliceRows), smem, s, \
+                               a, prologue);                                                       \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_la2<NT, false, PRE, SU == 4 ? 8 : 1, 2, SU == 4 ? 1 : SU>), dim3(a.pgrid), dim3(kSliceRows), smem, \
+                               s, a, prologue);                                                    \
+    } while (0)
 #define HPCCG_SPMV_LA4(NT, PRE)                                                                    \
     do {                                                                                           \
         const size_t smem = (size_t)a.alds4_doubles * sizeof(double);                              \
@@ -2873,7 +2902,7 @@ bool spmv_variant_ok(int v)
     case 8900: case 8927: case 8910: case 8902: case 8947:
     case 8236: case 8246: case 8336: case 8960: case 8962: case 8970:
     case 8961: case 8963: case 8965: case 8966: case 8967: case 8968:
-    case 8980: case 8982: case 8983:
+    case 8980: case 8982: case 8983: case 8972: case 8973: case 8974:
     case 8717: case 8737: case 8757: case 8837: case 8857: case 8817:
         return true;
     default:
@@ -2962,6 +2991,9 @@ void launch_cg_spmv(const CgArgs& a, int variant, bool prologue, hipStream_t s)
     case 8960: HPCCG_SPMV_LA2(true, 4); break;
     case 8962: HPCCG_SPMV_LA2(true, 2); break;
     case 8961: HPCCG_SPMV_LA2(true, 1); break;
+    case 8972: HPCCG_SPMV_LA2U(true, 3, 2); break;
+    case 8973: HPCCG_SPMV_LA2U(true, 3, 3); break;
+    case 8974: HPCCG_SPMV_LA2U(true, 3, 4); break;
     case 8980: HPCCG_SPMV_LA4(true, 0); break;
     case 8982: HPCCG_SPMV_LA4(true, 2); break;
     case 8983: HPCCG_SPMV_LA4(true, 3); break;

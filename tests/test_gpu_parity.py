@@ -60,7 +60,7 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
                                      8208, 8300, 8201, 8500, 8501, 8600, 8700, 8727, 8800,
                                      8900, 8902, 8910, 8927, 8947, 8737, 8757, 8837, 8857,
                                      8236, 8246, 8336, 8960, 8962, 8970, 8961, 8963,
-                                     8965, 8966, 8967, 8968, 8980, 8982, 8983])
+                                     8965, 8966, 8967, 8968, 8980, 8982, 8983, 8972, 8973, 8974])
 def test_sparsemv_variants_agree(hp, gpu, variant):
     """Every SpMV variant computes every row bitwise identically; variants with
     the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
