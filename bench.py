@@ -173,6 +173,8 @@ def main():
     ap.add_argument("--x-defer", type=int, default=-1, help="batched x update (-1 default)")
     ap.add_argument("--update-early", type=int, default=-1,
                     help="loop update loads Ap and r before the iteration test (-1 default)")
+    ap.add_argument("--pap-in-update", type=int, default=-1,
+                    help="the loop update sums the SpMV's p.Ap partials itself (-1 default)")
     ap.add_argument("--update-slices", type=int, default=-1,
                     help="slices per loop-update workgroup: 1, 2, 4, 8 (-1 default)")
     ap.add_argument("--x-ring", type=int, default=-1,
@@ -228,6 +230,8 @@ def main():
         M.set_option("update_slices", args.update_slices)
     if args.update_early >= 0:
         M.set_option("update_early", args.update_early)
+    if args.pap_in_update >= 0:
+        M.set_option("pap_in_update", args.pap_in_update)
     if args.x_ring > 0:
         M.set_option("x_ring", args.x_ring)
     if args.rev_update >= 0:
@@ -372,7 +376,7 @@ def main():
                 "spmv_variant": M.get_option("spmv_variant"),
                 "matrix_format": matrix_format(M.get_option("spmv_variant"))[0],
                 "matrix_bytes_per_slot": matrix_format(M.get_option("spmv_variant"))[1],
-                "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "update_slices", "update_early", "x_defer", "x_ring", "rev_update",
+                "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "update_slices", "update_early", "pap_in_update", "x_defer", "x_ring", "rev_update",
                                                          "resident_mb", "overlap", "value_codes")},
             },
             "cg_iterations_per_s_global": round(it_per_s, 3),

@@ -52,6 +52,8 @@ struct CgArgs {
     int ugrid;             // k_update_g grid (groups rounded up to a multiple of kNumXcd)
     int um;                // slices per k_update workgroup (1: k_update, else k_update_m)
     int uearly;            // um = 1: k_update_e (Ap and r loaded before the iteration test)
+    int pap_upd;           // one rank, um = 1: k_update_pr forms p.Ap itself (SpMV: partials only)
+    double* ppart;         // pap_upd: the SpMV's p.Ap slice partials (apart from the r.r ones)
     int umgrid;            // k_update_m grid (slice blocks of um rounded up to a multiple of kNumXcd)
     int s0, sn0, s1, sn1;  // SpMV launch: slices [s0, s0 + sn0) then [s1, s1 + sn1)
     int sgrid;             // SpMV launch grid (sn0 + sn1 rounded up to a multiple of kNumXcd)
@@ -118,6 +120,7 @@ struct CgArgs {
 // Is dot `which` (kRR / kPAP) completed inside its producing kernel?
 inline __host__ __device__ bool fold_of(const CgArgs& a, int which)
 {
+    if (which == kPAP && a.pap_upd) return false;  // the update kernel sums the partials itself
     return a.fold == 1 || (a.fold == 2 && which == kPAP) || (a.fold == 3 && which == kRR);
 }
 

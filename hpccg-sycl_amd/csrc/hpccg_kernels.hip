@@ -376,7 +376,8 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, int s0, int 
     unsigned* gt = a.tickets + which * (ng + 1);          // group tickets, then the top one
     const int lane = threadIdx.x;
     if (!fold_of(a, which)) {
-        if (lane < cnt) a.partial[s0 + lane] = bs;
+        double* dst = (which == kPAP && a.pap_upd) ? a.ppart : a.partial;
+        if (lane < cnt) dst[s0 + lane] = bs;
         return;
     }
     const int g = s0 / kGroup;
@@ -2410,11 +2411,11 @@ __global__ __launch_bounds__(kSliceRows / kRpt) void k_update_m(CgArgs a)
 constexpr int kUGThreads = 1024;
 
 // p.Ap (which = kPAP) or r.r total from the slice partials, in every thread.
-__device__ double total_from_partials(const CgArgs& a, int which, double* gs_lds)
+__device__ double total_from_partials(const CgArgs& a, int which, double* gs_lds, const double* part = nullptr)
 {
     const int ng = ngroups_of(a);
     (void)which;
-    const double* part = a.partial;  // the producing kernel's slice partials
+    if (!part) part = a.partial;  // the producing kernel's slice partials
     const int lane = threadIdx.x & (kWave - 1);
     const int nw = blockDim.x / kWave;
     constexpr int kB = 8;
@@ -2439,6 +2440,66 @@ __device__ double total_from_partials(const CgArgs& a, int which, double* gs_lds
     }
     __syncthreads();
     return tot;
+}
+
+// Loop update that forms p.Ap itself (a.pap_upd: one rank, at most kPapGroups
+// groups): every workgroup sums all SpMV slice partials with k_finalize's
+// fixed two-level shape (total_from_partials), so the SpMV publishes its
+// partials without tickets and no p.Ap finalize runs. Ap and r are loaded
+// before that sum. Same values as k_update.
+constexpr int kPapGroups = 64;
+
+template <int kRpt>
+__global__ __launch_bounds__(kSliceRows / kRpt) void k_update_pr(CgArgs a)
+{
+    __shared__ double gs[kPapGroups];
+    const int s = a.rev ? xcd_slice_rev(a.grid) : xcd_slice(a.grid);
+    const bool have = s < a.nslices;
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    Rows<kRpt> apv, rv;
+    if (have) {
+        apv = ld<kRpt>(a.Ap + row);
+        rv = ld<kRpt>(a.r + row);
+    }
+    const int k = a.kst[0];
+    const bool run = cg_run(a, k, false);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (run)
+            stamp(a, kStampUpdate);
+        else
+            mark_end(a);
+    }
+    if (!run) return;
+    const double pap = total_from_partials(a, kPAP, gs, a.ppart);  // every thread; block-wide barriers
+    if (!have) return;
+    const double alpha = a.g[kRR] / pap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.ahist[k] = alpha;
+        a.g[kPAP] = pap;
+        a.loc[kPAP] = pap;
+    }
+    Rows<kRpt> rn;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
+    if (!a.xdefer) {
+        const Rows<kRpt> xv = ld<kRpt>(a.x + row);
+        const Rows<kRpt> pv = ld<kRpt>(cur_p(a, k) + row);
+        Rows<kRpt> xn;
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) xn.v[i] = xv.v[i] + alpha * pv.v[i];
+        st_rows<kRpt>(a.x, row, a.n, xn);
+    } else if (k % a.nring == 0) {
+        Rows<kRpt> xn = ld<kRpt>(a.x + row);
+        x_accumulate<kRpt>(a, row, k - a.nring + 1, k, k, alpha, xn);
+        st_rows<kRpt>(a.x, row, a.n, xn);
+    }
+    st_rows<kRpt>(a.r, row, a.n, rn);
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += rn.v[i] * rn.v[i];
+    const double bs = block_sum<kSliceRows / kRpt>(d);
+    complete_dot<kSliceRows / kRpt>(a, s, bs, kRR, k + 1);
 }
 
 template <int kRpt, bool kPrologue>
@@ -3061,6 +3122,8 @@ void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)
         hipLaunchKernelGGL((k_update_m<kRpt, 4>), dim3(a.umgrid), dim3(kBlock), 0, s, a);
     else if (a.um == 8)
         hipLaunchKernelGGL((k_update_m<kRpt, 8>), dim3(a.umgrid), dim3(kBlock), 0, s, a);
+    else if (a.pap_upd)
+        hipLaunchKernelGGL(k_update_pr<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
     else if (a.uearly)
         hipLaunchKernelGGL(k_update_e<kRpt>, dim3(a.grid), dim3(kBlock), 0, s, a);
     else

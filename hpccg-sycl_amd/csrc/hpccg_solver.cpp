@@ -272,6 +272,7 @@ struct hpccg_hip_matrix {
     int redund = 0;            // consumers complete the dots themselves, no finalize kernels (measured slower)
     int update_slices = 1;     // slices per loop-update workgroup (1, 2, 4, 8)
     int update_early = 0;      // loop update loads Ap and r before the iteration test
+    int pap_upd = 0;           // the loop update forms p.Ap from the SpMV partials (one rank, <= 64 groups)
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_rbuf = nullptr;  // r with p_guard zeroed doubles on each side (fused SELL-512-A reads holes there)
     double* d_partial = nullptr;
@@ -951,7 +952,9 @@ int alloc_workspace(hpccg_hip_matrix* M)
         HIP_TRY(hipMemset(*v, 0, sizeof(double) * M->npad));
     }
     const int ngroups = (M->nslices + 63) / 64;  // kGroup in hpccg_kernels.hip
-    HIP_TRY(hipMalloc(&M->d_partial, sizeof(double) * (std::max(1, M->nslices) + 2 * ngroups + 8)));
+    // slice partials, group sums of both dots, 8 spare, then the p.Ap slice
+    // partials of the pap_upd mode
+    HIP_TRY(hipMalloc(&M->d_partial, sizeof(double) * (2 * std::max(1, M->nslices) + 2 * ngroups + 8)));
     M->ntickets = 2 * (ngroups + 1);
     HIP_TRY(hipMalloc(&M->d_tickets, sizeof(unsigned int) * M->ntickets));
     HIP_TRY(hipMemset(M->d_tickets, 0, sizeof(unsigned int) * M->ntickets));
@@ -1135,6 +1138,15 @@ int fold_effective(const hpccg_hip_matrix* M)
     return 2;
 }
 
+// p.Ap formed by every loop-update workgroup (k_update_pr): one rank, one
+// slice per update workgroup, no redundant mode, at most 64 groups of slice
+// partials (32 K slices: 16 M rows) to sum per workgroup.
+bool pap_upd_effective(const hpccg_hip_matrix* M)
+{
+    if (M->pap_upd <= 0 || M->nranks != 1 || M->update_slices != 1 || M->redund > 0) return false;
+    return (M->nslices + 63) / 64 <= 64;
+}
+
 // Redundant dot completion (k_update_g + cur_rr): single rank, group sums that
 // fit the update's LDS, at least one iteration (trace[0] then comes from hist).
 bool redund_effective(const hpccg_hip_matrix* M, int max_iter)
@@ -1183,6 +1195,8 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
         a.ugrid = std::max(kNumXcd, (ng + kNumXcd - 1) / kNumXcd * kNumXcd);
         a.um = M->update_slices;
         a.uearly = M->update_early ? 1 : 0;
+        a.pap_upd = pap_upd_effective(M) ? 1 : 0;
+        a.ppart = M->d_partial + std::max(1, M->nslices) + 2 * ng + 8;
         const int nb = (M->nslices + a.um - 1) / a.um;
         a.umgrid = std::max(kNumXcd, (nb + kNumXcd - 1) / kNumXcd * kNumXcd);
     }
@@ -1533,7 +1547,7 @@ int enqueue_spmv_overlapped(const Ranks& R, int slot, int k_host)
                 launch_cg_spmv(spmv_range(a, 0, lo, M->nslices - hi, hi), M->spmv_variant, false, M->stream);
         }
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
-        if (!a.redund && !fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
+        if (!a.redund && !a.pap_upd && !fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
     }
     return 0;
 }
@@ -1572,7 +1586,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
         launch_cg_spmv(a, M->spmv_variant, false, M->stream);
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
-        if (!a.redund && !fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
+        if (!a.redund && !a.pap_upd && !fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
     }
     if (multi) TRY(exch_allreduce(R, kPAP, false));
     for (int r = 0; r < R.P; r++) {
@@ -2554,6 +2568,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->redund = (int)value;
     } else if (!std::strcmp(key, "update_early")) {
         M->update_early = value != 0;
+    } else if (!std::strcmp(key, "pap_in_update")) {
+        M->pap_upd = (int)value;
     } else if (!std::strcmp(key, "update_slices")) {
         if (value != 1 && value != 2 && value != 4 && value != 8)
             return set_err(HPCCG_HIP_EINVAL, "update_slices must be 1, 2, 4 or 8");
@@ -2667,6 +2683,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "x_ring")) *value = x_ring_effective(M);
     else if (!std::strcmp(key, "update_slices")) *value = M->update_slices;
     else if (!std::strcmp(key, "update_early")) *value = M->update_early;
+    else if (!std::strcmp(key, "pap_in_update")) *value = pap_upd_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "resident_mb")) *value = resident_mb_effective(M);
     else if (!std::strcmp(key, "redund")) *value = redund_effective(M, 2) ? 1 : 0;  // off unless set

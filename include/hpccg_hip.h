@@ -137,7 +137,8 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  * depth, 2..64; -1 auto (default): 32 for matrix images over 512 MB, else 8;
  * a longer ring allocates more p buffers),
  * "update_slices" (1, 2, 4 or 8 slices per loop-update workgroup, default 1), "update_early" (1 = the one-slice
- * loop update loads Ap and r before its iteration test; same values), "rev_update" (1 = the update kernel walks each
+ * loop update loads Ap and r before its iteration test; same values), "pap_in_update" (1 = every loop-update workgroup
+ * sums the SpMV's p.Ap slice partials itself, one rank and at most 64 groups of 64 slices; same values), "rev_update" (1 = the update kernel walks each
  * XCD's slices backwards, default), "resident_mb" (non-temporal SpMV kernels:
  * this many MB of leading slices per XCD use default-policy loads so they can
  * stay in the Infinity Cache; -1 auto = 128 for images up to 400 MB, else 0),

@@ -147,14 +147,18 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
     M.set_option("update_slices", 1)
-    # the one-slice update with Ap and r loaded before its iteration test
-    for ue, fold, defer in itertools.product((1, 0), (1, 2), (1, 0)):
-        M.set_option("update_early", ue)
+    # the one-slice update with Ap and r loaded before its iteration test, or
+    # forming p.Ap itself from the SpMV's partials (no p.Ap tickets or finalize)
+    for ue, fold, defer in itertools.product((1, 0, 2), (1, 2, 3), (1, 0)):
+        M.set_option("update_early", ue == 1)
+        M.set_option("pap_in_update", ue == 2)
+        assert M.get_option("pap_in_update") == (ue == 2)
         M.set_option("fold", fold)
         M.set_option("x_defer", defer)
         x = prob.x
         _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
         results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    M.set_option("pap_in_update", 0)
     assert all(r == results[0] for r in results)
 
 
