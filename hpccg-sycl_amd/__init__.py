@@ -99,6 +99,9 @@ def lib() -> C.CDLL:
         "hpccg_hip_ddot": (ip, [ip, vp, vp, PD]),
         "hpccg_hip_waxpby": (ip, [ip, dp, vp, dp, vp, vp]),
         "hpccg_hip_HPCCG": (ip, [C.POINTER(_HPCMatrix), vp, vp, ip, dp, PI, PD, PD]),
+        "hpccg_hip_dropin_release": (ip, [C.POINTER(_HPCMatrix)]),
+        "hpccg_hip_dropin_cached": (ip, [C.POINTER(_HPCMatrix)]),
+        "hpccg_hip_set_keep_sell": (ip, [ip]),
         "hpccg_sell_build": (lp, [ip, lp, lp, vp, vp, vp, vp, vp, vp]),
         "hpccg_halo_plan": (ip, [ip, ip, ip, vp, vp, PI]),
         "hpccg_slab_plan": (ip, [ip, ip, PI, PI]),
@@ -225,6 +228,18 @@ def set_halo_mode(mode: int) -> None:
     _check(lib().hpccg_hip_set_halo_mode(mode), "set_halo_mode")
 
 
+def set_keep_sell(keep: bool) -> None:
+    """Matrices created afterwards keep their SELL-512 image beside SELL-512-A
+    (kernel A/B comparisons only; default off)."""
+    _check(lib().hpccg_hip_set_keep_sell(int(keep)), "set_keep_sell")
+
+
+SPMV_SELL, SPMV_DIRECT, SPMV_PAIRS = 0, 1, 2
+SPMV_KERNEL_NAMES = {0: "SELL-512 (int32 columns, x gathered)",
+                     1: "SELL-512-A (offset-aligned slots, x read at the slice's offsets)",
+                     2: "SELL-512-A (offset-aligned slots, x from LDS windows shared by slice pairs)"}
+
+
 # ---------------------------------------------------------------------------
 # device matrix
 # ---------------------------------------------------------------------------
@@ -262,7 +277,7 @@ class Matrix:
         a = (C.c_longlong * 8)()
         _check(lib().hpccg_hip_matrix_info(self.h, a), "matrix_info")
         return {"nrow": a[0], "ncol": a[1], "nnz": a[2], "slots": a[3], "ghost_lo": a[4],
-                "ghost_hi": a[5], "spmv_variant": a[6], "uniform_width": a[7]}
+                "ghost_hi": a[5], "spmv_kernel": a[6], "uniform_width": a[7]}
 
     def vectors(self):
         """Device pointers (b, x0, xexact) of a device-generated matrix."""
@@ -286,10 +301,11 @@ class Matrix:
         return {"spmv_ms": out[0], "spmv_launches": int(out[1]), "update_ms": out[2],
                 "update_launches": int(out[3])}
 
-    def diag_spmv(self, variant: int, reps: int = 20) -> float:
-        """Average us per launch of SpMV variant (diagnostic sweep)."""
+    def diag_spmv(self, kernel: int, reps: int = 20) -> float:
+        """Average us per launch of an SpMV kernel (0 SELL-512, 1 SELL-512-A
+        direct, 2 SELL-512-A pair windows), prologue form (diagnostics)."""
         us = C.c_double(0.0)
-        _check(lib().hpccg_hip_diag_spmv(self.h, variant, reps, C.byref(us)), "diag_spmv")
+        _check(lib().hpccg_hip_diag_spmv(self.h, kernel, reps, C.byref(us)), "diag_spmv")
         return us.value
 
     def last_trace(self, cap: int = 100000) -> np.ndarray:
@@ -307,6 +323,21 @@ class Matrix:
             self.close()
         except Exception:
             pass
+
+
+def dropin_HPCCG(prob: Problem, x: np.ndarray, max_iter: int = 500, tolerance: float = 0.0):
+    """The C drop-in hpccg_hip_HPCCG (HPCCG.hpp:61-63 signature) on a host
+    problem: device matrix cached per HPC_Sparse_Matrix (address + content
+    fingerprint). Returns (ierr, niters, normr, times)."""
+    it = C.c_int(0)
+    nr = C.c_double(0.0)
+    times = np.zeros(7, np.float64)
+    b = np.ascontiguousarray(prob.b, np.float64)
+    assert x.dtype == np.float64 and x.flags.c_contiguous
+    rc = lib().hpccg_hip_HPCCG(prob.A, b.ctypes.data, x.ctypes.data, max_iter, tolerance, C.byref(it),
+                               C.byref(nr), times.ctypes.data_as(C.POINTER(C.c_double)))
+    _check(rc, "hpccg_hip_HPCCG")
+    return rc, it.value, nr.value, times
 
 
 def HPCCG(M: Matrix, b, x, max_iter: int = 500, tolerance: float = 0.0, print_residuals=False,

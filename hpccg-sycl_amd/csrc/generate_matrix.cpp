@@ -35,6 +35,7 @@ inline int stencil_row_len(int ix, int iy, int nx, int ny, long long grow, long 
 void destroyMatrix(HPC_Sparse_Matrix*& A)
 {
     if (!A) return;
+    hpccg_hip_dropin_release(A);  // a later matrix at this address is a new one
     delete[] A->title;
     delete[] A->nnz_in_row;
     delete[] A->list_of_vals;

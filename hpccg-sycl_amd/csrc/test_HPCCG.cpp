@@ -130,7 +130,8 @@ int main(int argc, char* argv[])
             die("generate_matrix");
         if (hpccg_hip_matrix_create(A, &M)) die("matrix upload");
     }
-    if (env_int("HPCCG_VALUE_CODES", 0) && hpccg_hip_set_option(M, "value_codes", 1)) die("value_codes");
+    if (env_int("HPCCG_SPMV_KERNEL", -1) >= 0 && hpccg_hip_set_option(M, "spmv_kernel", env_int("HPCCG_SPMV_KERNEL", -1)))
+        die("spmv_kernel");
     times[6] = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
 
     int niters = 0;
@@ -247,7 +248,8 @@ int main(int argc, char* argv[])
         gs->add("Compute units", cus);
         gs->add("GPU ranks", size);
         gs->add("Stored nonzeros per rank", (long long)info[2]);
-        gs->add("SELL-512 slots per rank", (long long)info[3]);
+        gs->add("Matrix slots per rank", (long long)info[3]);
+        gs->add("SpMV kernel", info[6] == 2 ? "SELL-512-A pair windows" : (info[6] == 1 ? "SELL-512-A direct" : "SELL-512"));
         gs->add("CG iterations per second", times[0] > 0 ? fniters / times[0] : 0.0);
         gs->add("SPARSEMV effective GB/s per rank", gbs);
         gs->add("SPARSEMV fraction of 8 TB/s HBM peak", gbs / 8000.0);

@@ -8,13 +8,14 @@
  * error path (HPCCG.cpp:401 always returns 0; fatal conditions abort).
  *
  * Layout on the device (per GPU / rank):
- *   matrix   SELL-512: slices of 512 consecutive rows, slot-major inside a
- *            slice (vals[slice][slot][512] fp64, cols[...] int32, padding
- *            col = -1); slice width = max row length in the slice; entry
- *            order per row is the caller's order (so rounding matches).
- *            SELL-512-L adds per-slice x windows staged in LDS; SELL-512-C
- *            replaces the column by a 1-byte code into a per-slice dictionary
- *            of (column - row) offsets (9 B per stored entry). DESIGN.md 3.
+ *   matrix   SELL-512-A where it applies (every slice has at most 32 distinct
+ *            column - row offsets and every row's columns ascend: stencils):
+ *            slices of 512 consecutive rows, slot j of a slice holds every
+ *            row's entry at the slice's j-th smallest offset (0.0 where the row
+ *            has none), fp64, 8 B per slot, offsets per slice. Otherwise
+ *            SELL-512: slot-major vals[slice][slot][512] fp64 + cols int32
+ *            (padding col = -1). Entry order per row is the caller's order in
+ *            both, so every row sum rounds like the reference. DESIGN.md 3.
  *   vectors  fp64, length padded to a multiple of 512; p carries the halo:
  *            [ghost_lo | local rows | ghost_hi] (z-slab plan) or
  *            [local rows | externals] (gather plan).
@@ -39,7 +40,7 @@ typedef struct hpccg_hip_matrix hpccg_hip_matrix; /* opaque, device resident */
 #define HPCCG_HIP_ENODEV (-6)  /* no HIP device */
 
 /* ---- library ---------------------------------------------------------- */
-int hpccg_hip_abi_version(void);            /* == 1 */
+int hpccg_hip_abi_version(void);            /* == 2 */
 const char* hpccg_hip_last_error(void);     /* thread-local message */
 int hpccg_hip_device_count(int* count);
 int hpccg_hip_set_device(int device);       /* one GPU per rank/process */
@@ -103,7 +104,12 @@ int hpccg_hip_matrix_destroy(hpccg_hip_matrix* M);
  * halo exchange packs p at the requested rows (exchange_externals.cpp:51-131).
  * The device generator always builds slab plans. */
 int hpccg_hip_set_halo_mode(int mode);
-/* nrow, ncol (incl. ghosts), stored nnz, SELL slots (incl. padding). */
+/* Matrices created afterwards keep their SELL-512 image beside SELL-512-A
+ * (process-wide; default 0 frees it once the A image exists). Only for
+ * kernel A/B comparisons ("spmv_kernel" 0 on a stencil matrix). */
+int hpccg_hip_set_keep_sell(int keep);
+/* nrow, ncol (incl. ghosts), stored nnz, matrix slots (incl. padding),
+ * ghost_lo, ghost_hi, SpMV kernel, uniform slot count (0 = per slice). */
 int hpccg_hip_matrix_info(const hpccg_hip_matrix* M, long long info_out[8]);
 /* Device pointers owned by M: b, x0 (zeros) and xexact of a generated matrix. */
 int hpccg_hip_matrix_vectors(hpccg_hip_matrix* M, double** b_dev, double** x0_dev,
@@ -125,30 +131,33 @@ int hpccg_hip_solve_device(hpccg_hip_matrix* M, const double* b_dev, double* x_d
 /* normr computed in each iteration of the last solve: out[0] = initial
  * residual, out[k] = iteration k (k <= niters). Returns entries written. */
 int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
-/* Solver knobs: "use_graph" (capture CG iterations in a hipGraph; default
- * on for nranks == 1), "spmv_variant" (SpMV kernel, see hpccg_kernels.hip),
- * "event_timing" (1 = bracket every SpMV and fused-update launch with
- * hipEvents on the solver stream; eager launches), "fuse_p" (1 = compute
- * p = r + beta*p inside the SpMV; default on for the SELL-512-L kernels,
- * multi-rank only with those: the halo rows are updated first), "fold" (the last
- * block of the producing kernel completes a dot product: 0 neither, 1 both,
- * 2 p.Ap only, 3 r.r only; -1 auto (default): 2), "x_defer" (1 = x += alpha p batched
- * every x_ring iterations, default), "x_ring" (p ring length = x deferral
- * depth, 2..64; -1 auto (default): 32 for matrix images over 512 MB, else 8;
- * a longer ring allocates more p buffers),
- * "update_slices" (1, 2, 4 or 8 slices per loop-update workgroup, default 1), "update_early" (1 = the one-slice
- * loop update loads Ap and r before its iteration test; same values), "pap_in_update" (1 = every loop-update workgroup
- * sums the SpMV's p.Ap slice partials itself, one rank and at most 64 groups of 64 slices; same values), "rev_update" (1 = the update kernel walks each
- * XCD's slices backwards, default), "resident_mb" (non-temporal SpMV kernels:
- * this many MB of leading slices per XCD use default-policy loads so they can
- * stay in the Infinity Cache; -1 auto = 128 for images up to 400 MB, else 0),
- * "value_codes" (1 = choose a SELL-512-V kernel when every slice has at most
- * 255 distinct (column - row, value) pairs: values come from a per-slice
- * dictionary, ~1 B per stored entry instead of 9; default 0 = every stored
- * value is streamed from HBM each iteration; get: 1 if a V kernel is in use;
- * "value_codes_available" (get only) 1 if the V image was built).
- * None of them
- * changes a computed value: fuse_p/fold on and off are bitwise equal. */
+/* Solver knobs (set / get):
+ *   "spmv_kernel"   -1 auto (default), 0 SELL-512 gather, 1 SELL-512-A with x
+ *                   read at the slice's offsets, 2 SELL-512-A with x from LDS
+ *                   windows shared by slice pairs; get: the kernel in use
+ *   "use_graph"     replay CG iterations from hipGraphs (default 1; every rank
+ *                   count, RCCL calls captured; falls back to eager launches if
+ *                   the capture is refused); get "graph_used": the last solve did
+ *   "graph_chunk"   iterations per graph (default 8; a multiple of the p ring
+ *                   when a halo is exchanged)
+ *   "event_timing"  1 = eager launches with hipEvents around every SpMV and
+ *                   update (hpccg_hip_kernel_times)
+ *   "fuse_p"        -1 auto / 0 off: p = r + beta p formed inside the SpMV
+ *                   (pair kernel: any rank count; direct kernel: one rank)
+ *   "fold"          dots completed by the last block of the producing kernel:
+ *                   0 neither, 1 both, 2 p.Ap only (auto), 3 r.r only
+ *   "x_defer"       1 = x += alpha p batched every x_ring iterations (default)
+ *   "x_ring"        p ring length = x deferral depth, 2..64; -1 auto: 32 for
+ *                   matrix images over 512 MB, else 8
+ *   "rev_update"    1 = the update kernel walks each XCD's slices backwards
+ *   "overlap"       1 = multi-rank: halo exchange beside the interior SpMV
+ *   "force_comm"    diagnostics: route the two CG scalars through the RCCL
+ *                   communicator even with one rank (exercises the all-reduce
+ *                   path, captured in the graph)
+ * get only: "has_sell", "has_a", "has_pairs", "a_width", "lds_doubles", "nt",
+ * "halo_mode", "num_external", "overlap", "device_bytes" (device memory M
+ * holds). None of the knobs changes a computed value: every kernel, fusion and
+ * fold setting gives the same bits. */
 int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value);
 int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* value);
 /* hipEvent kernel timings of the last solve with event_timing on:
@@ -156,8 +165,9 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
  * out[3] update launches (launches that did work, i.e. <= niters + 1). */
 int hpccg_hip_kernel_times(const hpccg_hip_matrix* M, double out[4]);
 /* Diagnostic: average duration (hipEvents, solver stream) of `reps`
- * back-to-back launches of SpMV variant `variant` on the resident p. */
-int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int variant, int reps, double* avg_us);
+ * back-to-back launches of SpMV kernel `kernel` (prologue form) on the
+ * resident p. */
+int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_us);
 
 /* ---- in-process rank group --------------------------------------------------
  * The z-slab decomposition of one process's RCCL job (make_local_matrix.cpp
@@ -193,10 +203,18 @@ int hpccg_hip_ddot(int n, const double* x_dev, const double* y_dev, double* resu
 int hpccg_hip_waxpby(int n, double alpha, const double* x_dev, double beta, const double* y_dev,
                      double* w_dev);
 
-/* ---- drop-in driver: HPCCG.hpp:61-63 with C linkage. Prepares (and caches
- * by A) the device matrix, then runs hpccg_hip_solve. --------------------- */
+/* ---- drop-in driver: HPCCG.hpp:61-63 with C linkage. Prepares the device
+ * matrix (cached per A: keyed by the address AND a fingerprint of the sizes,
+ * row lengths, column indices and values, so a matrix re-created at the same
+ * address or edited in place is converted again), then runs hpccg_hip_solve.
+ * A localised matrix (local_ncol > local_nrow) is refused (HPCCG_HIP_EPLAN). */
 int hpccg_hip_HPCCG(struct HPC_Sparse_Matrix_STRUCT* A, double* b, double* x, int max_iter,
                     double tolerance, int* niters, double* normr, double* times);
+/* Frees the cached device matrix of A (destroyMatrix of this package calls
+ * it); returns 1 if there was one. */
+int hpccg_hip_dropin_release(const struct HPC_Sparse_Matrix_STRUCT* A);
+/* 1 if a device matrix is cached for A. */
+int hpccg_hip_dropin_cached(const struct HPC_Sparse_Matrix_STRUCT* A);
 
 /* ---- host-only helpers (no GPU needed; used by the CPU test suite) -------
  * Converts CSR rows [0, nrow) with global columns into the SELL-512 image the

@@ -45,6 +45,15 @@ RTRANS_CUTOFF = 1e-20
 
 
 CONVERGED_REL = 1e-15
+# SURVEY 8c(4) asks |log10(normr_gpu / normr_ref)| <= 1 for the final residual.
+# Stated deviation: that bar is applied only above the noise floor
+# (normr_ref / normr0 > 1e-15), where check_final requires more (equal niters
+# and 1e-4 relative). Below it the recurrence is rounding noise and the ratio
+# is not a property of the implementation: the reference's own OpenMP build
+# against its serial build gives ratios up to 10^1.14 (21 runs per case, see
+# check_final), and the 8-rank summation order of 16x16x128 gives 10^2.13
+# (1.76e-112 vs 2.35e-110, both ~1e-114 of normr0; GPU run of this round).
+# There both runs must be in the noise regime instead.
 
 
 def first_converged(tr):
@@ -70,6 +79,9 @@ def check_final(niters, normr, tr_test, ref_niters, ref_normr, ref_trace, max_it
       * both final residuals <= 1e-15 * normr0 (0 = underflow) whenever the
         reference's is;
       * the first converged iteration agrees within +-2.
+    This replaces SURVEY 8c(4)'s |log10(normr_gpu/normr_ref)| <= 1 in the
+    noise regime (stated deviation, see the comment above CONVERGED_REL's
+    use); above it the check is stricter than 8c(4).
     """
     full = max_iter - 1
     r0 = tr_test[0]
@@ -103,6 +115,27 @@ def check_trace(tr_test, tr_ref, rtol):
         assert abs(rt - rr) <= rtol * rr, (k, rt, rr, abs(rt - rr) / rr)
         checked += 1
     return checked
+
+
+def kat2_rr0(nx, ny, nz, s7=False):
+    """KAT-2: rtrans_0 = sum over rows of b_i^2 = (28 - nnz_i)^2
+    (generate_matrix.cpp:259-286), exact in integers. 27-pt: nnz_i is the
+    product of the per-axis counts (2 at a face, 3 inside, 1 on a 1-wide
+    axis); 7-pt: 1 + the per-axis neighbour counts."""
+    def axis(n):
+        c = np.full(n, 3, np.int64)
+        c[0] -= 1
+        c[-1] -= 1
+        if n == 1:
+            c[0] = 1
+        return np.unique(c, return_counts=True)
+    tot = 0
+    for cx, nx_ in zip(*axis(nx)):
+        for cy, ny_ in zip(*axis(ny)):
+            for cz, nz_ in zip(*axis(nz)):
+                nnz = (cx - 1) + (cy - 1) + (cz - 1) + 1 if s7 else cx * cy * cz
+                tot += int(nx_) * int(ny_) * int(nz_) * (28 - int(nnz)) ** 2
+    return tot
 
 
 def load_pkg():

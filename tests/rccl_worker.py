@@ -1,0 +1,50 @@
+"""One rank of the 2-process RCCL test (tests/test_gpu_rccl.py): gloo carries
+the unique id, RCCL the data path. Checks the 27pt_8x8x8_x2ranks golden."""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from conftest import (RTRANS_RTOL_MULTI, check_final, check_trace, load_pkg, solve_case,  # noqa: E402
+                      unhex)
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    hp = load_pkg()
+    torch.cuda.set_device(local)
+    hp.set_device(local)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    obj = [hp.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    hp.comm_init(obj[0], world, rank)
+    with open(os.path.join(HERE, "golden", "golden.json")) as f:
+        c = solve_case(json.load(f), "27pt_8x8x8_x2ranks")
+    assert c["ranks"] == world
+    M = hp.Matrix.generate(c["nx"], c["ny"], c["nz"])
+    b, _, _ = M.vectors()
+    n = c["nx"] * c["ny"] * c["nz"]
+    x = torch.zeros(n, dtype=torch.float64, device=f"cuda:{local}")
+    _, it, nr, times = hp.HPCCG(M, b, x, max_iter=500, device=True)
+    tr = M.last_trace()
+    ref_tr = [unhex(t) for t in c["trace_normr"]]
+    rr = c["runs"]["500"]
+    assert tr[0] == ref_tr[0]
+    assert check_trace(tr, ref_tr, RTRANS_RTOL_MULTI) >= 5
+    check_final(it, nr, tr, rr["niters"], unhex(rr["normr"]), ref_tr, 500)
+    assert (x - 1.0).abs().max().item() <= 1e-12
+    assert times[4] > 0.0 and times[5] > 0.0
+    print(f"RCCL-WORKER-OK rank {rank} graph_used={M.get_option('graph_used')}", flush=True)
+    M.close()
+    hp.comm_destroy()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

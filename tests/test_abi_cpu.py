@@ -18,7 +18,7 @@ def test_library_exports_every_declared_symbol(hp):
     assert len(declared) >= 29
     missing = [s for s in declared if not hasattr(L, s)]
     assert not missing, missing
-    assert L.hpccg_hip_abi_version() == 1
+    assert L.hpccg_hip_abi_version() == 2
     # and through the dynamic symbol table
     out = subprocess.run(["nm", "-D", "--defined-only", hp.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout

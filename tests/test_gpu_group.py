@@ -4,15 +4,18 @@ RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so a 1-GPU box
 cannot run the RCCL job itself. hpccg_hip_group_* drives the same z-slab
 ranks from one thread instead: every member is built and solved by the
 multi-rank code path (ghost-localised columns, LDS windows over the ghost
-planes, the allreduced scalars in g, cg_run on all-reduced values), and only
-the transport differs (peer copies of the ghost planes, a rank-ordered sum for
+planes, the all-reduced scalars in g, cg_run on all-reduced values, one
+hipGraph for all members on one device), and only the transport differs (peer copies of the ghost planes, a rank-ordered sum for
 the two scalars). The oracle is the serial reference run of the z-stacked
 global problem (SURVEY 4 "Multi-GPU oracle"; golden cases *_xNranks,
 generate_matrix.cpp:225-229), tolerance RTRANS_RTOL_MULTI."""
+import itertools
+import math
+
 import numpy as np
 import pytest
 
-from conftest import RTRANS_RTOL_MULTI, check_final, check_trace, solve_case, unhex
+from conftest import RTRANS_RTOL_MULTI, check_final, check_trace, kat2_rr0, solve_case, unhex
 
 pytestmark = pytest.mark.gpu
 
@@ -51,53 +54,85 @@ def test_group_matches_global_reference(hp, gpu, golden, name):
 
 
 def test_group_kernel_variants_bitwise(hp, gpu):
-    """Multi-rank SpMV kernels (plain SELL-512, NT, LDS-staged windows that
-    include the ghost planes, 1-byte offset codes, 1-byte (offset, value)
-    codes), the p update fused into the LDS SpMV (halo rows by k_p_boundary
-    first), the halo overlapped with the
-    interior slices, the dot completion modes and the deferred x update give
-    the same bits."""
-    Ms = hp.group_generate(24, 20, 9, 3)
+    """Multi-rank SpMV kernels (SELL-512 gather, SELL-512-A direct, SELL-512-A
+    pair windows whose windows include the ghost planes), the p update fused
+    into the pair kernel (halo rows by k_p_boundary first), the halo
+    overlapped with the interior units, the dot completion modes, the deferred
+    x update and graph replay give the same bits."""
+    hp.set_keep_sell(True)
+    try:
+        Ms = hp.group_generate(24, 20, 9, 3)
+    finally:
+        hp.set_keep_sell(False)
     ref = None
-    import itertools
-    for v, fold, fuse, defer, ovl in itertools.product((1000, 0, 2000, 2100, 4200, 5200, 7201, 8200, 8500, 8800, 8900, 8910, 8963, 8983),
-                                                       (0, 1, 2), (0, 1), (0, 1),
-                                                      (0, 1)):
+    for kernel, fold, fuse, defer, ovl, graph in itertools.product((2, 1, 0), (0, 1, 2), (0, -1), (0, 1),
+                                                                   (0, 1), (0, 1)):
         for M in Ms:
-            M.set_option("spmv_variant", v)
+            M.set_option("spmv_kernel", kernel)
             M.set_option("fold", fold)
             M.set_option("fuse_p", fuse)
             M.set_option("x_defer", defer)
             M.set_option("overlap", ovl)  # halo on the second stream beside the interior SpMV
-        if v >= 2000 and fuse:
+            M.set_option("use_graph", graph)
+        if kernel > 0:
             assert Ms[1].get_option("overlap") == ovl
-        # p = r + beta p inside the SpMV: LDS kernels only on multiple ranks
-        lds = 2000 <= v < 3000 or 4000 <= v < 6000 or 8000 <= v < 8500 or 8900 <= v < 9000
-        assert Ms[1].get_option("fuse_p") == (fuse if lds else 0)
+        # p = r + beta p inside the SpMV: the pair kernel only on multiple ranks
+        assert Ms[1].get_option("fuse_p") == (1 if (fuse and kernel == 2) else 0)
         niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
+        if graph:
+            assert Ms[0].get_option("graph_used") == 1
         got = (niters, normr, Ms[0].last_trace().tobytes(), b"".join(x.tobytes() for x in xs))
         if ref is None:
             ref = got
         if got != ref:  # (a plain assert would diff megabytes of bytes)
-            pytest.fail(f"{(v, fold, fuse, defer, ovl)}: niters {got[0]} vs {ref[0]}, normr {got[1]} vs {ref[1]}, "
-                        f"trace equal {got[2] == ref[2]}")
-    # several slices per update workgroup (r.r folded or not) and the x ring length
-    for v, um, ring, fold in ((8200, 4, 5, 1), (8236, 8, 16, 3), (8500, 2, -1, 2), (8200, 1, 32, 0),
-                              (8900, 4, 16, 2), (8700, 1, 8, 2)):
+            pytest.fail(f"{(kernel, fold, fuse, defer, ovl, graph)}: niters {got[0]} vs {ref[0]}, normr {got[1]} "
+                        f"vs {ref[1]}, trace equal {got[2] == ref[2]}")
+    # the x ring length and graph chunk (a multiple of the ring with a halo)
+    for ring, chunk, fold in ((5, 8, 1), (16, 3, 3), (-1, 8, 2), (32, 1, 0), (2, 13, 2)):
         for M in Ms:
-            M.set_option("spmv_variant", v)
-            M.set_option("fuse_p", 1)
+            M.set_option("spmv_kernel", -1)
+            M.set_option("fuse_p", -1)
             M.set_option("overlap", 1)
             M.set_option("x_defer", 1)
-            M.set_option("update_slices", um)
             M.set_option("x_ring", ring)
+            M.set_option("graph_chunk", chunk)
             M.set_option("fold", fold)
         niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
         got = (niters, normr, Ms[0].last_trace().tobytes(), b"".join(x.tobytes() for x in xs))
         if got != ref:
-            pytest.fail(f"{(v, um, ring, fold)}: niters {got[0]} vs {ref[0]}, normr {got[1]} vs {ref[1]}")
+            pytest.fail(f"{(ring, chunk, fold)}: niters {got[0]} vs {ref[0]}, normr {got[1]} vs {ref[1]}")
     assert Ms[0].get_option("lds_doubles") > 0
 
+
+def test_group_8x200_weak_scaled(hp, gpu):
+    """BASELINE configs[3] on the HIP path: 8 z-stacked ranks of local 200^3
+    (global 200 x 200 x 1600, generate_matrix.cpp:225-229), every rank the
+    multi-rank kernels (pair windows over the ghost planes, overlapped halo,
+    all-reduced scalars), all eight on this one GPU (about 4.2 GB each),
+    graph-replayed. KAT-4 on the global nnz, KAT-2 (rtrans_0 exact), the full
+    499 iterations, one trace on every rank, the final residual and x."""
+    import torch
+    P, nx = 8, 200
+    Ms = hp.group_generate(nx, nx, nx, P)
+    nnz = sum(M.info()["nnz"] for M in Ms)
+    assert nnz == 1715783992  # SURVEY 8: (3*200-2)^2 * (3*1600-2)
+    for r, M in enumerate(Ms):
+        assert M.get_option("spmv_kernel") == 2 and M.get_option("overlap") == 1
+        assert M.get_option("device_bytes") <= 4.6e9
+    niters, normr, xs, times = _solve_group(hp, Ms, max_iter=500)
+    assert Ms[0].get_option("graph_used") == 1
+    assert niters == 499
+    tr = Ms[0].last_trace()
+    for M in Ms[1:]:
+        assert np.array_equal(M.last_trace(), tr)
+    assert tr[0] == math.sqrt(kat2_rr0(nx, nx, P * nx))
+    assert normr / tr[0] <= 1e-15
+    assert max(np.max(np.abs(x - 1.0)) for x in xs) <= 1e-12
+    assert times[4] > 0.0 and times[5] > 0.0
+    del xs
+    for M in Ms:
+        M.close()
+    torch.cuda.empty_cache()
 
 
 def test_group_from_host_csr_equals_device_generator(hp, gpu):

@@ -9,18 +9,23 @@ All calls go through the C ABI (libhpccg_hip.so). Bars:
   every k with rtrans_ref,k >= 1e-20 * rtrans_ref,0; final relative residual
   <= 1e-15 (or underflow to 0 exactly where the reference underflows);
   |x - 1|_inf <= 1e-12.
+Every SpMV kernel (SELL-512, SELL-512-A direct, SELL-512-A pair windows), the
+fused p update, the dot folding, graph replay and the x deferral change where
+work happens, never a value: the tests below require bitwise equal solves.
 """
+import itertools
 import math
 
 import numpy as np
 import pytest
 
 import oracle
-from conftest import (RTRANS_RTOL_1GPU, check_final, check_trace, solve_case, unb64, unhex)
+from conftest import (RTRANS_RTOL_1GPU, check_final, check_trace, kat2_rr0, solve_case, unb64, unhex)
 
 pytestmark = pytest.mark.gpu
 
 DDOT_RTOL = 1e-13
+SELL, DIRECT, PAIRS = 0, 1, 2
 
 
 def dev(torch_device, a):
@@ -32,14 +37,38 @@ def host(t):
     return t.cpu().numpy()
 
 
+@pytest.fixture
+def keep_sell(hp):
+    """Matrices created inside the test keep SELL-512 beside SELL-512-A, so the
+    three kernels can be compared on one matrix."""
+    hp.set_keep_sell(True)
+    yield
+    hp.set_keep_sell(False)
+
+
+def solve_bits(hp, M, b, max_iter, gpu=None):
+    """(niters, normr, trace bytes, x bytes) of one solve from x0 = 0."""
+    if gpu is None:
+        x = np.zeros(len(b))
+        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=max_iter)
+        return it, nr, M.last_trace().tobytes(), x.tobytes()
+    import torch
+    n = M.info()["nrow"]
+    x = torch.zeros(n, dtype=torch.float64, device=gpu)
+    _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=max_iter, device=True)
+    return it, nr, M.last_trace().tobytes(), host(x).tobytes()
+
+
 # ---------------------------------------------------------------------------
 # kernel level
 # ---------------------------------------------------------------------------
-def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
+@pytest.mark.parametrize("kernel", [SELL, DIRECT])
+def test_sparsemv_bitwise_vs_reference(hp, gpu, golden, keep_sell, kernel):
     import torch
     k = golden["kernels_20x20x20"]
     prob = hp.generate_matrix(20, 20, 20)
     M = hp.Matrix.from_hpc(prob)
+    M.set_option("spmv_kernel", kernel)
     v = dev(gpu, unb64(k["v_b64"]))
     y = torch.zeros_like(v)
     hp.HPC_sparsemv(M, v, y)
@@ -52,113 +81,60 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden):
     assert np.array_equal(host(y), prob.b)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 27, 327, 427, 1000, 1001, 1002, 1027, 2000, 2001,
-                                     2002, 2100, 2200, 2208, 2300, 2308, 3000, 3001, 3002, 3100,
-                                     4000, 4200, 4300, 3027, 5000, 5100, 5200, 5208, 5300, 5308,
-                                     5401, 5404, 5204, 6000, 6100, 6104, 6001, 7001, 7101, 7002,
-                                     7102, 7027, 7127, 7201, 7202, 7301, 7302, 7204, 8000, 8200,
-                                     8208, 8300, 8201, 8500, 8501, 8600, 8700, 8727, 8800,
-                                     8900, 8902, 8910, 8927, 8947, 8737, 8757, 8837, 8857,
-                                     8236, 8246, 8336, 8960, 8962, 8970, 8961, 8963,
-                                     8965, 8966, 8967, 8968, 8980, 8982, 8983, 8972, 8973, 8974])
-def test_sparsemv_variants_agree(hp, gpu, variant):
-    """Every SpMV variant computes every row bitwise identically; variants with
-    the same rows-per-thread (all but 1 and 2) also share the p.Ap summation
-    tree, so their CG traces are bitwise equal; 1 and 2 stay in tolerance."""
-    prob = hp.generate_matrix(24, 20, 18)
+@pytest.mark.parametrize("dims,s7", [((24, 20, 18), False), ((13, 7, 5), False), ((40, 40, 40), False),
+                                     ((32, 16, 40), True), ((17, 9, 11), True)])
+def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
+    """SELL-512 gather, SELL-512-A direct and SELL-512-A pair windows, with the
+    p update separate or formed inside the SpMV, give bitwise the same solve
+    (same row sums, same p.Ap tree)."""
+    prob = hp.generate_matrix(*dims, use_7pt=s7)
     M = hp.Matrix.from_hpc(prob)
-    M.set_option("spmv_variant", variant)
-    x = prob.x
-    _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=60)
-    tr = M.last_trace()
-    M.set_option("spmv_variant", 1000)
-    x0 = prob.x
-    _, it0, nr0, _ = hp.HPCCG(M, prob.b, x0, max_iter=60)
-    assert it == it0
-    if variant in (1, 2, 1001, 1002, 2001, 2002, 3001, 3002, 5401, 5404, 5204, 6104, 6001, 8201, 8501):
-        assert check_trace(tr, M.last_trace(), RTRANS_RTOL_1GPU) > 10
-    else:
-        assert nr == nr0
-        assert np.array_equal(tr, M.last_trace())
-        assert np.array_equal(x, x0)
+    assert M.get_option("has_a") == 1 and M.get_option("has_pairs") == 1 and M.get_option("has_sell") == 1
+    assert M.get_option("a_width") == (7 if s7 else 27)
+    out = {}
+    for kernel, fuse in itertools.product((SELL, DIRECT, PAIRS), (0, -1)):
+        M.set_option("spmv_kernel", kernel)
+        M.set_option("fuse_p", fuse)
+        assert M.get_option("spmv_kernel") == kernel
+        assert M.get_option("fuse_p") == (1 if (fuse and kernel != SELL) else 0)
+        out[(kernel, fuse)] = solve_bits(hp, M, prob.b, 120)
+    assert all(o == out[(SELL, 0)] for o in out.values())
 
 
 @pytest.mark.parametrize("dims", [(24, 20, 18), (13, 7, 5), (40, 40, 40)])
 def test_fusion_options_bitwise_equal(hp, gpu, dims):
-    """fuse_p (p update inside the SpMV gather), fold (last-block dot
-    completion) and x_defer (x updated every x_ring iterations) change only where
-    work happens, never a value: every combination, eager and graph launches,
-    gives bitwise the same solve."""
+    """fuse_p, fold (last-block dot completion), graph replay, x_defer and the
+    update's slice order change only where work happens, never a value: every
+    combination gives bitwise the same solve, with the default kernel."""
     prob = hp.generate_matrix(*dims)
     M = hp.Matrix.from_hpc(prob)
     results = []
-    M.set_option("spmv_variant", 1000)  # fuse_p is implemented by the SELL-512 kernels
-    import itertools
-    for fuse, fold, graph, defer, red in itertools.product((0, 1), (0, 1), (0, 1), (0, 1), (0, 1)):
-        M.set_option("fuse_p", fuse)
-        M.set_option("fold", fold)
-        M.set_option("use_graph", graph)
-        M.set_option("x_defer", defer)
-        M.set_option("redund", red)  # consumers complete the dots themselves (fold unused then)
-        M.set_option("rev_update", (fuse + fold + defer) % 2)  # slice order: no value changes
-        x = prob.x
-        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)  # 119 iterations: x updates left for k_xflush
-        assert M.get_option("fuse_p") == fuse
-        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
-    # one dot folded, the other finalized by its own kernel
-    M.set_option("redund", 0)
-    for fold in (2, 3):
-        M.set_option("fold", fold)
-        x = prob.x
-        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
-        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
-    # and the LDS kernels (same rows per thread), fused or not, give the same bits
-    for v, fuse in itertools.product((2000, 2100, 2200, 2308, 3000, 3100, 4200, 4300, 5200, 5300, 6000, 6100,
-                                      7001, 7102, 8000, 8200, 8300, 8500, 8600, 8700, 8800, 8900, 8910, 8960),
-                                     (0, 1)):
-        M.set_option("spmv_variant", v)
-        M.set_option("fuse_p", fuse)
-        M.set_option("redund", 1 - fuse)
-        M.set_option("resident_mb", fuse)  # 1 MB on default-policy loads: no value changes
-        assert M.get_option("fuse_p") == fuse
-        x = prob.x
-        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
-        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
+    for kernel in (DIRECT, PAIRS):
+        M.set_option("spmv_kernel", kernel)
+        for fuse, fold, graph, defer in itertools.product((0, -1), (0, 1, 2, 3), (0, 1), (0, 1)):
+            M.set_option("fuse_p", fuse)
+            M.set_option("fold", fold)
+            M.set_option("use_graph", graph)
+            M.set_option("x_defer", defer)
+            M.set_option("rev_update", (fold + defer) % 2)
+            assert M.get_option("fold") == fold
+            # 119 iterations: x updates left for k_xflush
+            results.append(solve_bits(hp, M, prob.b, 120))
+            if graph:
+                assert M.get_option("graph_used") == 1
     # the x-deferral depth (p ring length) only moves when x is written:
     # rings of 2 .. 64, 119 iterations leave 1 .. 55 updates for k_xflush
-    M.set_option("spmv_variant", 8200)
-    M.set_option("redund", 0)
     M.set_option("x_defer", 1)
+    M.set_option("fold", -1)
     for ring, graph in ((2, 1), (5, 0), (16, 1), (32, 1), (64, 0), (8, 1), (-1, 1)):
         M.set_option("x_ring", ring)
         M.set_option("use_graph", graph)
         assert M.get_option("x_ring") == (ring if ring > 0 else 8)  # auto: 8 for a small image
-        x = prob.x
-        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
-        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
-    # several slices per update workgroup: same partials and tree, r.r folded or not,
-    # x deferred or not, slice count not a multiple of the slices per workgroup
-    for um, fold, defer in itertools.product((2, 4, 8), (1, 2), (1, 0)):
-        M.set_option("update_slices", um)
-        M.set_option("fold", fold)
-        M.set_option("x_defer", defer)
-        assert M.get_option("update_slices") == um
-        x = prob.x
-        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
-        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
-    M.set_option("update_slices", 1)
-    # the one-slice update with Ap and r loaded before its iteration test, or
-    # forming p.Ap itself from the SpMV's partials (no p.Ap tickets or finalize)
-    for ue, fold, defer in itertools.product((1, 0, 2), (1, 2, 3), (1, 0)):
-        M.set_option("update_early", ue == 1)
-        M.set_option("pap_in_update", ue == 2)
-        assert M.get_option("pap_in_update") == (ue == 2)
-        M.set_option("fold", fold)
-        M.set_option("x_defer", defer)
-        x = prob.x
-        _, it, nr, _ = hp.HPCCG(M, prob.b, x, max_iter=120)
-        results.append((it, nr, M.last_trace().tobytes(), x.tobytes()))
-    M.set_option("pap_in_update", 0)
+        results.append(solve_bits(hp, M, prob.b, 120))
+    # graph chunks that do not divide the iteration count (eager tail)
+    for chunk in (1, 3, 13, 64):
+        M.set_option("graph_chunk", chunk)
+        results.append(solve_bits(hp, M, prob.b, 120))
     assert all(r == results[0] for r in results)
 
 
@@ -169,18 +145,15 @@ def test_folded_dot_completion_stress(hp, gpu):
     k_finalize path (data handed over by a kernel boundary)."""
     prob = hp.generate_matrix(64, 64, 48)  # 384 slices -> 6 groups, partial last group
     M = hp.Matrix.from_hpc(prob)
-    M.set_option("redund", 0)
-    M.set_option("fold", 0)
-    x = prob.x
-    hp.HPCCG(M, prob.b, x, max_iter=150)
-    ref = (M.last_trace().tobytes(), x.tobytes())
-    M.set_option("fold", 1)
-    for graph in (1, 0):
-        M.set_option("use_graph", graph)
-        for _ in range(20):
-            x = prob.x
-            hp.HPCCG(M, prob.b, x, max_iter=150)
-            assert (M.last_trace().tobytes(), x.tobytes()) == ref
+    for kernel in (DIRECT, PAIRS):
+        M.set_option("spmv_kernel", kernel)
+        M.set_option("fold", 0)
+        ref = solve_bits(hp, M, prob.b, 150)
+        M.set_option("fold", 1)
+        for graph in (1, 0):
+            M.set_option("use_graph", graph)
+            for _ in range(12):
+                assert solve_bits(hp, M, prob.b, 150) == ref
 
 
 def test_waxpby_bitwise_vs_reference(hp, gpu, golden):
@@ -272,21 +245,18 @@ def test_solve_vs_reference(hp, gpu, golden, name, how):
             assert np.all(np.isfinite(x))
             assert np.max(np.abs(x - 1.0)) <= 1e-12
         assert times[0] > 0
+        # the timer classes (device stamps) partition the solve
+        assert 0.0 <= times[1] + times[2] + times[3] <= times[0] * 1.05 + 1e-3
 
 
 def test_solve_reproducible(hp, gpu):
     prob = hp.generate_matrix(30, 30, 30)
     M = hp.Matrix.from_hpc(prob)
-    res = []
-    for _ in range(2):
-        x = prob.x
-        hp.HPCCG(M, prob.b, x, max_iter=200)
-        res.append((M.last_trace().tobytes(), x.tobytes()))
-    assert res[0] == res[1]
+    assert solve_bits(hp, M, prob.b, 200) == solve_bits(hp, M, prob.b, 200)
 
 
 def test_device_generator_matches_host(hp, gpu):
-    """SURVEY 8(f)#1: the device generator writes the same SELL image."""
+    """SURVEY 8(f)#1: the device generator writes the same image."""
     import torch
     for dims, s7 in [((20, 20, 20), False), ((13, 7, 5), False), ((17, 9, 11), True)]:
         prob = hp.generate_matrix(*dims, use_7pt=s7)
@@ -296,11 +266,8 @@ def test_device_generator_matches_host(hp, gpu):
         b, x0, xe = Md.vectors()
         n = prob.nrow
         bt = torch.empty(n, dtype=torch.float64, device=gpu)
-        import ctypes
-        hp.lib()  # ensure loaded
         torch.cuda.synchronize()
-        # copy device b into a tensor through a waxpby (w = b + 0*b)
-        hp.waxpby(n, 1.0, b, 0.0, b, bt)
+        hp.waxpby(n, 1.0, b, 0.0, b, bt)  # copy device b through w = b + 0*b
         assert np.array_equal(host(bt), prob.b)
         x1 = prob.x
         hp.HPCCG(Mh, prob.b, x1, max_iter=80)
@@ -329,24 +296,18 @@ def test_edge_max_iter_and_tolerance(hp, gpu):
         assert it == ref["niters"], tol
 
 
-def test_csr_entry_and_ragged_rows(hp, gpu):
-    """A general (non-stencil) SPD matrix with ragged row lengths, including an
-    empty-ish row pattern, through the CSR entry point."""
-    rng = np.random.default_rng(7)
-    n = 1500
-    rows = []
-    for i in range(n):
-        k = int(rng.integers(0, 40))
-        cs = np.unique(rng.integers(0, n, size=k))
-        cs = cs[cs != i]
-        rows.append(cs)
-    # symmetrise and make diagonally dominant
+def _random_sym(n, seed, kmax=40):
+    """A general (non-stencil) SPD matrix with ragged row lengths: many
+    distinct offsets per slice, so no SELL-512-A image."""
+    rng = np.random.default_rng(seed)
     import collections
     nb = collections.defaultdict(set)
-    for i, cs in enumerate(rows):
-        for c in cs:
-            nb[i].add(int(c))
-            nb[int(c)].add(i)
+    for i in range(n):
+        k = int(rng.integers(0, kmax))
+        for c in np.unique(rng.integers(0, n, size=k)):
+            if c != i:
+                nb[i].add(int(c))
+                nb[int(c)].add(i)
     row_ptr = [0]
     cols, vals = [], []
     for i in range(n):
@@ -355,12 +316,21 @@ def test_csr_entry_and_ragged_rows(hp, gpu):
             cols.append(c)
             vals.append(float(len(cs) + 1) if c == i else -1.0)
         row_ptr.append(len(cols))
-    row_ptr = np.array(row_ptr, np.int64)
-    cols = np.array(cols, np.int32)
-    vals = np.array(vals, np.float64)
+    return np.array(row_ptr, np.int64), np.array(cols, np.int32), np.array(vals, np.float64)
+
+
+def test_csr_entry_and_ragged_rows(hp, gpu):
+    """A general SPD matrix with ragged row lengths through the CSR entry
+    point: more than 32 offsets per slice, so the SELL-512 kernel runs and the
+    A kernels are refused."""
+    n = 1500
+    row_ptr, cols, vals = _random_sym(n, 7)
     b = np.arange(n, dtype=np.float64) % 13 - 6.0
     A = oracle.CSR(row_ptr, cols, vals, np.zeros(n), b, np.ones(n))
     M = hp.Matrix.from_csr(row_ptr, cols, vals)
+    assert M.get_option("has_a") == 0 and M.get_option("spmv_kernel") == SELL
+    with pytest.raises(hp.HPCCGError, match="not built"):
+        M.set_option("spmv_kernel", DIRECT)
     x = np.zeros(n)
     _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=120)
     ref = oracle.hpccg(A, max_iter=120)
@@ -374,119 +344,72 @@ def test_csr_entry_and_ragged_rows(hp, gpu):
 
 
 # ---------------------------------------------------------------------------
-# BASELINE sizes: size-independent properties (the oracle is too slow there)
+# BASELINE sizes: full-size parity (oracle trace where it finishes in seconds)
+# and size-independent properties
 # ---------------------------------------------------------------------------
-def kat2_rr0(nx, ny, nz):
-    """sum over rows of b_i^2 = (28 - nnz_i)^2, nnz_i a product of per-axis counts
-    (generate_matrix.cpp:259-286); exact in integers."""
-    def axis(n):
-        c = np.full(n, 3, np.int64)
-        c[0] -= 1
-        c[-1] -= 1
-        return np.unique(c, return_counts=True)
-    tot = 0
-    for cx, nx_ in zip(*axis(nx)):
-        for cy, ny_ in zip(*axis(ny)):
-            for cz, nz_ in zip(*axis(nz)):
-                tot += int(nx_) * int(ny_) * int(nz_) * (28 - int(cx * cy * cz)) ** 2
-    return tot
+def _oracle_trace(dims, s7, iters):
+    """The OpenMP oracle's first `iters` iterations on the same matrix."""
+    A = oracle.generate(*dims, use_7pt=s7)
+    ref = oracle.hpccg(A, max_iter=iters + 1, nthreads=max(1, min(16, oracle.max_threads())))
+    del A
+    return ref["trace"]
 
 
-@pytest.mark.parametrize("dims,s7,rr0", [((100, 100, 100), False, 7007848),
-                                         ((200, 200, 200), False, 31896248),
-                                         ((320, 320, 320), False, None)])
-def test_full_size_properties(hp, gpu, dims, s7, rr0):
-    """Full and beyond-BASELINE sizes (320^3: 32.8 M rows, 0.88 G nonzeros,
-    0.88 G SELL slots) through size-independent properties."""
-    if rr0 is None:
-        rr0 = kat2_rr0(*dims)
+@pytest.mark.parametrize("dims,s7,trace_iters", [((100, 100, 100), False, 90),
+                                                  ((200, 200, 200), False, 60),
+                                                  ((256, 256, 256), True, 60),
+                                                  ((320, 320, 320), False, 0)])
+def test_full_size(hp, gpu, dims, s7, trace_iters):
+    """BASELINE sizes (and 320^3: 32.8 M rows, 0.88 G nonzeros) on the default
+    kernel: the first iterations' rtrans against the OpenMP oracle on the same
+    matrix (1e-8), KAT-1 (A*1 == b bitwise), KAT-2 (rtrans_0 exact), KAT-4 (nnz
+    formula), the full 499-iteration solve's final residual and x, and the
+    device footprint (SELL-512 freed once the A image exists)."""
     import torch
     M = hp.Matrix.generate(*dims, use_7pt=s7)
     info = M.info()
     nx, ny, nz = dims
-    assert info["nnz"] == (3 * nx - 2) * (3 * ny - 2) * (3 * nz - 2)  # KAT-4
-    b, x0, xe = M.vectors()
     n = nx * ny * nz
-    # KAT-1 on the device: A*1 == b bitwise
+    if s7:
+        assert info["nnz"] == 7 * n - 2 * (ny * nz + nx * nz + nx * ny)  # KAT-4
+    else:
+        assert info["nnz"] == (3 * nx - 2) * (3 * ny - 2) * (3 * nz - 2)  # KAT-4
+    assert M.get_option("has_a") == 1 and M.get_option("has_sell") == 0
+    # 8 B per slot of the A image, the p ring, r / Ap / x / b and the generated
+    # b / x0 / xexact, and small tables (no SELL-512 image left)
+    ring = M.get_option("x_ring")
+    limit = info["slots"] * 8 + (ring + 7) * (n + 4 * 2048 + 2 * nx * ny) * 8 + 64e6
+    assert M.get_option("device_bytes") <= limit
+    if dims == (200, 200, 200):
+        assert M.get_option("device_bytes") <= 4.5e9  # VERDICT r1: <= 4.5 GB per 200^3 rank
+    b, x0, xe = M.vectors()
     ones = torch.ones(n, dtype=torch.float64, device=gpu)
     y = torch.empty(n, dtype=torch.float64, device=gpu)
     hp.HPC_sparsemv(M, ones, y)
     bt = torch.empty(n, dtype=torch.float64, device=gpu)
     hp.waxpby(n, 1.0, b, 0.0, b, bt)
-    assert torch.equal(y, bt)
+    assert torch.equal(y, bt)  # KAT-1
+    del ones, y, bt
     x = torch.zeros(n, dtype=torch.float64, device=gpu)
     _, it, nr, times = hp.HPCCG(M, b, x, max_iter=500, device=True)
     tr = M.last_trace()
     assert it == 499
-    assert tr[0] == math.sqrt(rr0)  # KAT-2
-    assert nr / tr[0] <= 1e-15
-    err = (x - 1.0).abs().max().item()
-    assert err <= 1e-12
-    # the oracle (OpenMP) for the first iterations at this size
-    if dims[0] == 100:
-        A = oracle.generate(*dims)
-        ref = oracle.hpccg(A, max_iter=90, nthreads=max(1, min(16, oracle.max_threads())))
-        assert check_trace(tr, ref["trace"], RTRANS_RTOL_1GPU) >= 30
-
-
-def test_7pt_256_properties(hp, gpu):
-    import torch
-    dims = (256, 256, 256)
-    M = hp.Matrix.generate(*dims, use_7pt=True)
-    n = 256 ** 3
-    assert M.info()["nnz"] == 7 * n - 2 * 3 * 256 * 256
-    b, _, _ = M.vectors()
-    x = torch.zeros(n, dtype=torch.float64, device=gpu)
-    _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=500, device=True)
-    tr = M.last_trace()
-    assert it == 499
+    assert tr[0] == math.sqrt(kat2_rr0(*dims, s7=s7))  # KAT-2
     assert nr / tr[0] <= 1e-15
     assert (x - 1.0).abs().max().item() <= 1e-12
+    if trace_iters:
+        ref = np.asarray(_oracle_trace(dims, s7, trace_iters))
+        # every leading point above the 1e-20 cutoff (7-pt 256^3 passes it by k = 10)
+        above = int(np.argmax(ref ** 2 < 1e-20 * ref[0] ** 2)) if np.any(ref ** 2 < 1e-20 * ref[0] ** 2) \
+            else len(ref)
+        assert above >= 10
+        assert check_trace(tr, ref, RTRANS_RTOL_1GPU) == min(above, len(tr))
 
 
-def test_sell_c_fallback_for_many_offsets(hp, gpu):
-    """SELL-512-C codes a slice's (column - row) offsets with one byte; a slice
-    with more than 255 distinct offsets cannot, and the library falls back to
-    the int32 SELL-512 kernels (same bits either way)."""
-    n = 20000
-    rows_c, rows_v = [], []
-    for i in range(n):
-        far = (i * 7919 + 13) % n  # a different offset on every row
-        nb = [c for c in (i - 1, i + 1) if 0 <= c < n]
-        cols = [i] + nb + ([far] if far not in nb and far != i else [])
-        rows_c.append(cols)
-        rows_v.append([6.0 if c == i else -1.0 for c in cols])
-    # make it symmetric: add the transpose of the far couplings
-    extra = {}
-    for i in range(n):
-        for c in rows_c[i][3:]:
-            extra.setdefault(c, []).append(i)
-    for c, lst in extra.items():
-        for i in lst:
-            if i not in rows_c[c]:
-                rows_c[c].append(i)
-                rows_v[c].append(-1.0)
-        rows_v[c][0] = 2.0 + len(rows_c[c])
-    rp = np.zeros(n + 1, np.int64)
-    rp[1:] = np.cumsum([len(c) for c in rows_c])
-    cols = np.array([c for r in rows_c for c in r], np.int32)
-    vals = np.array([v for r in rows_v for v in r], np.float64)
-    M = hp.Matrix.from_csr(rp, cols, vals)
-    assert M.get_option("spmv_variant") < 3000  # no SELL-512-C for this image
-    with pytest.raises(hp.HPCCGError, match="SELL-512-C"):
-        M.set_option("spmv_variant", 3000)
-    with pytest.raises(hp.HPCCGError, match="SELL-512-V"):
-        M.set_option("spmv_variant", 6000)
-    b = 1.0 + (np.arange(n) % 5)
-    x = np.zeros(n)
-    _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=30)
-    A = oracle.CSR(rp, cols, vals, np.zeros(n), b, np.zeros(n))
-    ref = oracle.hpccg(A, max_iter=30)
-    assert check_trace(M.last_trace(), ref["trace"], RTRANS_RTOL_1GPU) >= 5
-
-
-@pytest.mark.parametrize("dims", [(1, 1, 1), (2, 1, 1), (3, 2, 1), (1, 1, 700), (31, 1, 1)])
-@pytest.mark.parametrize("s7", [False, True])
+@pytest.mark.parametrize("dims,s7", [((1, 1, 1), False), ((2, 1, 1), False), ((3, 2, 1), False),
+                                     ((1, 1, 700), False), ((31, 1, 1), False), ((1, 1, 1), True),
+                                     ((2, 1, 1), True), ((3, 2, 1), True), ((1, 1, 700), True),
+                                     ((31, 1, 1), True)])
 def test_tiny_and_thin_grids(hp, gpu, dims, s7):
     """Degenerate grids (one row; lines; a slice-straddling 1x1x700 column),
     from the host and the device generator, against the oracle.
@@ -513,7 +436,7 @@ def test_tiny_and_thin_grids(hp, gpu, dims, s7):
             assert np.max(np.abs(x - prob.xexact)) <= 1e-12
 
 
-def _banded(n, vals_of):
+def _banded(n, vals_of, diag_first=True):
     """Symmetric 5-band matrix with the given off-diagonal value per (i, j)."""
     rp = [0]
     cols, vals = [], []
@@ -523,84 +446,17 @@ def _banded(n, vals_of):
             if 0 <= j < n:
                 row.append((j, vals_of(min(i, j), max(i, j))))
         row[0] = (i, 4.5 + 2.0 * sum(abs(v) for _, v in row[1:]))  # well conditioned
+        if not diag_first:
+            row.sort()
         cols += [c for c, _ in row]
         vals += [v for _, v in row]
         rp.append(len(cols))
     return np.array(rp, np.int64), np.array(cols, np.int32), np.array(vals, np.float64)
 
 
-def _solve_all(hp, M, b, variants, max_iter=40):
-    out = {}
-    for v in variants:
-        M.set_option("spmv_variant", v)
-        x = np.zeros(len(b))
-        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=max_iter)
-        out[v] = (it, nr, M.last_trace().tobytes(), x.tobytes())
-    return out
-
-
-def test_sell_v_value_dictionary_edges(hp, gpu):
-    """SELL-512-V codes (offset, value) pairs: keys are the value's bits, so a
-    stored -0.0 and +0.0 are different entries, and tiny/huge magnitudes keep
-    their exact bits. Same solve bits as the SELL-512 kernels."""
-    n = 3000
-    pick = [-1.0, -0.0, 0.0, -1e-300, -3.0e5, -2.0 ** -1074, -0.25]
-    rp, cols, vals = _banded(n, lambda i, j: pick[(i * 3 + j) % len(pick)])
-    M = hp.Matrix.from_csr(rp, cols, vals)
-    assert M.get_option("value_codes") == 0  # opt-in
-    M.set_option("value_codes", 1)
-    assert M.get_option("spmv_variant") >= 5000  # fits: few distinct values per slice
-    b = 1.0 + (np.arange(n) % 7)
-    out = _solve_all(hp, M, b, (1000, 3000, 6000, 6100, 7001, 7102))
-    assert all(o == out[1000] for o in out.values())
-    A = oracle.CSR(rp, cols, vals, np.zeros(n), b, np.zeros(n))
-    ref = oracle.hpccg(A, max_iter=40)
-    assert check_trace(np.frombuffer(out[6000][2]), ref["trace"], RTRANS_RTOL_1GPU) >= 5
-
-
-def test_sell_v_fallback_for_many_values(hp, gpu):
-    """Few offsets but a different value on every row: SELL-512-C fits, the
-    (offset, value) dictionary of SELL-512-V does not (> 255 pairs per
-    slice), and the library keeps the C kernels."""
-    n = 4096
-    rp, cols, vals = _banded(n, lambda i, j: -1.0 - ((i * 131 + j) % 1000) / 1000.0)
-    M = hp.Matrix.from_csr(rp, cols, vals)
-    assert M.get_option("value_codes_available") == 0
-    M.set_option("value_codes", 1)
-    v = M.get_option("spmv_variant")
-    assert 3000 <= v < 5000 or 8000 <= v < 9000  # SELL-512-C or -P, not -V
-    for v in (5200, 6000):
-        with pytest.raises(hp.HPCCGError, match="SELL-512-V"):
-            M.set_option("spmv_variant", v)
-    b = 1.0 + (np.arange(n) % 5)
-    out = _solve_all(hp, M, b, (1000, 3000, 3100))
-    assert all(o == out[1000] for o in out.values())
-
-
-@pytest.mark.parametrize("dims,s7", [((40, 36, 44), False), ((64, 64, 64), True)])
-def test_value_codes_opt_in_bitwise(hp, gpu, dims, s7):
-    """value_codes is off by default (the stored values stream from HBM); on,
-    the generated stencil picks a SELL-512-V kernel and the solve gives the
-    same bits as the default kernel."""
-    M = hp.Matrix.generate(*dims, use_7pt=s7)
-    assert M.get_option("value_codes") == 0 and M.get_option("spmv_variant") >= 8000  # SELL-512-P / -A
-    assert M.get_option("value_codes_available") == 1
-    b, _, _ = M.vectors()
-    import torch
-    outs = []
-    for vc in (0, 1, 0):
-        M.set_option("value_codes", vc)
-        assert M.get_option("value_codes") == vc
-        x = torch.zeros(dims[0] * dims[1] * dims[2], dtype=torch.float64, device=gpu)
-        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=80, device=True)
-        outs.append((it, nr, M.last_trace().tobytes(), host(x).tobytes()))
-    assert outs[0] == outs[1] == outs[2]
-
-
-def _random_patterns(n, seed, noffs=10, band=None, diag_first=True):
+def _random_patterns(n, seed, noffs=10, diag_first=True):
     """Symmetric matrix whose rows each keep a random subset of `noffs`
-    offsets: few distinct offsets per slice (SELL-512-C fits), hundreds of
-    distinct row patterns per 512-row slice."""
+    offsets: few distinct offsets per slice, many holes."""
     rng = np.random.default_rng(seed)
     offs = [1, 2, 3, 5, 8, 13, 21, 34, 55, 89][:noffs]
     nb = [set() for _ in range(n)]
@@ -619,84 +475,68 @@ def _random_patterns(n, seed, noffs=10, band=None, diag_first=True):
     return np.array(rp, np.int64), np.array(cols, np.int32), np.array(vals, np.float64)
 
 
-def test_sell_p_fallback_for_many_patterns(hp, gpu):
-    """Rows with random subsets of 10 offsets: SELL-512-C fits (<= 20 offsets
-    per slice) but a slice has far more than 256 row patterns, so the
-    library keeps the C kernels and refuses the P variants; same bits."""
-    n = 3000
-    rp, cols, vals = _random_patterns(n, 7)
-    M = hp.Matrix.from_csr(rp, cols, vals)
-    assert 3000 <= M.get_option("spmv_variant") < 5000  # diagonal first: no SELL-512-A either
-    for v in (8200, 8500):
-        with pytest.raises(hp.HPCCGError, match="SELL-512-P"):
-            M.set_option("spmv_variant", v)
-    b = 1.0 + (np.arange(n) % 5)
-    out = _solve_all(hp, M, b, (1000, 3000, 3100))
-    assert all(o == out[1000] for o in out.values())
-
-
-def test_sell_p_few_patterns_irregular(hp, gpu):
-    """Rows with random subsets of 3 offsets (at most 8 patterns per slice,
-    irregular order): the P kernels fit and give the SELL-512 bits, and the
-    solve tracks the oracle."""
-    n = 5000
-    rp, cols, vals = _random_patterns(n, 11, noffs=3)
-    M = hp.Matrix.from_csr(rp, cols, vals)
-    b = 1.0 + (np.arange(n) % 7)
-    out = _solve_all(hp, M, b, (1000, 8500, 8600) + ((8200, 8300) if M.get_option("lds_doubles") else ()))
-    assert all(o == out[1000] for o in out.values())
-    A = oracle.CSR(rp, cols, vals, np.zeros(n), b, np.zeros(n))
-    ref = oracle.hpccg(A, max_iter=40)
-    assert check_trace(np.frombuffer(out[1000][2]), ref["trace"], RTRANS_RTOL_1GPU) >= 5
-
-
-def test_sell_a_holes_fused_and_refused(hp, gpu):
+def test_sell_a_holes_and_refusal(hp, gpu, keep_sell):
     """SELL-512-A stores, per slice, one slot per distinct (column - row)
     offset in ascending order, 0.0 where a row has no entry. Rows with random
     offset subsets (many holes, x read past both ends of the vector for the
-    first and last slices) give the SELL-512 bits with the p update separate
-    or formed per load; a matrix whose rows are not in ascending column order
-    (diagonal first) gets no A image, since its sums would round in another
-    order."""
+    first and last slices, a ragged last slice) give the SELL-512 bits on
+    every kernel, fused or not; a matrix whose rows are not in ascending
+    column order (diagonal first) gets no A image, since its sums would round
+    in another order."""
     n = 2600  # 5 full slices + a ragged one
     rp, cols, vals = _random_patterns(n, 5, noffs=10, diag_first=False)
     M = hp.Matrix.from_csr(rp, cols, vals)
+    assert M.get_option("has_a") == 1
     b = 1.0 + (np.arange(n) % 3)
     out = {}
-    for v, fuse in ((1000, 0), (8700, 0), (8700, 1), (8800, 0), (8800, 1), (8900, 0), (8900, 1), (8910, 1),
-                    (8960, 0), (8960, 1), (8983, 0), (8983, 1)):
-        M.set_option("spmv_variant", v)
+    for kernel, fuse in itertools.product((SELL, DIRECT, PAIRS), (0, -1)):
+        M.set_option("spmv_kernel", kernel)
         M.set_option("fuse_p", fuse)
-        assert M.get_option("fuse_p") == fuse
-        x = np.zeros(n)
-        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=70)
-        out[(v, fuse)] = (it, nr, M.last_trace().tobytes(), x.tobytes())
-    assert all(o == out[(1000, 0)] for o in out.values())
-    rp, cols, vals = _banded(1500, lambda i, j: -1.0)
+        out[(kernel, fuse)] = solve_bits(hp, M, b, 70)
+    assert all(o == out[(SELL, 0)] for o in out.values())
+    A = oracle.CSR(rp, cols, vals, np.zeros(n), b, np.zeros(n))
+    ref = oracle.hpccg(A, max_iter=70)
+    assert check_trace(np.frombuffer(out[(SELL, 0)][2]), ref["trace"], RTRANS_RTOL_1GPU) >= 5
+    # rows diagonal first: not ascending -> SELL-512 only
+    rp, cols, vals = _banded(1500, lambda i, j: -1.0, diag_first=True)
     M = hp.Matrix.from_csr(rp, cols, vals)
-    assert not 8700 <= M.get_option("spmv_variant") < 8900
-    with pytest.raises(hp.HPCCGError, match="SELL-512-A"):
-        M.set_option("spmv_variant", 8700)
+    assert M.get_option("has_a") == 0 and M.get_option("spmv_kernel") == SELL
+    with pytest.raises(hp.HPCCGError, match="not built"):
+        M.set_option("spmv_kernel", PAIRS)
+    # the same band sorted: an A image of width 5
+    rp, cols, vals = _banded(1500, lambda i, j: -1.0 - ((i + j) % 5) * 0.25, diag_first=False)
+    M = hp.Matrix.from_csr(rp, cols, vals)
+    assert M.get_option("has_a") == 1 and M.get_option("a_width") == 5
+    b = 1.0 + (np.arange(1500) % 7)
+    A = oracle.CSR(rp, cols, vals, np.zeros(1500), b, np.zeros(1500))
+    ref = oracle.hpccg(A, max_iter=40)
+    got = solve_bits(hp, M, b, 40)
+    assert check_trace(np.frombuffer(got[2]), ref["trace"], RTRANS_RTOL_1GPU) >= 5
 
 
-def test_sell_a_early_loads_7pt(hp, gpu):
-    """The SELL-512-A variants that load a slice's values and offsets before
-    the iteration test (width 7 unrolled, 7-pt stencil) give the SELL-512
-    bits with the p update separate or formed per load; a width-7 variant is
-    refused on a 27-pt image."""
-    dims = (32, 16, 40)  # 40 planes of one slice each, plus the first and last
-    M = hp.Matrix.generate(*dims, use_7pt=True)
-    b, _, _ = M.vectors()
-    import torch
-    n = dims[0] * dims[1] * dims[2]
-    out = {}
-    for v, fuse in ((1000, 0), (8707, 1), (8717, 0), (8717, 1), (8817, 1), (8807, 0)):
-        M.set_option("spmv_variant", v)
-        M.set_option("fuse_p", fuse)
-        x = torch.zeros(n, dtype=torch.float64, device=gpu)
-        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=60, device=True)
-        out[(v, fuse)] = (it, nr, M.last_trace().tobytes(), host(x).tobytes())
-    assert all(o == out[(1000, 0)] for o in out.values())
-    M27 = hp.Matrix.generate(24, 20, 18)
-    with pytest.raises(hp.HPCCGError, match="width"):
-        M27.set_option("spmv_variant", 8717)
+def test_sell_a_offset_limit(hp, gpu):
+    """A slice with more than 32 distinct offsets gets no SELL-512-A image; 32
+    still fit (the limit is per slice, not per matrix)."""
+    for noffs, fits in ((16, True), (40, False)):
+        n = 2048
+        offs = [3 * k + 1 for k in range(noffs // 2)]
+        nb = [set() for _ in range(n)]
+        for i in range(n):
+            for o in offs:
+                if i + o < n:
+                    nb[i].add(i + o)
+                    nb[i + o].add(i)
+        rp, cols, vals = [0], [], []
+        for i in range(n):
+            row = sorted(nb[i] | {i})
+            cols += row
+            vals += [1.0 + len(row) if c == i else -1.0 for c in row]
+            rp.append(len(cols))
+        rp, cols, vals = np.array(rp, np.int64), np.array(cols, np.int32), np.array(vals, np.float64)
+        M = hp.Matrix.from_csr(rp, cols, vals)
+        assert M.get_option("has_a") == int(fits), noffs
+        b = 1.0 + (np.arange(n) % 5)
+        A = oracle.CSR(rp, cols, vals, np.zeros(n), b, np.zeros(n))
+        ref = oracle.hpccg(A, max_iter=30)
+        got = solve_bits(hp, M, b, 30)
+        assert check_trace(np.frombuffer(got[2]), ref["trace"], RTRANS_RTOL_1GPU) >= 5

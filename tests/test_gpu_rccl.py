@@ -1,11 +1,20 @@
-"""RCCL through the library on one GPU: bootstrap (ncclGetUniqueId /
-ncclCommInitRank), an all-reduce on the library's stream and teardown, with a
-1-rank communicator. Two ranks cannot share a GPU under RCCL ("Duplicate GPU
-detected"), so the multi-rank kernels are covered by the in-process group
-(test_gpu_group.py) and the RCCL transport's call pattern by the gloo
-emulation (test_multirank_cpu.py)."""
+"""RCCL through the library: bootstrap (ncclGetUniqueId / ncclCommInitRank),
+an all-reduce on the library's stream and teardown with a 1-rank
+communicator; the CG's two scalars routed through ncclAllReduce inside the
+captured hipGraph (force_comm, 1 rank); and, where two GPUs are visible, the
+real 2-process RCCL job (one rank per GPU, halo by ncclSend/Recv, scalars by
+ncclAllReduce) against the reference's 2-rank golden. Two ranks cannot share
+a GPU under RCCL ("Duplicate GPU detected"), so on a 1-GPU box the multi-rank
+kernels are covered by the in-process group (test_gpu_group.py) and the RCCL
+call pattern by the gloo emulation (test_multirank_cpu.py)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
+
+from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -28,3 +37,46 @@ def test_rccl_one_rank_comm(hp, gpu):
         M.close()
     finally:
         hp.comm_destroy()
+
+
+@pytest.mark.parametrize("graph", [1, 0])
+def test_rccl_scalars_in_graph(hp, gpu, graph):
+    """force_comm: p.Ap and r.r go loc -> ncclAllReduce -> g, as on several
+    ranks, with the RCCL calls captured into the CG hipGraph; a 1-rank sum is
+    the identity, so the solve is bitwise the plain one."""
+    import torch
+    hp.comm_init(hp.comm_unique_id(), 1, 0)
+    try:
+        M = hp.Matrix.generate(40, 36, 30)
+        b, _, _ = M.vectors()
+        outs = []
+        for fc in (0, 1):
+            M.set_option("force_comm", fc)
+            M.set_option("use_graph", graph)
+            x = torch.zeros(40 * 36 * 30, dtype=torch.float64, device=gpu)
+            _, it, nr, times = hp.HPCCG(M, b, x, max_iter=120, device=True)
+            outs.append((it, nr, M.last_trace().tobytes(), x.cpu().numpy().tobytes()))
+            if fc:
+                assert times[4] > 0.0  # the all-reduce class was stamped
+                assert M.get_option("graph_used") == graph
+        assert outs[0] == outs[1]
+        M.close()
+    finally:
+        hp.comm_destroy()
+
+
+def test_rccl_two_processes(hp, gpu, golden):
+    """The RCCL job itself: torch.distributed.run launches 2 ranks, one per
+    GPU; each generates its z-slab of the 2 x 8^3 problem on its GPU and
+    solves with the RCCL halo + all-reduce, graph-replayed; the trace must
+    meet the reference's 2-rank golden (27pt_8x8x8_x2ranks, 1e-7)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two visible GPUs (RCCL refuses two ranks on one GPU)")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29517",
+                        os.path.join(ROOT, "tests", "rccl_worker.py")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "RCCL-WORKER-OK rank 0" in r.stdout and "RCCL-WORKER-OK rank 1" in r.stdout
