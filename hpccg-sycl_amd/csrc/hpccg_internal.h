@@ -142,6 +142,9 @@ void launch_waxpby(int n, double alpha, const double* x, double beta, const doub
 void launch_ddot(int n, const double* x, const double* y, double* partial, int nparts, double* out, hipStream_t s);
 int ddot_nparts(int n);
 void launch_sparsemv(const CgArgs& a, const double* xext, double* y, hipStream_t s);
+// Diagnostic: the SELL-512-A values streamed like the SpMV, known bytes (FETCH calibration).
+constexpr int kDiagStreamA = 9;
+void launch_stream_a(const CgArgs& a, hipStream_t s);
 
 // Device generator: writes the SELL-512 image, b, xexact.
 void launch_generate(int nx, int ny, int nz, int rank, int size, int use_7pt, long long col_base,

@@ -727,6 +727,26 @@ __global__ __launch_bounds__(kBlock) void k_spmv_plain(CgArgs a, const double* _
         if (row + i < a.n) y[row + i] = sum[i];
 }
 
+// Diagnostic only (never in the CG path): streams the SELL-512-A values like
+// the SpMV (16 B non-temporal loads per lane, slot-major) without the x side,
+// writing one sum per row -- a known byte count (8 B x slots read, 8 B x n
+// written) for the rocprofv3 FETCH_SIZE / WRITE_SIZE calibration.
+__global__ __launch_bounds__(kBlock) void k_stream_a(CgArgs a)
+{
+    const int s = xcd_slice(a.grid);
+    if (s >= a.nslices) return;
+    const int w = (int)(a.abase[s + 1] - a.abase[s]);
+    const double* __restrict__ vp = a.aval + (size_t)a.abase[s] * kSliceRows + (size_t)threadIdx.x * kRpt;
+    double sum[kRpt] = {0.0, 0.0};
+#pragma unroll 4
+    for (int j = 0; j < w; j++) {
+        const Rows v = ld_m<true>(vp + (size_t)j * kSliceRows);
+        sum[0] = sum[0] + v.v[0];
+        sum[1] = sum[1] + v.v[1];
+    }
+    st_rows(a.Ap, s * kSliceRows + threadIdx.x * kRpt, a.n, Rows{{sum[0], sum[1]}});
+}
+
 // ---------------------------------------------------------------------------
 // Separate final reduction (dot not folded): the same two levels and order as
 // the folded completion, so fold on/off give the same bits. The partials are
@@ -736,27 +756,22 @@ __global__ __launch_bounds__(kBlock) void k_spmv_plain(CgArgs a, const double* _
 constexpr int kFinalizeThreads = 1024;
 constexpr int kFinLdsGroups = 2048;  // group sums kept in LDS up to 128 K slices (64 M rows)
 
-__global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int which, bool prologue)
+// kB groups per wave per round, every load of a round issued before the sums
+// (one round up to 16 x kB groups: 200^3 has 245, 7-pt 256^3 512).
+template <int kB>
+__device__ __forceinline__ void finalize_groups(const CgArgs& a, int ng, bool in_lds, double* gs, double* gp)
 {
-    __shared__ double gs[kFinLdsGroups];
-    const int ng = ngroups_of(a);
-    const bool in_lds = ng <= kFinLdsGroups;
-    double* gp = a.partial + a.nslices + which * ng;
     const int lane = threadIdx.x & (kWave - 1);
     constexpr int kWaves = kFinalizeThreads / kWave;
-    constexpr int kBatch = 8;  // groups per wave per round, loads in flight together
-    const int k = prologue ? 0 : a.kst[0];
-    // stamped unconditionally: stamps after the end stamp are dropped on the host
-    if (threadIdx.x == 0) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
-    for (int g0 = threadIdx.x / kWave; g0 < ng; g0 += kWaves * kBatch) {
-        double v[kBatch];
+    for (int g0 = threadIdx.x / kWave; g0 < ng; g0 += kWaves * kB) {
+        double v[kB];
 #pragma unroll
-        for (int b = 0; b < kBatch; b++) {
+        for (int b = 0; b < kB; b++) {
             const int i = (g0 + b * kWaves) * kGroup + lane;
             v[b] = (g0 + b * kWaves < ng && i < a.nslices) ? a.partial[i] : 0.0;
         }
 #pragma unroll
-        for (int b = 0; b < kBatch; b++) {
+        for (int b = 0; b < kB; b++) {
             const double w = wave_sum(v[b]);
             const int g = g0 + b * kWaves;
             if (lane == 0 && g < ng) {
@@ -767,6 +782,24 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
             }
         }
     }
+}
+
+__global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int which, bool prologue)
+{
+    __shared__ double gs[kFinLdsGroups];
+    const int ng = ngroups_of(a);
+    const bool in_lds = ng <= kFinLdsGroups;
+    double* gp = a.partial + a.nslices + which * ng;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int k = prologue ? 0 : a.kst[0];
+    // stamped unconditionally: stamps after the end stamp are dropped on the host
+    if (threadIdx.x == 0) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
+    if (ng <= 4 * (kFinalizeThreads / kWave))
+        finalize_groups<4>(a, ng, in_lds, gs, gp);
+    else if (ng <= 16 * (kFinalizeThreads / kWave))
+        finalize_groups<16>(a, ng, in_lds, gs, gp);
+    else
+        finalize_groups<32>(a, ng, in_lds, gs, gp);
     const bool run = prologue || cg_run(a, k, false);
     if (!run) {
         if (threadIdx.x == 0) mark_end(a);
@@ -1188,6 +1221,11 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         break;
     }
 #undef HPCCG_A
+}
+
+void launch_stream_a(const CgArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_stream_a, dim3(a.grid), dim3(kBlock), 0, s, a);
 }
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)

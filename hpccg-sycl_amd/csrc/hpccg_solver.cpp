@@ -207,7 +207,7 @@ struct hpccg_hip_matrix {
     // halo / interior overlap (multi-rank slab plan): the leading and trailing
     // units (slices; pairs for the pair kernel) that read ghost rows
     int halo_s_lo = -1, halo_s_hi = -1, halo_p_lo = -1, halo_p_hi = -1;
-    int overlap = 1;
+    int overlap = 0;  // eager launches only (see overlap_ok)
     hipStream_t stream = nullptr, stream2 = nullptr;
     hipEvent_t ev_pb = nullptr, ev_halo = nullptr;
     long long nnz = 0, nslots = 0;
@@ -217,7 +217,8 @@ struct hpccg_hip_matrix {
     int use_graph = 1;
     int fuse_p = -1;      // -1 auto: on where the kernel forms p_k itself
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
-    int force_comm = 0;   // diagnostics: scalars through the RCCL communicator even at one rank
+    int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
+                          // 2 also the multi-rank iteration with a self send/recv as its halo
     // SELL-512 (the general kernel; freed once SELL-512-A exists unless kept)
     int has_sell = 0;
     unsigned int* d_slice_base = nullptr;
@@ -250,6 +251,7 @@ struct hpccg_hip_matrix {
     int* d_kst = nullptr;
     double* d_hist = nullptr;
     unsigned long long* d_stamps = nullptr;
+    double* d_emul = nullptr;  // force_comm 2: self-exchange receive buffer
     int hist_cap = 0;
     long long stamp_cap = 0;
     double *d_gen_b = nullptr, *d_gen_x0 = nullptr, *d_gen_xexact = nullptr;
@@ -302,7 +304,7 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_pbuf,    M->d_ahist,    M->d_rbuf,
                     M->d_Ap,         M->d_x,      M->d_b,         M->d_partial, M->d_tickets,  M->d_scal,
                     M->d_kst,        M->d_hist,   M->d_stamps,    M->d_gen_b,   M->d_gen_x0,   M->d_gen_xexact,
-                    M->d_send_idx,   M->d_send_buf};
+                    M->d_send_idx,   M->d_send_buf,  M->d_emul};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -841,8 +843,19 @@ int alloc_workspace(hpccg_hip_matrix* M)
     return 0;
 }
 
+// force_comm 2 on a 1-rank communicator: the multi-rank iteration shape
+// (halo fork/join, RCCL send/recv, all-reduced scalars) on one GPU, to time
+// what the RCCL path adds per iteration where only one GPU is available.
+bool emulated_multi(const hpccg_hip_matrix* M)
+{
+    return M->nranks == 1 && M->force_comm == 2 && g_comm.comm && g_comm.nranks == 1 && !M->in_group;
+}
+size_t emul_rows(const hpccg_hip_matrix* M) { return std::min<size_t>(M->nrow, 40000); }  // a 200^2 plane
+bool multi_of(const hpccg_hip_matrix* M) { return M->nranks > 1 || emulated_multi(M); }
+
 int ensure_hist(hpccg_hip_matrix* M, int max_iter)
 {
+    if (emulated_multi(M) && !M->d_emul) TRY(dev_alloc(M, &M->d_emul, emul_rows(M), true));
     const int need = std::max(2, max_iter + 1);
     if (need > M->hist_cap) {
         dev_free(M, &M->d_hist, M->hist_cap);
@@ -933,7 +946,17 @@ CgArgs unit_range(const CgArgs& a, int s0, int n0, int s1, int n1)
 // last send_hi rows up, and receives straight into the ghost regions.
 int enqueue_halo(hpccg_hip_matrix* M, double* p, hipStream_t st)
 {
-    if (g_comm.nranks == 1) return 0;
+    if (g_comm.nranks == 1) {
+        if (!emulated_multi(M)) return 0;
+        // force_comm 2: one rank sends a slab plane's worth of its first rows
+        // to itself, through the same RCCL calls and streams
+        const size_t cnt = emul_rows(M);
+        NCCL_TRY(ncclGroupStart());
+        NCCL_TRY(ncclRecv(M->d_emul, cnt, ncclFloat64, 0, g_comm.comm, st));
+        NCCL_TRY(ncclSend(p, cnt, ncclFloat64, 0, g_comm.comm, st));
+        NCCL_TRY(ncclGroupEnd());
+        return 0;
+    }
     const int r = g_comm.rank;
     NCCL_TRY(ncclGroupStart());
     if (r > 0) {
@@ -1143,8 +1166,20 @@ void halo_units(const hpccg_hip_matrix* M, int* lo, int* hi)
 // then the exchange on the second stream while the main stream runs the SpMV
 // over the units that read no ghost row; the halo-dependent units follow once
 // the halo has landed. Same values, same partial slots.
+//
+// Eager launches only, opt-in. Measured on one MI355X (tools/comm_bench.py,
+// tools/group_bench.py, profiles/r02_comm): a hipGraph capture that forks the
+// halo stream around RCCL calls segfaults in the ROCm 7.2 runtime (the same
+// fault as capturing 3+ forked streams, tools/probe/capture_probe.hip), and
+// the fork/join's cross-stream waits cost more than the exchange they hide
+// (1-rank self exchange: +17.8 vs +12.4 us per iteration eager at 100^3;
+// in-process group of 2: +400-450 us). Captured iterations therefore run the
+// halo in line on the main stream.
+thread_local bool g_capturing = false;
+
 bool overlap_ok(const Ranks& R)
 {
+    if (g_capturing) return false;
     for (int r = 0; r < R.P; r++) {
         const hpccg_hip_matrix* M = R.M[r];
         int lo, hi;
@@ -1214,7 +1249,7 @@ int enqueue_spmv_overlapped(const Ranks& R, int slot, int k_host)
 // p_k's ring slot for the halo.
 int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
 {
-    const bool multi = R.M[0]->nranks > 1;
+    const bool multi = multi_of(R.M[0]);
     if (multi && overlap_ok(R)) {
         TRY(enqueue_spmv_overlapped(R, slot, k_host));
     } else {
@@ -1253,7 +1288,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
 
 int enqueue_prologue(const Ranks& R, bool events)
 {
-    const bool multi = R.M[0]->nranks > 1;
+    const bool multi = multi_of(R.M[0]);
     for (int r = 0; r < R.P; r++) {
         TRY(use_device(R, r));
         launch_cg_prologue_copy(R.a[r], R.M[r]->stream);  // p = x
@@ -1283,7 +1318,7 @@ int enqueue_prologue(const Ranks& R, bool events)
 int graph_chunk_of(const Ranks& R)
 {
     int chunk = std::max(1, R.M[0]->graph_iters);
-    if (R.M[0]->nranks > 1) {
+    if (multi_of(R.M[0])) {
         const int ring = R.a[0].nring;
         chunk = (chunk + ring - 1) / ring * ring;
     }
@@ -1326,7 +1361,9 @@ int build_graph(const Ranks& R, int chunk)
     hipGraph_t g = nullptr;
     HIP_TRY(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
     int rc = 0;
+    g_capturing = true;
     for (int i = 0; i < chunk && rc == 0; i++) rc = enqueue_iteration(R, -1, i + 1);
+    g_capturing = false;
     hipError_t e = hipStreamEndCapture(s0, &g);
     if (rc) {
         if (g) (void)hipGraphDestroy(g);
@@ -2182,7 +2219,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         if (value < -1 || value > 3) return set_err(HPCCG_HIP_EINVAL, "fold must be -1 (auto) or 0..3");
         M->fold = (int)value;
     } else if (!std::strcmp(key, "force_comm")) {
-        M->force_comm = value ? 1 : 0;
+        if (value < 0 || value > 2) return set_err(HPCCG_HIP_EINVAL, "force_comm is 0, 1 or 2");
+        M->force_comm = (int)value;
     } else if (!std::strcmp(key, "spmv_kernel")) {
         if (value != -1 && !spmv_kernel_ok((int)value))
             return set_err(HPCCG_HIP_EINVAL, "spmv_kernel must be -1 (auto), 0 (SELL-512), 1 (SELL-512-A direct) or "
@@ -2216,7 +2254,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "overlap")) {
         int lo, hi;
         halo_units(M, &lo, &hi);
-        *value = (M->overlap && M->nranks > 1 && !M->general && lo >= 0) ? 1 : 0;
+        *value = (M->overlap && multi_of(M) && !M->general && lo >= 0 && (!M->use_graph || M->graph_failed)) ? 1 : 0;
     } else if (!std::strcmp(key, "num_external")) *value = M->general ? M->ghost_hi : M->ghost_lo + M->ghost_hi;
     else if (!std::strcmp(key, "has_sell")) *value = M->has_sell;
     else if (!std::strcmp(key, "has_a")) *value = M->has_a;
@@ -2269,20 +2307,27 @@ int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_ite
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_us)
 {
     if (!M || !avg_us || reps < 1) return set_err(HPCCG_HIP_EINVAL, "bad argument");
-    if (!spmv_kernel_ok(kernel) || !kernel_available(M, kernel))
+    const bool stream = kernel == kDiagStreamA && M->has_a;
+    if (!stream && (!spmv_kernel_ok(kernel) || !kernel_available(M, kernel)))
         return set_err(HPCCG_HIP_EINVAL, "spmv_kernel %d is not available for this matrix", kernel);
     HIP_TRY(hipSetDevice(M->device));
     TRY(ensure_hist(M, 2));
     const int keep = M->kernel;
-    M->kernel = kernel;  // make_args sizes the grid for that kernel
+    if (!stream) M->kernel = kernel;  // make_args sizes the grid for that kernel
     CgArgs a = make_args(M, M->d_b, M->d_x, 2, 0.0);
     M->kernel = keep;
+    auto launch = [&]() {
+        if (stream)
+            launch_stream_a(a, M->stream);
+        else
+            launch_cg_spmv(a, kernel, true, M->stream);
+    };
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
-    launch_cg_spmv(a, kernel, true, M->stream);  // warm
+    launch();  // warm
     HIP_TRY(hipEventRecord(e0, M->stream));
-    for (int i = 0; i < reps; i++) launch_cg_spmv(a, kernel, true, M->stream);
+    for (int i = 0; i < reps; i++) launch();
     HIP_TRY(hipEventRecord(e1, M->stream));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventSynchronize(e1));

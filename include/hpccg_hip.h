@@ -150,10 +150,14 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *   "x_ring"        p ring length = x deferral depth, 2..64; -1 auto: 32 for
  *                   matrix images over 512 MB, else 8
  *   "rev_update"    1 = the update kernel walks each XCD's slices backwards
- *   "overlap"       1 = multi-rank: halo exchange beside the interior SpMV
- *   "force_comm"    diagnostics: route the two CG scalars through the RCCL
- *                   communicator even with one rank (exercises the all-reduce
- *                   path, captured in the graph)
+ *   "overlap"       1 = multi-rank, eager launches: halo exchange on a second
+ *                   stream beside the interior SpMV (default 0; hipGraph
+ *                   replays always run the halo in line on the main stream --
+ *                   see DESIGN.md section 6 for the measurements)
+ *   "force_comm"    diagnostics, 1-rank communicator: 1 = route the two CG
+ *                   scalars through ncclAllReduce; 2 = also the multi-rank
+ *                   iteration (boundary rows, a plane-sized ncclSend/ncclRecv
+ *                   to itself as the halo); captured in the graph like N > 1
  * get only: "has_sell", "has_a", "has_pairs", "a_width", "lds_doubles", "nt",
  * "halo_mode", "num_external", "overlap", "device_bytes" (device memory M
  * holds). None of the knobs changes a computed value: every kernel, fusion and
@@ -166,7 +170,8 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
 int hpccg_hip_kernel_times(const hpccg_hip_matrix* M, double out[4]);
 /* Diagnostic: average duration (hipEvents, solver stream) of `reps`
  * back-to-back launches of SpMV kernel `kernel` (prologue form) on the
- * resident p. */
+ * resident p; kernel 9 streams the SELL-512-A values alone (8 B x slots read,
+ * 8 B x n written: the rocprofv3 FETCH_SIZE calibration). */
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_us);
 
 /* ---- in-process rank group --------------------------------------------------

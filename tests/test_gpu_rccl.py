@@ -65,6 +65,38 @@ def test_rccl_scalars_in_graph(hp, gpu, graph):
         hp.comm_destroy()
 
 
+def test_rccl_emulated_multirank_iteration(hp, gpu):
+    """force_comm 2 on a 1-rank communicator: the multi-rank iteration shape
+    (k_p_boundary path, the halo as a plane-sized ncclSend/ncclRecv to itself,
+    both scalars through ncclAllReduce) in a captured hipGraph and eagerly,
+    halo in line and (eager) on the second stream. Every variant is bitwise the
+    plain solve. This is the capture the N > 1 RCCL job replays: with the halo
+    on a forked stream it segfaulted inside the ROCm runtime, so graphs run it
+    in line."""
+    import torch
+    hp.comm_init(hp.comm_unique_id(), 1, 0)
+    try:
+        M = hp.Matrix.generate(40, 36, 30)
+        b, _, _ = M.vectors()
+        outs = []
+        for fc, ovl, graph in ((0, 0, 1), (2, 0, 1), (2, 1, 1), (2, 0, 0), (2, 1, 0)):
+            M.set_option("force_comm", fc)
+            M.set_option("overlap", ovl)
+            M.set_option("use_graph", graph)
+            x = torch.zeros(40 * 36 * 30, dtype=torch.float64, device=gpu)
+            _, it, nr, times = hp.HPCCG(M, b, x, max_iter=120, device=True)
+            outs.append((it, nr, M.last_trace().tobytes(), x.cpu().numpy().tobytes()))
+            assert M.get_option("graph_used") == graph
+            assert M.get_option("overlap") == (1 if (fc == 2 and ovl and not graph) else 0)
+            if fc:
+                assert times[4] > 0.0
+        for o in outs[1:]:
+            assert o == outs[0]
+        M.close()
+    finally:
+        hp.comm_destroy()
+
+
 def test_rccl_two_processes(hp, gpu, golden):
     """The RCCL job itself: torch.distributed.run launches 2 ranks, one per
     GPU; each generates its z-slab of the 2 x 8^3 problem on its GPU and

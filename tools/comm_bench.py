@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""What the RCCL rank path adds per CG iteration, measured on ONE GPU
+(diagnostic, not a scaling number): a 1-rank RCCL communicator and
+force_comm = 1 (p.Ap and r.r through ncclAllReduce) or 2 (also the
+multi-rank iteration: halo fork/join on the second stream, a plane-sized
+ncclSend/ncclRecv to itself), against the plain single-GPU solve. One JSON
+line per (force_comm, overlap, use_graph).
+
+usage: tools/comm_bench.py [--n 200] [--steps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import load_pkg  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--max-iter", type=int, default=500)
+    ap.add_argument("--7pt", dest="s7", action="store_true")
+    ap.add_argument("--variants", default="0:0:1,1:0:1,2:0:1,2:1:1,2:0:0,2:1:0",
+                    help="force_comm:overlap:use_graph triples")
+    args = ap.parse_args()
+    import torch
+    hp = load_pkg()
+    hp.set_device(0)
+    hp.comm_init(hp.comm_unique_id(), 1, 0)
+    try:
+        n3 = args.n ** 3
+        M = hp.Matrix.generate(args.n, args.n, args.n, use_7pt=args.s7)
+        b = M.vectors()[0]
+        x = torch.zeros(n3, dtype=torch.float64, device="cuda:0")
+        base = None
+        traces = {}
+        for v in args.variants.split(","):
+            fc, ovl, graph = (int(t) for t in v.split(":"))
+            M.set_option("force_comm", fc)
+            M.set_option("overlap", ovl)
+            M.set_option("use_graph", graph)
+
+            def solve():
+                x.zero_()
+                return hp.HPCCG(M, b, x, max_iter=args.max_iter, device=True)[1]
+
+            solve()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                it = solve()
+            torch.cuda.synchronize()
+            us = (time.perf_counter() - t0) / args.steps / it * 1e6
+            if base is None:
+                base = us
+            traces[v] = M.last_trace().tobytes()
+            print(json.dumps({"n": args.n, "stencil": 7 if args.s7 else 27, "force_comm": fc, "overlap": ovl,
+                              "use_graph": graph, "us_per_iter": round(us, 2),
+                              "added_us_per_iter": round(us - base, 2),
+                              "overlap_in_use": M.get_option("overlap"), "graph_used": M.get_option("graph_used"),
+                              "kernel": M.get_option("spmv_kernel"), "niters": it,
+                              "trace_equal_first": traces[v] == next(iter(traces.values()))}), flush=True)
+        M.close()
+    finally:
+        hp.comm_destroy()
+
+
+if __name__ == "__main__":
+    main()

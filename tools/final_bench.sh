@@ -2,4 +2,4 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
 timeout -k 10 400 python bench.py > gpurun_out/fb200.log 2> gpurun_out/fb200.err &&
 timeout -k 10 300 python bench.py --n 100 > gpurun_out/fb100.log 2> gpurun_out/fb100.err &&
-timeout -k 10 400 python bench.py --n 256 --stencil 7 --steps 3 > gpurun_out/fb7.log 2> gpurun_out/fb7.err
+timeout -k 10 400 python bench.py --n 256 --stencil 7 > gpurun_out/fb7.log 2> gpurun_out/fb7.err

@@ -18,7 +18,7 @@ step() {
 }
 
 S=${STENCIL:-27}
-step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --stencil $S --steps 2 --warmup 1 --no-cpu-baseline --no-secondary
+step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --stencil $S --steps 3 --warmup 1 --no-cpu-baseline
 step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python tools/pmc_workload.py --n $N --stencil $S
 step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python tools/pmc_workload.py --n $N --stencil $S
 find $OUT -name "*.csv" | head -20

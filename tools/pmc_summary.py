@@ -5,9 +5,9 @@
 * HBM traffic per SpMV launch from two separate --pmc passes (FETCH_SIZE,
   WRITE_SIZE; KiB units). gfx950 correction (MI355X_MICROARCH.md, HBM):
   FETCH_SIZE reports 1/2 of a wide coalesced stream; the factor is
-  calibrated here on k_stream_diag, which reads exactly
-  12 * sell_slots bytes (vals fp64 + cols int32, 16 B / 8 B per lane, the
-  SpMV's own matrix access pattern) and writes 8 * nrow.
+  calibrated here on k_stream_a, which reads exactly 8 * a_slots bytes (the
+  SELL-512-A values, 16 B non-temporal loads per lane: the SpMV's own matrix
+  access pattern) and writes 8 * nrow.
 
 usage: tools/pmc_summary.py <prof_dir> <tag> <nx> [<bench_json_log>] [<stencil 27|7>]
 """
@@ -24,15 +24,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 FORMATS = {
-    "k_spmv": "SELL-512 (8 B value + int32 column per slot)",
-    "k_spmv_c": "SELL-512-C (8 B value + 1-byte offset code per slot)",
-    "k_spmv_lds": "SELL-512-L/-C with x from LDS windows",
-    "k_spmv_lp": "SELL-512-P (8 B value per slot + 1-byte row-pattern id per row), x from LDS windows",
-    "k_spmv_pp": "SELL-512-P (8 B value per slot + 1-byte row-pattern id per row), x gathered",
-    "k_spmv_v4": "SELL-512-V (1-byte (offset, value) codes in 4-slot chunks)",
-    "k_spmv_la2": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice pairs",
-    "k_spmv_la": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows",
-    "k_spmv_pa": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at per-slice offsets",
+    "k_spmv_sell": "SELL-512 (8 B value + int32 column per slot)",
+    "k_spmv_a": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets",
+    "k_spmv_a2": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice pairs",
 }
 
 
@@ -83,35 +77,31 @@ def main():
 
     stencil = int(sys.argv[5]) if len(sys.argv) > 5 else 27
     nrow = n ** 3
-    # SELL-512 uniform image of the stencil problem
+    # the uniform SELL-512-A image of the stencil problem
     width = 27 if stencil == 27 else 7
     slots = ((nrow + 511) // 512) * 512 * width
     nnz = (3 * n - 2) ** 3 if stencil == 27 else 7 * n ** 3 - 6 * n * n
-    if stencil == 27:
-        stream_read = 12.0 * slots  # k_stream_diag reads the 12 B/slot SELL-512 image
-        f_stream, _ = pick(fetch, "k_stream_diag", "FETCH_SIZE")
-        w_stream, _ = pick(write, "k_stream_diag", "WRITE_SIZE")
-        fetch_factor = stream_read / (f_stream * 1024.0)
-    else:  # no width-27 image to stream: the factor the 27-pt calibrations measure (2.0)
-        stream_read, f_stream, w_stream, fetch_factor = None, None, None, 2.0
-    SPMV = ("k_spmv<", "k_spmv_lds<", "k_spmv_c<", "k_spmv_lp<", "k_spmv_pp<", "k_spmv_v4<", "k_spmv_pa<", "k_spmv_la<", "k_spmv_la2<")
+    stream_read = 8.0 * slots  # k_stream_a reads the 8 B/slot A image
+    f_stream, _ = pick(fetch, "k_stream_a", "FETCH_SIZE")
+    w_stream, _ = pick(write, "k_stream_a", "WRITE_SIZE")
+    fetch_factor = stream_read / (f_stream * 1024.0)
+    SPMV = ("k_spmv_sell<", "k_spmv_a<", "k_spmv_a2<")
     f_spmv, kname = pick(fetch, SPMV, "FETCH_SIZE")
     w_spmv, _ = pick(write, SPMV, "WRITE_SIZE")
     spmv_read = f_spmv * 1024.0 * fetch_factor
     spmv_write = w_spmv * 1024.0
     targs = re.search(r"k_spmv\w*<([^>]*)>", kname).group(1).split(",")
-    # k_spmv<kRpt, kW, kMinW, kNT, kFuse> has kFuse last,
-    # k_spmv_pa<kRpt, kNT, kW, kFuse, kPre> fourth; every other SpMV kernel
-    # (k_spmv_lds, k_spmv_c, k_spmv_lp, k_spmv_pp, k_spmv_v4, k_spmv_la) third
-    if "k_spmv<" in kname:
-        fuse_p = targs[-1].strip() == "true"
-    elif "k_spmv_pa<" in kname:
-        fuse_p = targs[3].strip() == "true"
-    elif "k_spmv_la2<" in kname:  # k_spmv_la2<kNT, kFuse, kPre, kMinW>
+    # k_spmv_a<kW, kNT, kFuse, kPre>, k_spmv_a2<kNT, kFuse, kPre>, k_spmv_sell<kNT> (never fused)
+    if "k_spmv_a<" in kname:
+        fuse_p = targs[2].strip() == "true"
+    elif "k_spmv_a2<" in kname:
         fuse_p = targs[1].strip() == "true"
     else:
-        fuse_p = targs[2].strip() == "true"
+        fuse_p = False
     algo = 12.0 * nnz + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fuse_p else 0.0)
+    # the bytes the format must move: 8 B per stored slot, + r, p_{k-1} read and
+    # p_k, Ap written (fused) or p read and Ap written
+    compulsory = 8.0 * slots + (32.0 if fuse_p else 16.0) * nrow
 
     avg_ns = None
     calls = -1
@@ -127,9 +117,10 @@ def main():
         "kernel": kname,
         "fuse_p": fuse_p,
         "bytes_formula": "12 nnz + 20 n + 16 n" + (" + 24 n" if fuse_p else ""),
+        "format_compulsory_bytes_per_launch": compulsory,
         "fetch_size_kib_raw": f_spmv,
         "write_size_kib_raw": w_spmv,
-        "fetch_calibration": {"kernel": "k_stream_diag<27>", "known_read_bytes": stream_read,
+        "fetch_calibration": {"kernel": "k_stream_a", "known_read_bytes": stream_read,
                               "fetch_size_kib": f_stream, "factor": round(fetch_factor, 4),
                               "write_size_kib": w_stream, "known_write_bytes": 8.0 * nrow},
         "spmv_hbm_read_bytes_per_launch": spmv_read,
@@ -137,8 +128,11 @@ def main():
         "spmv_hbm_bytes_per_launch": spmv_read + spmv_write,
         "spmv_algorithmic_bytes_per_launch": algo,
         "traffic_over_algorithmic": (spmv_read + spmv_write) / algo,
+        "traffic_over_compulsory": (spmv_read + spmv_write) / compulsory,
         "rocprof_avg_spmv_ns": avg_ns,
-        "rocprof_spmv_GBs": algo / avg_ns if avg_ns else None,
+        "rocprof_spmv_traffic_GBs": (spmv_read + spmv_write) / avg_ns if avg_ns else None,
+        "rocprof_spmv_compulsory_GBs": compulsory / avg_ns if avg_ns else None,
+        "rocprof_spmv_credited_GBs": algo / avg_ns if avg_ns else None,
     }
     # every kernel of the pmc workload: corrected HBM bytes per launch
     per_kernel = {}

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Workload for the rocprofv3 --pmc passes: the known-bytes streaming kernel
-(FETCH_SIZE calibration) and a short CG solve with the production kernels."""
+"""Workload for the rocprofv3 --pmc passes: the known-bytes stream of the
+SELL-512-A values (FETCH_SIZE calibration, hpccg_hip_diag_spmv kernel 9) and a
+short eager CG solve with the production kernels."""
 import argparse
 import os
 import sys
@@ -13,21 +14,20 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=200)
 ap.add_argument("--iters", type=int, default=12)
 ap.add_argument("--stencil", type=int, default=27, choices=[27, 7])
-ap.add_argument("--variant", type=int, default=-1, help="SpMV variant (-1: the library's choice)")
+ap.add_argument("--kernel", type=int, default=-1, help="SpMV kernel (-1: the library's choice)")
 ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1: default)")
 args = ap.parse_args()
 import torch  # noqa: E402,F401
 hp = load_pkg()
 hp.set_device(0)
 M = hp.Matrix.generate(args.n, args.n, args.n, use_7pt=args.stencil == 7)
-if args.stencil == 27:
-    M.diag_spmv(9999, 3)  # known-bytes stream of the uniform width-27 image (FETCH calibration)
-if args.variant >= 0:
-    M.set_option("spmv_variant", args.variant)
+M.diag_spmv(9, 3)  # known-bytes stream of the A image (FETCH calibration)
+if args.kernel >= 0:
+    M.set_option("spmv_kernel", args.kernel)
 if args.fuse_p >= 0:
     M.set_option("fuse_p", args.fuse_p)
 b, _, _ = M.vectors()
 x = torch.zeros(args.n ** 3, dtype=torch.float64, device="cuda:0")
 M.set_option("use_graph", 0)
 hp.HPCCG(M, b, x, max_iter=args.iters, device=True)
-print("fuse_p", M.get_option("fuse_p"), "variant", M.get_option("spmv_variant"))
+print("fuse_p", M.get_option("fuse_p"), "kernel", M.get_option("spmv_kernel"), "slots", M.info()["slots"])
