@@ -179,6 +179,7 @@ def main():
     ap.add_argument("--x-ring", type=int, default=-1, help="x-update deferral depth = p ring length")
     ap.add_argument("--rev-update", type=int, default=-1, help="update kernel walks slices backwards")
     ap.add_argument("--overlap", type=int, default=-1, help="multi-rank: halo beside the interior SpMV")
+    ap.add_argument("--a-pre", type=int, default=-1, help="direct kernel: value slots loaded before the test")
     ap.add_argument("--use-graph", type=int, default=-1, help="hipGraph replay (-1 default on)")
     ap.add_argument("--event-steps", type=int, default=1,
                     help="timed steps launched eagerly with hipEvents around every SpMV (the roofline's kernel "
@@ -211,7 +212,8 @@ def main():
     info = M.info()
     for opt, val in (("spmv_kernel", args.kernel), ("fuse_p", args.fuse_p), ("fold", args.fold),
                      ("graph_chunk", args.graph_chunk), ("x_defer", args.x_defer), ("x_ring", args.x_ring),
-                     ("rev_update", args.rev_update), ("overlap", args.overlap), ("use_graph", args.use_graph)):
+                     ("rev_update", args.rev_update), ("overlap", args.overlap), ("a_pre", args.a_pre),
+                     ("use_graph", args.use_graph)):
         if val != -1:
             M.set_option(opt, val)
     b, x0, _ = M.vectors()

@@ -64,6 +64,7 @@ struct CgArgs {
     int sgrid;             // SpMV launch grid (sn0 + sn1 rounded up to a multiple of kNumXcd)
     int nt;                // non-temporal matrix loads (image beyond the Infinity Cache)
     int a_width;           // SELL-512-A uniform slot count (27, 7, ...), 0 = per-slice widths
+    int apre;              // direct kernel: value slots loaded before the iteration test (-1 auto)
     double* ahist;         // [max_iter + 1]: alpha_k (for the deferred x update)
     int fuse_p;            // 1: p = r + beta p computed inside the SpMV
     int fold;              // dots completed in the producing kernel: 0 none, 1 both, 2 p.Ap only, 3 r.r only

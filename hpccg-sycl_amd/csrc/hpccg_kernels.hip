@@ -1206,9 +1206,19 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     }
     case kSpmvDirect:
         if (a.a_width == 27) {
-            if (a.nt) HPCCG_A(27, true, 4); else HPCCG_A(27, false, 4);
+            if (a.apre == 0) {
+                if (a.nt) HPCCG_A(27, true, 0); else HPCCG_A(27, false, 0);
+            } else {
+                if (a.nt) HPCCG_A(27, true, 4); else HPCCG_A(27, false, 4);
+            }
         } else if (a.a_width == 7) {
-            if (a.nt) HPCCG_A(7, true, 0); else HPCCG_A(7, false, 0);
+            if (a.apre == 3) {
+                if (a.nt) HPCCG_A(7, true, 3); else HPCCG_A(7, false, 3);
+            } else if (a.apre == 0) {
+                if (a.nt) HPCCG_A(7, true, 0); else HPCCG_A(7, false, 0);
+            } else {  // auto: all 7 slots early (7-pt 256^3 same-process A/B: 2445 vs 2422 it/s)
+                if (a.nt) HPCCG_A(7, true, 7); else HPCCG_A(7, false, 7);
+            }
         } else {
             if (a.nt) HPCCG_A(0, true, 0); else HPCCG_A(0, false, 0);
         }

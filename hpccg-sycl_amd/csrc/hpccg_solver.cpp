@@ -216,6 +216,7 @@ struct hpccg_hip_matrix {
     int kernel_opt = -1;  // option spmv_kernel (-1 auto)
     int use_graph = 1;
     int fuse_p = -1;      // -1 auto: on where the kernel forms p_k itself
+    int a_pre = -1;       // direct kernel prefetch depth (-1 auto: 4 at width 27, 7 at width 7)
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
                           // 2 also the multi-rank iteration with a self send/recv as its halo
@@ -903,6 +904,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.sgrid = grid_of(units);
     a.nt = image_big(M) ? 1 : 0;
     a.a_width = M->a_width;
+    a.apre = M->a_pre;
     a.ahist = M->d_ahist;
     a.fold = fold_effective(M);
     a.tickets = M->d_tickets;
@@ -923,6 +925,9 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.awin2 = M->d_awin2;
     a.awn2 = M->d_awn2;
     a.alds2_doubles = std::max(1, M->alds2_doubles);
+    if (std::getenv("HPCCG_DEBUG_ADDR"))
+        std::fprintf(stderr, "hpccg_hip addr: aval %p p %p pstride_B %lld r %p Ap %p x %p b %p\n", (void*)a.aval,
+                     (void*)a.p, a.pstride * 8, (void*)a.r, (void*)a.Ap, (void*)a.x, (void*)a.b);
     return a;
 }
 
@@ -2218,6 +2223,10 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "fold")) {
         if (value < -1 || value > 3) return set_err(HPCCG_HIP_EINVAL, "fold must be -1 (auto) or 0..3");
         M->fold = (int)value;
+    } else if (!std::strcmp(key, "a_pre")) {
+        if (value != -1 && value != 0 && value != 3 && value != 4 && value != 7)
+            return set_err(HPCCG_HIP_EINVAL, "a_pre must be -1 (auto), 0, 3 (width 7), 4 (width 27) or 7 (width 7)");
+        M->a_pre = (int)value;
     } else if (!std::strcmp(key, "force_comm")) {
         if (value < 0 || value > 2) return set_err(HPCCG_HIP_EINVAL, "force_comm is 0, 1 or 2");
         M->force_comm = (int)value;
@@ -2251,6 +2260,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "graph_chunk")) *value = M->graph_iters;
     else if (!std::strcmp(key, "graph_used")) *value = M->graph_used;
     else if (!std::strcmp(key, "force_comm")) *value = M->force_comm;
+    else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
     else if (!std::strcmp(key, "overlap")) {
         int lo, hi;
         halo_units(M, &lo, &hi);

@@ -154,6 +154,9 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   stream beside the interior SpMV (default 0; hipGraph
  *                   replays always run the halo in line on the main stream --
  *                   see DESIGN.md section 6 for the measurements)
+ *   "a_pre"         direct SELL-512-A kernel: value slots loaded before the
+ *                   iteration test, -1 auto (4 at width 27, 7 at width 7), 0,
+ *                   3 or 7 (width 7), 4 (width 27)
  *   "force_comm"    diagnostics, 1-rank communicator: 1 = route the two CG
  *                   scalars through ncclAllReduce; 2 = also the multi-rank
  *                   iteration (boundary rows, a plane-sized ncclSend/ncclRecv
