@@ -44,8 +44,14 @@ import time
 
 # the OpenMP leg of the CPU baseline: libgomp reads these when it first loads
 # (torch loads it), so they are set before anything is imported
-os.environ.setdefault("OMP_NUM_THREADS", str(len(os.sched_getaffinity(0))))
-os.environ.setdefault("OMP_PROC_BIND", "close")
+# (the process's CPU mask is read here too: libgomp later binds the main
+# thread to its first place). The box's share is OMP_NUM_THREADS (16 there);
+# spread over cores, so the threads reach more memory channels than 16
+# neighbouring cores would (the reference is memory-bound on the host too).
+AFFINITY_CPUS = len(os.sched_getaffinity(0))
+os.environ.setdefault("OMP_NUM_THREADS", str(AFFINITY_CPUS))
+os.environ.setdefault("OMP_PROC_BIND", "spread")
+os.environ.setdefault("OMP_PLACES", "cores")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -75,7 +81,8 @@ def log(*a):
 
 def host_cpu():
     """CPU model and counts of the host (lscpu), and this process's affinity."""
-    info = {"affinity_cpus": len(os.sched_getaffinity(0))}
+    info = {"affinity_cpus": AFFINITY_CPUS, "omp_proc_bind": os.environ.get("OMP_PROC_BIND"),
+            "omp_places": os.environ.get("OMP_PLACES")}
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         for line in out.splitlines():
@@ -122,7 +129,9 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=10.0, budget_1t_s=5.0):
                       f"reference HPCCG() solve ({res['times'][0]:.1f} s)")
             if leg == "omp":
                 out.update({"value": its, "cores": nthreads, "kind": "reference",
-                            "sample": sample + f", OpenMP {nthreads} threads (OMP_PROC_BIND=close)"})
+                            "sample": sample + f", OpenMP {nthreads} threads (OMP_PROC_BIND="
+                                                f"{os.environ.get('OMP_PROC_BIND')}, OMP_PLACES="
+                                                f"{os.environ.get('OMP_PLACES')})"})
             else:
                 out["single_thread"] = {"value": its, "cores": 1, "kind": "reference", "sample": sample + ", serial"}
     finally:

@@ -151,7 +151,7 @@ def main():
             b = json.loads(lines[-1])
             out["bench_avg_launch_us"] = b["roofline"]["avg_launch_us"]
             out["bench_value"] = b["value"]
-            shutil.copy(bench_log, os.path.join(outdir, "bench_under_rocprof.json"))
+            shutil.copy(bench_log, os.path.join(outdir, "bench_line.json"))
     with open(os.path.join(ROOT, "profiles", f"pmc_spmv_{stencil}pt_{n}.json"), "w") as f:
         json.dump(out, f, indent=1)
     with open(os.path.join(outdir, "summary.json"), "w") as f:
