@@ -94,6 +94,7 @@ def lib() -> C.CDLL:
         "hpccg_hip_set_option": (ip, [vp, C.c_char_p, lp]),
         "hpccg_hip_get_option": (ip, [vp, C.c_char_p, C.POINTER(lp)]),
         "hpccg_hip_kernel_times": (ip, [vp, PD]),
+        "hpccg_hip_kernel_times_iter": (ip, [vp, PD, ip]),
         "hpccg_hip_diag_spmv": (ip, [vp, ip, ip, PD]),
         "hpccg_hip_sparsemv": (ip, [vp, vp, vp]),
         "hpccg_hip_ddot": (ip, [ip, vp, vp, PD]),
@@ -300,6 +301,14 @@ class Matrix:
         _check(lib().hpccg_hip_kernel_times(self.h, out), "kernel_times")
         return {"spmv_ms": out[0], "spmv_launches": int(out[1]), "update_ms": out[2],
                 "update_launches": int(out[3])}
+
+    def kernel_times_iter(self, cap: int = 100000) -> np.ndarray:
+        """Per-iteration (SpMV ms, update ms) of the last event-timed solve."""
+        out = np.zeros(2 * cap, np.float64)
+        n = lib().hpccg_hip_kernel_times_iter(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), cap)
+        if n < 0:
+            _check(n, "kernel_times_iter")
+        return out[:2 * n].reshape(n, 2)
 
     def diag_spmv(self, kernel: int, reps: int = 20) -> float:
         """Average us per launch of an SpMV kernel (0 SELL-512, 1 SELL-512-A

@@ -269,6 +269,7 @@ struct hpccg_hip_matrix {
     int event_timing = 0;
     std::vector<hipEvent_t> ev;
     double ktimes[4] = {0, 0, 0, 0};
+    std::vector<double> kiter;  // event_timing: per iteration {SpMV ms, update ms}
     std::vector<double> trace;
     int last_niters = 0;
 };
@@ -1555,12 +1556,15 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     const double normr = M->trace[niters];
     if (events) {
         double sp = 0, up = 0;
+        M->kiter.assign(2 * (size_t)(niters + 1), 0.0);
         for (int i = 0; i <= niters; i++) {
             float ms = 0.f;
             HIP_TRY(hipEventElapsedTime(&ms, M->ev[4 * i], M->ev[4 * i + 1]));
             sp += ms;
+            M->kiter[2 * i] = ms;
             HIP_TRY(hipEventElapsedTime(&ms, M->ev[4 * i + 2], M->ev[4 * i + 3]));
             up += ms;
+            M->kiter[2 * i + 1] = ms;
         }
         M->ktimes[0] = sp;
         M->ktimes[1] = niters + 1;
@@ -2354,6 +2358,14 @@ int hpccg_hip_kernel_times(const hpccg_hip_matrix* M, double out[4])
     if (!M || !out) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
     for (int i = 0; i < 4; i++) out[i] = M->ktimes[i];
     return 0;
+}
+
+int hpccg_hip_kernel_times_iter(const hpccg_hip_matrix* M, double* out, int cap)
+{
+    if (!M || !out) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    const int n = std::min<int>(cap, (int)(M->kiter.size() / 2));
+    for (int i = 0; i < 2 * n; i++) out[i] = M->kiter[i];
+    return n;
 }
 
 int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap)

@@ -171,6 +171,9 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
  * out[0] SpMV total ms, out[1] SpMV launches, out[2] fused-update total ms,
  * out[3] update launches (launches that did work, i.e. <= niters + 1). */
 int hpccg_hip_kernel_times(const hpccg_hip_matrix* M, double out[4]);
+/* The same per iteration (0 = the prologue): out[2i] SpMV ms, out[2i + 1]
+ * update ms, up to cap iterations; returns the count (diagnostics). */
+int hpccg_hip_kernel_times_iter(const hpccg_hip_matrix* M, double* out, int cap);
 /* Diagnostic: average duration (hipEvents, solver stream) of `reps`
  * back-to-back launches of SpMV kernel `kernel` (prologue form) on the
  * resident p; kernel 9 streams the SELL-512-A values alone (8 B x slots read,
