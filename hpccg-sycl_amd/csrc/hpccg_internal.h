@@ -87,6 +87,9 @@ struct CgArgs {
     const int* alds2;             // pair windows: per slice, kAMax LDS positions (minus the pair row)
     const int* awin2;             // per pair, kAWin windows (first row - pair row, length, LDS base)
     const int* awn2;              // windows per pair
+    const int* adiag2;            // per slice: LDS position of offset 0 (minus the pair row), -1 none
+    int lds_ep;                   // pair kernel: the rows' own p_k from the staged window
+    int stage16;                  // pair kernel: stage row pairs with 16-B loads / LDS stores
     int alds2_doubles;            // dynamic LDS per two-slice block
 };
 

@@ -480,15 +480,20 @@ __device__ __forceinline__ int unit_of(const CgArgs& a)
 // The epilogue every SpMV kernel shares for its two rows: store Ap; p_k
 // (fused: r + beta p_{k-1}, k_p_update's expression, stored for the update's
 // deferred x and the next iteration); the rows' p.Ap terms in order.
+// pk (optional): the rows' p_k as the caller already holds it (the pair
+// kernel's staged window; fused, the same expression, so the same bits).
 template <bool kFuse>
 __device__ __forceinline__ double spmv_rows_out(const CgArgs& a, const IterState& st, bool prologue, int row,
-                                                const double (&sum)[kRpt])
+                                                const double (&sum)[kRpt], const Rows* pk = nullptr)
 {
     st_rows(a.Ap, row, a.n, Rows{{sum[0], sum[1]}});
     if (prologue) return 0.0;  // HPCCG.cpp:351: the prologue SpMV has no p.Ap
     double* __restrict__ p = cur_p(a, st.k);
     Rows pv;
-    if constexpr (kFuse) {
+    if (pk) {
+        pv = *pk;
+        if constexpr (kFuse) st_rows(p, row, a.n, pv);
+    } else if constexpr (kFuse) {
         const double* __restrict__ pold = (st.k == 1) ? a.r : cur_p(a, st.k - 1);
         const Rows rv = ld(a.r + row);
         const Rows yv = ld(pold + row);
@@ -656,12 +661,34 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2(CgArgs a, bool prologue)
         const int* __restrict__ win = a.awin2 + (size_t)P * kAWin * 3;
         for (int w = 0; w < nw; w++) {
             const int st0 = prow0 + win[3 * w], len = win[3 * w + 1], base = win[3 * w + 2];
-            for (int i = threadIdx.x; i < len; i += 2 * kBlock) {
-                const int l = st0 + i;  // local row (< 0 / >= n: ghosts, guard or padding zeros)
-                if constexpr (kFuse)
-                    xs[base + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
-                else
-                    xs[base + i] = p[l];
+            if (a.stage16) {
+                // row pairs: first row, length and LDS base are even (pair_windows)
+                for (int i = 2 * threadIdx.x; i < len; i += 4 * kBlock) {
+                    const int l = st0 + i;  // local rows l, l + 1 (< 0 / >= n: ghosts, guard or padding zeros)
+                    d2v v;
+                    if constexpr (kFuse) {
+                        if (l >= 0 && l + 1 < a.n) {  // both own rows (r has no ghost region)
+                            const d2v rv = *reinterpret_cast<const d2v*>(a.r + l);
+                            const d2v yv = *reinterpret_cast<const d2v*>(pold + l);
+                            v.x = rv.x + st.beta * yv.x;
+                            v.y = rv.y + st.beta * yv.y;
+                        } else {
+                            v.x = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
+                            v.y = ((unsigned)(l + 1) < (unsigned)a.n) ? a.r[l + 1] + st.beta * pold[l + 1] : p[l + 1];
+                        }
+                    } else {
+                        v = *reinterpret_cast<const d2v*>(p + l);
+                    }
+                    *reinterpret_cast<d2v*>(xs + base + i) = v;
+                }
+            } else {
+                for (int i = threadIdx.x; i < len; i += 2 * kBlock) {
+                    const int l = st0 + i;  // local row (< 0 / >= n: ghosts, guard or padding zeros)
+                    if constexpr (kFuse)
+                        xs[base + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
+                    else
+                        xs[base + i] = p[l];
+                }
             }
         }
     }
@@ -686,7 +713,13 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2(CgArgs a, bool prologue)
 #pragma unroll
             for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xs[c + i];
         }
-        d = spmv_rows_out<kFuse>(a, st, prologue, s * kSliceRows + lrow, sum);
+        const int pd = a.adiag2 ? a.adiag2[s] : -1;  // LDS position of the slice's offset 0
+        if (pd >= 0 && a.lds_ep) {
+            const Rows pk{{xs[prow + pd], xs[prow + pd + 1]}};
+            d = spmv_rows_out<kFuse>(a, st, prologue, s * kSliceRows + lrow, sum, &pk);
+        } else {
+            d = spmv_rows_out<kFuse>(a, st, prologue, s * kSliceRows + lrow, sum);
+        }
     }
     if (prologue) return;
     // per-slice partials with block_sum<256>'s shape

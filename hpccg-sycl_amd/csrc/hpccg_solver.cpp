@@ -217,6 +217,8 @@ struct hpccg_hip_matrix {
     int use_graph = 1;
     int fuse_p = -1;      // -1 auto: on where the kernel forms p_k itself
     int a_pre = -1;       // direct kernel prefetch depth (-1 auto: 4 at width 27, 7 at width 7)
+    int lds_ep = 1;       // pair kernel: own p_k from the staged window
+    int stage16 = 1;      // pair kernel: 16-B staging of row pairs
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
                           // 2 also the multi-rank iteration with a self send/recv as its halo
@@ -232,7 +234,7 @@ struct hpccg_hip_matrix {
     int* d_aoff = nullptr;
     unsigned int* d_abase = nullptr;
     int has_pairs = 0, alds2_doubles = 0;
-    int *d_alds2 = nullptr, *d_awin2 = nullptr, *d_awn2 = nullptr;
+    int *d_alds2 = nullptr, *d_awin2 = nullptr, *d_awn2 = nullptr, *d_adiag2 = nullptr;
     // workspace (padded to a multiple of kSliceRows rows)
     size_t npad = 0;
     double* d_pbuf = nullptr;  // ring_alloc buffers of [guard | ghost_lo_pad | npad | ghost_hi_pad | guard]
@@ -303,7 +305,7 @@ int free_matrix(hpccg_hip_matrix* M)
     if (M->stream) (void)hipStreamSynchronize(M->stream);
     if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
     void* ptrs[] = {M->d_slice_base, M->d_cols,   M->d_vals,      M->d_aval,    M->d_aoff,     M->d_abase,
-                    M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_pbuf,    M->d_ahist,    M->d_rbuf,
+                    M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_adiag2,      M->d_pbuf,    M->d_ahist,    M->d_rbuf,
                     M->d_Ap,         M->d_x,      M->d_b,         M->d_partial, M->d_tickets,  M->d_scal,
                     M->d_kst,        M->d_hist,   M->d_stamps,    M->d_gen_b,   M->d_gen_x0,   M->d_gen_xexact,
                     M->d_send_idx,   M->d_send_buf,  M->d_emul};
@@ -590,12 +592,16 @@ int pair_windows(const std::vector<int>& off, const std::vector<int>& cnt, int s
         size_t e = j;
         while (e + 1 < u.size() && u[e + 1] - u[e] <= kSliceRows) e++;
         if (nw == kAWin) return -1;
-        win[3 * nw] = u[j];
-        win[3 * nw + 1] = rows + u[e] - u[j];
+        // even first row and length: the kernel stages row pairs with 16-B
+        // loads and stores (one extra row at most at either end)
+        const int lo = u[j] - (u[j] & 1);
+        const int len = (rows + u[e] - lo + 1) & ~1;
+        win[3 * nw] = lo;
+        win[3 * nw + 1] = len;
         win[3 * nw + 2] = base;
-        wlo.push_back(u[j]);
+        wlo.push_back(lo);
         wbase.push_back(base);
-        base += rows + u[e] - u[j];
+        base += len;
         nw++;
         j = e + 1;
     }
@@ -726,6 +732,12 @@ int build_a_image(hpccg_hip_matrix* M)
         }
     }
     halo_runs(tp, &M->halo_p_lo, &M->halo_p_hi);
+    std::vector<int> diag(S, -1);  // LDS position of offset 0 (the rows' own p_k)
+    for (int s = 0; s < S; s++)
+        for (int j = 0; j < cnt[s]; j++)
+            if (off[(size_t)s * kAMax + j] == 0) diag[s] = lds[(size_t)s * kAMax + j];
+    TRY(dev_alloc(M, &M->d_adiag2, diag.size()));
+    HIP_TRY(hipMemcpy(M->d_adiag2, diag.data(), sizeof(int) * diag.size(), hipMemcpyHostToDevice));
     TRY(dev_alloc(M, &M->d_alds2, lds.size()));
     TRY(dev_alloc(M, &M->d_awin2, win.size()));
     TRY(dev_alloc(M, &M->d_awn2, wn.size()));
@@ -923,6 +935,9 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.aoff = M->d_aoff;
     a.abase = M->d_abase;
     a.alds2 = M->d_alds2;
+    a.adiag2 = M->d_adiag2;
+    a.lds_ep = M->lds_ep;
+    a.stage16 = M->stage16;
     a.awin2 = M->d_awin2;
     a.awn2 = M->d_awn2;
     a.alds2_doubles = std::max(1, M->alds2_doubles);
@@ -2227,6 +2242,10 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "fold")) {
         if (value < -1 || value > 3) return set_err(HPCCG_HIP_EINVAL, "fold must be -1 (auto) or 0..3");
         M->fold = (int)value;
+    } else if (!std::strcmp(key, "lds_ep")) {
+        M->lds_ep = value ? 1 : 0;
+    } else if (!std::strcmp(key, "stage16")) {
+        M->stage16 = value ? 1 : 0;
     } else if (!std::strcmp(key, "a_pre")) {
         if (value != -1 && value != 0 && value != 3 && value != 4 && value != 7)
             return set_err(HPCCG_HIP_EINVAL, "a_pre must be -1 (auto), 0, 3 (width 7), 4 (width 27) or 7 (width 7)");
@@ -2265,6 +2284,8 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "graph_used")) *value = M->graph_used;
     else if (!std::strcmp(key, "force_comm")) *value = M->force_comm;
     else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
+    else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;
+    else if (!std::strcmp(key, "stage16")) *value = M->stage16;
     else if (!std::strcmp(key, "overlap")) {
         int lo, hi;
         halo_units(M, &lo, &hi);
