@@ -90,6 +90,7 @@ struct CgArgs {
     const int* adiag2;            // per slice: LDS position of offset 0 (minus the pair row), -1 none
     int lds_ep;                   // pair kernel: the rows' own p_k from the staged window
     int stage16;                  // pair kernel: stage row pairs with 16-B loads / LDS stores
+    const unsigned char* atri;    // direct kernel: per slice, 1 = offsets in the width's triple plan (null: off)
     int alds2_doubles;            // dynamic LDS per two-slice block
 };
 

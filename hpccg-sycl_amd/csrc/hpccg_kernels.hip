@@ -78,6 +78,21 @@ __device__ __forceinline__ double from_lane_plus(double v)
     return __hiloint2double(rhi, rlo);
 }
 
+// Whole-wave lane shifts (DPP wave_shr:1 / wave_shl:1): lane l receives lane
+// l - 1 / l + 1; lane 0 / lane 63 receive 0.0 (the caller loads those itself).
+__device__ __forceinline__ double wave_shr1(double v)
+{
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, 0x138, 0xF, 0xF, false),
+                            __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double wave_shl1(double v)
+{
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, 0x130, 0xF, 0xF, false),
+                            __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xF, 0xF, false));
+}
+
 // Wave sum, result valid in LANE 0 only. Fixed tree: v_l += v_{l+off} for
 // off = 32, 16, 8, 4, 2, 1 (lanes >= off are don't-care).
 __device__ __forceinline__ double wave_sum(double v)
@@ -560,7 +575,18 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(CgArgs a, bool prologue)
 // rank, never the prologue): x = r + beta*p_{k-1} formed per load, k_p_update's
 // exact expression, so every row sum is unchanged.
 // ---------------------------------------------------------------------------
-template <int kW, bool kNT, bool kFuse, int kPre>
+// Triple plan of the 7-point width: slot groups in slot order -- z-, y-, the
+// x triple (offsets -1, 0, +1), y+, z+. A slice whose offsets group exactly so
+// (atri[s], checked on the host) reads x once for the triple: its centre pair,
+// the neighbours' rows from the adjacent lanes (wave_shr1 / wave_shl1), lanes
+// 0 and 63 loading their one outside value. Same x values, same products,
+// same order: same bits. 7-pt 256^3 same-process A/B: 2679 vs 2641 it/s. (The
+// 27-wide plan, nine triples, needs 83+ VGPRs and measured 52 vs 45 us at 100^3.)
+__host__ __device__ constexpr int tri_groups(int w) { return w == 7 ? 5 : 0; }
+__host__ __device__ constexpr int tri_first(int w, int g) { return g <= 2 ? g : g + 2; }
+__host__ __device__ constexpr int tri_size(int w, int g) { return g == 2 ? 3 : 1; }
+
+template <int kW, bool kNT, bool kFuse, int kPre, bool kTri = false>
 __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 {
     static_assert(kPre == 0 || (kW > 0 && kPre <= kW), "early loads need the uniform width");
@@ -590,6 +616,57 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
     const double* __restrict__ vp = a.aval + vb * kSliceRows + (size_t)threadIdx.x * kRpt;
     const int* __restrict__ off = a.aoff + (size_t)s * kAMax;
     double sum[kRpt] = {0.0, 0.0};
+    if constexpr (kTri && tri_groups(kW) > 0 && kPre > 0) {
+        if (a.atri[s]) {
+            auto xpair = [&](int o) -> Rows {
+                if constexpr (kFuse) {
+                    const Rows rv = ld_u(rr_ + o);
+                    const Rows yv = ld_u(py + o);
+                    return Rows{{rv.v[0] + st.beta * yv.v[0], rv.v[1] + st.beta * yv.v[1]}};
+                } else {
+                    return ld_u(xr + o);
+                }
+            };
+            auto x1 = [&](int o) -> double {
+                if constexpr (kFuse)
+                    return rr_[o] + st.beta * py[o];
+                else
+                    return xr[o];
+            };
+            auto val = [&](int j) -> Rows { return j < kPre ? vpre[j] : ld_m<kNT>(vp + (size_t)j * kSliceRows); };
+            const int lane = threadIdx.x & (kWave - 1);
+            auto triple = [&](const Rows& v0, const Rows& v1, const Rows& v2, int o) {
+                const Rows c = xpair(o);
+                double left = wave_shr1(c.v[1]);
+                double right = wave_shl1(c.v[0]);
+                if (lane == 0) left = x1(o - 1);
+                if (lane == kWave - 1) right = x1(o + 2);
+                sum[0] = sum[0] + v0.v[0] * left;
+                sum[1] = sum[1] + v0.v[1] * c.v[0];
+                sum[0] = sum[0] + v1.v[0] * c.v[0];
+                sum[1] = sum[1] + v1.v[1] * c.v[1];
+                sum[0] = sum[0] + v2.v[0] * c.v[1];
+                sum[1] = sum[1] + v2.v[1] * right;
+            };
+#pragma unroll
+            for (int g = 0; g < tri_groups(kW); g++) {
+                const int j0 = tri_first(kW, g);
+                if (tri_size(kW, g) == 1) {
+                    const Rows v = val(j0);
+                    const Rows xv = xpair(offp[j0]);
+#pragma unroll
+                    for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xv.v[i];
+                } else {
+                    triple(val(j0), val(j0 + 1), val(j0 + 2), offp[j0 + 1]);
+                }
+            }
+            const double d = spmv_rows_out<kFuse>(a, st, prologue, row, sum);
+            if (prologue) return;
+            const double bs = block_sum<kBlock>(d);
+            complete_dot(a, s, bs, kPAP, st.k);
+            return;
+        }
+    }
 #pragma unroll kW > 0 ? kW : 4
     for (int j = 0; j < wdt; j++) {
         Rows v;
@@ -1221,12 +1298,16 @@ bool spmv_kernel_ok(int kernel) { return kernel >= kSpmvSell && kernel <= kSpmvP
 void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
 {
     const bool fuse = a.fuse_p && !prologue;
-#define HPCCG_A(W, NT, PRE)                                                                                 \
-    do {                                                                                                    \
-        if (fuse)                                                                                           \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue); \
-        else                                                                                                \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue); \
+#define HPCCG_A(W, NT, PRE)                                                                                       \
+    do {                                                                                                          \
+        if (a.atri && tri_groups(W) > 0 && PRE > 0 && fuse)                                                     \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE, true>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue); \
+        else if (a.atri && tri_groups(W) > 0 && PRE > 0)                                                        \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE, true>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue); \
+        else if (fuse)                                                                                            \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue);       \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue);      \
     } while (0)
     switch (kernel) {
     case kSpmvPairs: {

@@ -219,6 +219,7 @@ struct hpccg_hip_matrix {
     int a_pre = -1;       // direct kernel prefetch depth (-1 auto: 4 at width 27, 7 at width 7)
     int lds_ep = 1;       // pair kernel: own p_k from the staged window
     int stage16 = 1;      // pair kernel: 16-B staging of row pairs
+    int tri = 1;          // direct kernel, width 7: x triple from adjacent lanes where the slice allows
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
                           // 2 also the multi-rank iteration with a self send/recv as its halo
@@ -235,6 +236,7 @@ struct hpccg_hip_matrix {
     unsigned int* d_abase = nullptr;
     int has_pairs = 0, alds2_doubles = 0;
     int *d_alds2 = nullptr, *d_awin2 = nullptr, *d_awn2 = nullptr, *d_adiag2 = nullptr;
+    unsigned char* d_atri = nullptr;  // direct kernel: slices in the width's triple plan
     // workspace (padded to a multiple of kSliceRows rows)
     size_t npad = 0;
     double* d_pbuf = nullptr;  // ring_alloc buffers of [guard | ghost_lo_pad | npad | ghost_hi_pad | guard]
@@ -305,7 +307,7 @@ int free_matrix(hpccg_hip_matrix* M)
     if (M->stream) (void)hipStreamSynchronize(M->stream);
     if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
     void* ptrs[] = {M->d_slice_base, M->d_cols,   M->d_vals,      M->d_aval,    M->d_aoff,     M->d_abase,
-                    M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_adiag2,      M->d_pbuf,    M->d_ahist,    M->d_rbuf,
+                    M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_adiag2,     M->d_atri,      M->d_pbuf,    M->d_ahist,    M->d_rbuf,
                     M->d_Ap,         M->d_x,      M->d_b,         M->d_partial, M->d_tickets,  M->d_scal,
                     M->d_kst,        M->d_hist,   M->d_stamps,    M->d_gen_b,   M->d_gen_x0,   M->d_gen_xexact,
                     M->d_send_idx,   M->d_send_buf,  M->d_emul};
@@ -716,6 +718,26 @@ int build_a_image(hpccg_hip_matrix* M)
         }
         halo_runs(t, &M->halo_s_lo, &M->halo_s_hi);
     }
+    // 7-pt triple plan of the direct kernel (tri_first / tri_size in hpccg_kernels.hip):
+    // the slice's offsets, grouped greedily into runs of three consecutive
+    // offsets, form exactly the width's group sequence
+    if (M->a_width == 7) {
+        std::vector<unsigned char> tri(S, 0);
+        for (int s = 0; s < S; s++) {
+            if (cnt[s] != M->a_width) continue;
+            const int* o = &off[(size_t)s * kAMax];
+            std::vector<int> sizes;
+            for (int j = 0; j < cnt[s];) {
+                const bool t3 = j + 2 < cnt[s] && o[j + 1] == o[j] + 1 && o[j + 2] == o[j] + 2;
+                sizes.push_back(t3 ? 3 : 1);
+                j += t3 ? 3 : 1;
+            }
+            const std::vector<int> want{1, 1, 3, 1, 1};
+            tri[s] = sizes == want ? 1 : 0;
+        }
+        TRY(dev_alloc(M, &M->d_atri, tri.size()));
+        HIP_TRY(hipMemcpy(M->d_atri, tri.data(), tri.size(), hipMemcpyHostToDevice));
+    }
     // pair windows
     const int NP = (S + 1) / 2;
     std::vector<int> lds((size_t)S * kAMax, 0), win((size_t)NP * kAWin * 3, 0), wn(NP, 0);
@@ -936,6 +958,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.abase = M->d_abase;
     a.alds2 = M->d_alds2;
     a.adiag2 = M->d_adiag2;
+    a.atri = M->tri ? M->d_atri : nullptr;
     a.lds_ep = M->lds_ep;
     a.stage16 = M->stage16;
     a.awin2 = M->d_awin2;
@@ -2244,6 +2267,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->fold = (int)value;
     } else if (!std::strcmp(key, "lds_ep")) {
         M->lds_ep = value ? 1 : 0;
+    } else if (!std::strcmp(key, "tri")) {
+        M->tri = value ? 1 : 0;
     } else if (!std::strcmp(key, "stage16")) {
         M->stage16 = value ? 1 : 0;
     } else if (!std::strcmp(key, "a_pre")) {
@@ -2286,6 +2311,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
     else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;
     else if (!std::strcmp(key, "stage16")) *value = M->stage16;
+    else if (!std::strcmp(key, "tri")) *value = M->tri;
     else if (!std::strcmp(key, "overlap")) {
         int lo, hi;
         halo_units(M, &lo, &hi);

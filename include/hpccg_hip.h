@@ -158,6 +158,8 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   window instead of reloading r and p_{k-1} (default 1)
  *   "stage16"       pair kernel: windows staged as row pairs with 16-B loads
  *                   and LDS stores (default 1; 0 = one row per thread)
+ *   "tri"           direct kernel at width 7: the x triple (offsets -1, 0, +1)
+ *                   read once, neighbours from adjacent lanes (default 1)
  *   "a_pre"         direct SELL-512-A kernel: value slots loaded before the
  *                   iteration test, -1 auto (4 at width 27, 7 at width 7), 0,
  *                   3 or 7 (width 7), 4 (width 27)

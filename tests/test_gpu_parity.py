@@ -98,7 +98,22 @@ def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
         assert M.get_option("spmv_kernel") == kernel
         assert M.get_option("fuse_p") == (1 if (fuse and kernel != SELL) else 0)
         out[(kernel, fuse)] = solve_bits(hp, M, prob.b, 120)
-    assert all(o == out[(SELL, 0)] for o in out.values())
+    # the direct kernel's variants: prefetch depth; at width 7 the x triple read
+    # once and shared across lanes (tri), the pair kernel's staging forms
+    M.set_option("spmv_kernel", DIRECT)
+    for fuse, pre, tri in itertools.product((0, -1), ((0, 3, 7) if s7 else (0, 4)), (0, 1)):
+        M.set_option("fuse_p", fuse)
+        M.set_option("a_pre", pre)
+        M.set_option("tri", tri)
+        out[("direct", fuse, pre, tri)] = solve_bits(hp, M, prob.b, 120)
+    M.set_option("spmv_kernel", PAIRS)
+    for fuse, st16, ep in itertools.product((0, -1), (0, 1), (0, 1)):
+        M.set_option("fuse_p", fuse)
+        M.set_option("stage16", st16)
+        M.set_option("lds_ep", ep)
+        out[("pairs", fuse, st16, ep)] = solve_bits(hp, M, prob.b, 120)
+    bad = [k for k, o in out.items() if o != out[(SELL, 0)]]
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("dims", [(24, 20, 18), (13, 7, 5), (40, 40, 40)])
