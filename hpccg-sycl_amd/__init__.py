@@ -59,13 +59,14 @@ def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise HPCCGError(f"{LIB_PATH} missing: run build() (the HIP path has no CPU fallback)")
+    path = os.environ.get("HPCCG_HIP_LIB", LIB_PATH)  # diagnostics: A/B against another build
+    if not os.path.exists(path):
+        raise HPCCGError(f"{path} missing: run build() (the HIP path has no CPU fallback)")
     try:  # share torch's HIP runtime when torch is around (same sonames)
         import torch  # noqa: F401
     except Exception:
         pass
-    L = C.CDLL(LIB_PATH)  # RTLD_LOCAL: never interpose HPCCG() into other libraries
+    L = C.CDLL(path)  # RTLD_LOCAL: never interpose HPCCG() into other libraries
     vp, ip, dp, lp = C.c_void_p, C.c_int, C.c_double, C.c_longlong
     PI, PD = C.POINTER(C.c_int), C.POINTER(C.c_double)
     sig = {

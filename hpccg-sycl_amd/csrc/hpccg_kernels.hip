@@ -357,6 +357,20 @@ __device__ __forceinline__ void complete_dot(const CgArgs& a, int s, double bs, 
     complete_dot_lanes(a, s, 1, bs, which, k);
 }
 
+// The SpMV of iteration k publishes {k, run} (kst[4..5]) for the kernels that
+// follow it in the iteration (update, finalize): one 8-byte load gives them
+// both, instead of k and then the history value the loop test depends on.
+__device__ __forceinline__ void publish_iter(const CgArgs& a, int k, bool run)
+{
+    *reinterpret_cast<int2*>(a.kst + 4) = make_int2(k, run ? 1 : 0);
+}
+__device__ __forceinline__ bool iter_of(const CgArgs& a, int& k)
+{
+    const int2 v = *reinterpret_cast<const int2*>(a.kst + 4);
+    k = v.x;
+    return v.y != 0;
+}
+
 // Iteration state every SpMV kernel reads first: k, and for the fused p update
 // r_{k-1}.r_{k-1} and beta. Returns false when the solve has ended.
 struct IterState {
@@ -376,6 +390,7 @@ __device__ __forceinline__ bool spmv_begin(const CgArgs& a, bool prologue, IterS
     if (kFuse) st.rr = a.g[kRR];
     const bool run = cg_run(a, st.k, kFuse, st.rr);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+        publish_iter(a, st.k, run);
         if (kFuse && (st.k == 1 || run)) a.hist[st.k - 1] = st.rr;
         if (run)
             stamp(a, st.k, kStampSpmv);
@@ -901,7 +916,9 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
     const bool in_lds = ng <= kFinLdsGroups;
     double* gp = a.partial + a.nslices + which * ng;
     const int lane = threadIdx.x & (kWave - 1);
-    const int k = prologue ? 0 : a.kst[0];
+    int k = 0;
+    bool run = true;
+    if (!prologue) run = iter_of(a, k);
     // stamped unconditionally: stamps after the end stamp are dropped on the host
     if (threadIdx.x == 0) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
     if (ng <= 4 * (kFinalizeThreads / kWave))
@@ -910,7 +927,6 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
         finalize_groups<16>(a, ng, in_lds, gs, gp);
     else
         finalize_groups<32>(a, ng, in_lds, gs, gp);
-    const bool run = prologue || cg_run(a, k, false);
     if (!run) {
         if (threadIdx.x == 0) mark_end(a);
         return;
@@ -968,8 +984,7 @@ __global__ __launch_bounds__(kBlock) void k_update(CgArgs a)
 {
     int k = 0;
     if constexpr (!kPrologue) {
-        k = a.kst[0];
-        const bool run = cg_run(a, k, false);
+        const bool run = iter_of(a, k);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             if (run)
                 stamp(a, k, kStampUpdate);
