@@ -179,6 +179,14 @@ __device__ __forceinline__ Rows ld_u(const double* __restrict__ p)
     return Rows{{t.x, t.y}};
 }
 
+// Load through the constant address space: a scalar load (s_load) for a
+// wave-uniform address. Only for data no kernel of the same launch writes.
+template <class T>
+__device__ __forceinline__ T sld(const T* p)
+{
+    return *(const __attribute__((address_space(4))) T*)(p);
+}
+
 // Matrix streams: non-temporal when the image is far beyond the Infinity
 // Cache (read once per SpMV; keeps L2 for the vectors).
 template <bool kNT>
@@ -724,11 +732,158 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 // is bitwise the one-slice kernels'. 27-pt 200^3: a plane window covers 1024
 // rows for 1426 staged doubles (4.2 per row).
 // ---------------------------------------------------------------------------
+// The pair's windows into LDS (xs): fused, p_k = r + beta*p_{k-1} per staged
+// own row; ghost rows of a multi-rank slab come from the halo, guard rows are
+// zeros. stage16: row pairs (the windows' first row, length and LDS base are
+// even, pair_windows) with 16-B loads and LDS stores.
+template <bool kFuse>
+__device__ __forceinline__ void stage_pair_windows(const CgArgs& a, const IterState& st, int P, const double* __restrict__ p,
+                                                   const double* __restrict__ pold, double* __restrict__ xs)
+{
+    const int prow0 = 2 * P * kSliceRows;  // first row of the pair
+    const int nw = a.awn2[P];
+    const int* __restrict__ win = a.awin2 + (size_t)P * kAWin * 3;
+    for (int w = 0; w < nw; w++) {
+        const int st0 = prow0 + win[3 * w], len = win[3 * w + 1], base = win[3 * w + 2];
+        if (a.stage16) {
+            for (int i = 2 * threadIdx.x; i < len; i += 4 * kBlock) {
+                const int l = st0 + i;  // local rows l, l + 1 (< 0 / >= n: ghosts, guard or padding zeros)
+                d2v v;
+                if constexpr (kFuse) {
+                    if (l >= 0 && l + 1 < a.n) {  // both own rows (r has no ghost region)
+                        const d2v rv = *reinterpret_cast<const d2v*>(a.r + l);
+                        const d2v yv = *reinterpret_cast<const d2v*>(pold + l);
+                        v.x = rv.x + st.beta * yv.x;
+                        v.y = rv.y + st.beta * yv.y;
+                    } else {
+                        v.x = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
+                        v.y = ((unsigned)(l + 1) < (unsigned)a.n) ? a.r[l + 1] + st.beta * pold[l + 1] : p[l + 1];
+                    }
+                } else {
+                    v = *reinterpret_cast<const d2v*>(p + l);
+                }
+                *reinterpret_cast<d2v*>(xs + base + i) = v;
+            }
+        } else {
+            for (int i = threadIdx.x; i < len; i += 2 * kBlock) {
+                const int l = st0 + i;  // local row (< 0 / >= n: ghosts, guard or padding zeros)
+                if constexpr (kFuse)
+                    xs[base + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
+                else
+                    xs[base + i] = p[l];
+            }
+        }
+    }
+}
+
+// stage_pair_windows with every load of a round issued before its LDS
+// stores: the pair's windows are one LDS range [0, tot) (pair_windows lays
+// them out back to back, even bases and lengths), each thread stages the row
+// pairs e = 2 t + 1024 u of it, kU per round. Same values as
+// stage_pair_windows (stage16).
+template <bool kFuse, int kU = 5>
+__device__ __forceinline__ void stage_pair_windows_batched(const CgArgs& a, const IterState& st, int P,
+                                                           const double* __restrict__ p, const double* __restrict__ pold,
+                                                           double* __restrict__ xs)
+{
+    const int prow0 = 2 * P * kSliceRows;
+    const int nw = sld(a.awn2 + P);  // P is wave-uniform: the tables come through the scalar cache
+    const int* __restrict__ win = a.awin2 + (size_t)P * kAWin * 3;
+    int wlo[kAWin], wbase[kAWin];
+#pragma unroll
+    for (int w = 0; w < kAWin; w++) {
+        wlo[w] = w < nw ? sld(win + 3 * w) : 0;
+        wbase[w] = w < nw ? sld(win + 3 * w + 2) : INT_MAX;
+    }
+    const int tot = sld(win + 3 * (nw - 1) + 2) + sld(win + 3 * (nw - 1) + 1);
+    for (int e0 = 2 * (int)threadIdx.x; e0 < tot; e0 += 4 * kBlock * kU) {
+        d2v rv[kU], yv[kU];
+        unsigned direct = 0;  // bit u: rv[u] holds the staged values themselves
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int e = e0 + 4 * kBlock * u;
+            if (e < tot) {
+                int lo = wlo[0], base = wbase[0];
+#pragma unroll
+                for (int w = 1; w < kAWin; w++)
+                    if (e >= wbase[w]) lo = wlo[w], base = wbase[w];
+                const int l = prow0 + lo + (e - base);  // local rows l, l + 1
+                if (!kFuse) {
+                    rv[u] = *reinterpret_cast<const d2v*>(p + l);
+                    direct |= 1u << u;
+                } else if (l >= 0 && l + 1 < a.n) {
+                    rv[u] = *reinterpret_cast<const d2v*>(a.r + l);
+                    yv[u] = *reinterpret_cast<const d2v*>(pold + l);
+                } else {  // ghosts, guard or padding zeros; an own row beside them
+                    rv[u].x = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
+                    rv[u].y = ((unsigned)(l + 1) < (unsigned)a.n) ? a.r[l + 1] + st.beta * pold[l + 1] : p[l + 1];
+                    direct |= 1u << u;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int e = e0 + 4 * kBlock * u;
+            if (e < tot) {
+                d2v v = rv[u];
+                if (!(direct & (1u << u))) {
+                    v.x = rv[u].x + st.beta * yv[u].x;
+                    v.y = rv[u].y + st.beta * yv[u].y;
+                }
+                *reinterpret_cast<d2v*>(xs + e) = v;
+            }
+        }
+    }
+}
+
+// The pair kernel's epilogue: Ap, p_k (from the window when lds_ep), the two
+// slices' p.Ap partials with block_sum<256>'s shape, completed (fold) or stored.
+template <bool kFuse>
+__device__ __forceinline__ void pair_epilogue(const CgArgs& a, const IterState& st, bool prologue, int P, int s, bool have,
+                                              int lrow, const double* __restrict__ xs, const double (&sum)[kRpt])
+{
+    __shared__ double wsum[2 * kBlock / kWave];
+    double d = 0.0;
+    if (have) {
+        const int prow = (threadIdx.x / kBlock) * kSliceRows + lrow;  // row within the pair
+        const int pd = a.adiag2 ? a.adiag2[s] : -1;  // LDS position of the slice's offset 0
+        if (pd >= 0 && a.lds_ep) {
+            const Rows pk{{xs[prow + pd], xs[prow + pd + 1]}};
+            d = spmv_rows_out<kFuse>(a, st, prologue, s * kSliceRows + lrow, sum, &pk);
+        } else {
+            d = spmv_rows_out<kFuse>(a, st, prologue, s * kSliceRows + lrow, sum);
+        }
+    }
+    if (prologue) return;
+    const double wv = wave_sum(d);
+    const int lane = threadIdx.x & (kWave - 1);
+    if (lane == 0) wsum[threadIdx.x / kWave] = wv;
+    __syncthreads();
+    if (threadIdx.x >= kWave) return;
+    constexpr int kWh = kBlock / kWave;
+    double bs = 0.0;
+    if (lane < 2) {
+#pragma unroll
+        for (int i = 0; i < kWh; i++) bs += wsum[lane * kWh + i];
+    }
+    complete_dot_lanes(a, 2 * P, min(2, a.nslices - 2 * P), bs, kPAP, st.k);
+}
+
+// ---------------------------------------------------------------------------
+// SELL-512-A with x from LDS windows shared by slice pairs: block P owns
+// slices 2P and 2P + 1 with 512 threads (waves 0-3 slice 2P, 4-7 slice
+// 2P + 1, two rows per thread). The pair's windows (one per offset cluster:
+// one per z-plane for the 27-pt stencil, holes included) are staged first
+// (stage_pair_windows). Slot j then reads xs[pair row + alds[s][j]]: one
+// per-slice scalar per slot. kPre value slots are loaded before the iteration
+// test. Each half forms its slice's partial with block_sum<256>'s shape, so
+// the dot is bitwise the one-slice kernels'. 27-pt 200^3: a plane window
+// covers 1024 rows for 1426 staged doubles (4.2 per row).
+// ---------------------------------------------------------------------------
 template <bool kNT, bool kFuse, int kPre>
 __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2(CgArgs a, bool prologue)
 {
     extern __shared__ __attribute__((aligned(16))) double xs[];
-    __shared__ double wsum[2 * kBlock / kWave];
     const int P = unit_of(a);  // pair: all, or the interior / halo runs
     const int half = threadIdx.x / kBlock;
     const int s = P < 0 ? a.nslices : 2 * P + half;
@@ -744,50 +899,13 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2(CgArgs a, bool prologue)
     IterState st;
     if (!spmv_begin<kFuse>(a, prologue, st)) return;
     if (P < 0 || 2 * P >= a.nslices) return;
-    double* __restrict__ p = cur_p(a, st.k);
+    const double* __restrict__ p = cur_p(a, st.k);
     const double* __restrict__ pold = a.r;
     if constexpr (kFuse) pold = (st.k == 1) ? a.r : cur_p(a, st.k - 1);
-    const int prow0 = 2 * P * kSliceRows;  // first row of the pair
-    {
-        const int nw = a.awn2[P];
-        const int* __restrict__ win = a.awin2 + (size_t)P * kAWin * 3;
-        for (int w = 0; w < nw; w++) {
-            const int st0 = prow0 + win[3 * w], len = win[3 * w + 1], base = win[3 * w + 2];
-            if (a.stage16) {
-                // row pairs: first row, length and LDS base are even (pair_windows)
-                for (int i = 2 * threadIdx.x; i < len; i += 4 * kBlock) {
-                    const int l = st0 + i;  // local rows l, l + 1 (< 0 / >= n: ghosts, guard or padding zeros)
-                    d2v v;
-                    if constexpr (kFuse) {
-                        if (l >= 0 && l + 1 < a.n) {  // both own rows (r has no ghost region)
-                            const d2v rv = *reinterpret_cast<const d2v*>(a.r + l);
-                            const d2v yv = *reinterpret_cast<const d2v*>(pold + l);
-                            v.x = rv.x + st.beta * yv.x;
-                            v.y = rv.y + st.beta * yv.y;
-                        } else {
-                            v.x = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
-                            v.y = ((unsigned)(l + 1) < (unsigned)a.n) ? a.r[l + 1] + st.beta * pold[l + 1] : p[l + 1];
-                        }
-                    } else {
-                        v = *reinterpret_cast<const d2v*>(p + l);
-                    }
-                    *reinterpret_cast<d2v*>(xs + base + i) = v;
-                }
-            } else {
-                for (int i = threadIdx.x; i < len; i += 2 * kBlock) {
-                    const int l = st0 + i;  // local row (< 0 / >= n: ghosts, guard or padding zeros)
-                    if constexpr (kFuse)
-                        xs[base + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
-                    else
-                        xs[base + i] = p[l];
-                }
-            }
-        }
-    }
+    stage_pair_windows<kFuse>(a, st, P, p, pold, xs);
     __syncthreads();
-    double d = 0.0;
+    double sum[kRpt] = {0.0, 0.0};
     if (have) {
-        double sum[kRpt] = {0.0, 0.0};
         const int* __restrict__ cl = a.alds2 + (size_t)s * kAMax;
         const int prow = half * kSliceRows + lrow;  // row within the pair
 #pragma unroll
@@ -805,28 +923,121 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2(CgArgs a, bool prologue)
 #pragma unroll
             for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xs[c + i];
         }
-        const int pd = a.adiag2 ? a.adiag2[s] : -1;  // LDS position of the slice's offset 0
-        if (pd >= 0 && a.lds_ep) {
-            const Rows pk{{xs[prow + pd], xs[prow + pd + 1]}};
-            d = spmv_rows_out<kFuse>(a, st, prologue, s * kSliceRows + lrow, sum, &pk);
-        } else {
-            d = spmv_rows_out<kFuse>(a, st, prologue, s * kSliceRows + lrow, sum);
+    }
+    pair_epilogue<kFuse>(a, st, prologue, P, s, have, lrow, xs, sum);
+}
+
+// ---------------------------------------------------------------------------
+// The pair kernel with the value stream through LDS-DMA (uniform width kW):
+// every wave owns 128 rows of one slice and streams their value slots from
+// HBM straight into a private ring of kR 1-KB LDS entries
+// (global_load_lds_dwordx4, non-temporal; lane l's 16 B land at entry + 16 l
+// and are read back by lane l). The first kR slots are issued before the
+// iteration test, so they land while the windows are staged; each consumed
+// entry is refilled with slot j + kR right away, a counted vmcnt wait ahead
+// of each read. No value occupies a VGPR across the staging barrier.
+// The iteration state and the window/offset tables come through the scalar
+// cache, so nothing but the ring is counted on vmcnt in the slot loop.
+// 27-pt 200^3, same-process A/B (tools/ab_inproc.py): SpMV 337.8 us at kR = 3
+// (2579 CG it/s) against 342.0 / 343.5 us at kR = 2 / 4 and 355.1 us for the
+// register pair kernel (2469 it/s); storing Ap and p_k after the p.Ap ticket
+// instead measured 341.8 us. Same products in the same order: same bits.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void vm_wait(int n)  // n: a constant after unrolling
+{
+    switch (n) {
+#define HPCCG_VMW(i) \
+    case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+        HPCCG_VMW(0) HPCCG_VMW(1) HPCCG_VMW(2) HPCCG_VMW(3) HPCCG_VMW(4) HPCCG_VMW(5) HPCCG_VMW(6) HPCCG_VMW(7)
+#undef HPCCG_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr int kA2RingMax = 4;
+
+
+template <bool kFuse, int kW, int kR>
+__global__ __launch_bounds__(2 * kBlock) void k_spmv_a2r(CgArgs a, bool prologue)
+{
+    static_assert(kR >= 1 && kR <= kA2RingMax && kR <= kW, "ring depth");
+    extern __shared__ __attribute__((aligned(16))) double xs[];
+    const int P = unit_of(a);
+    const int half = threadIdx.x / kBlock;
+    const int s = P < 0 ? a.nslices : 2 * P + half;
+    const bool have = s < a.nslices;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int lrow = (threadIdx.x % kBlock) * kRpt;  // row within the slice: wave's 128 rows, lane-linear
+    // an odd last pair's second half streams its partner's values (never used)
+    const double* __restrict__ vp = a.aval + (size_t)(have ? s : s - 1) * kW * kSliceRows + lrow;
+    double* __restrict__ ring = xs + ((a.alds2_doubles + 1) & ~1) + (threadIdx.x / kWave) * (kR * 2 * kWave);
+    if (P < 0 || 2 * P >= a.nslices) return;
+#pragma unroll
+    for (int j = 0; j < kR; j++)
+        __builtin_amdgcn_global_load_lds((const void*)(vp + (size_t)j * kSliceRows), (lds_void*)(ring + j * 2 * kWave),
+                                         16, 0, 2 /* nt */);
+    // the slot offsets: scalar loads (slice index made wave-uniform), all
+    // before the ring is counted, so no vector load lands among the DMAs
+    const int su = __builtin_amdgcn_readfirstlane(have ? s : s - 1);
+    typedef const __attribute__((address_space(4))) int* cint_p;  // constant space: s_load
+    const cint_p cl = (cint_p)(a.alds2 + (size_t)su * kAMax);
+    int clv[kW];
+#pragma unroll
+    for (int j = 0; j < kW; j++) clv[j] = cl[j];
+    // iteration state through the scalar cache (s_load counts on lgkmcnt, so
+    // it does not queue behind the ring's DMAs on vmcnt); written by earlier
+    // kernels only
+    IterState st;
+    st.k = 0;
+    st.rr = 0.0;
+    st.beta = 0.0;
+    bool run = true;
+    if (!prologue) {
+        st.k = sld(a.kst);
+        if (kFuse) st.rr = sld(a.g + kRR);
+        const double h1 = sld(a.hist + max(st.k - 2, 0));  // r_{k-2}.r_{k-2} (k >= 2)
+        run = st.k < a.max_iter && sqrt(st.k == 1 ? (kFuse ? st.rr : sld(a.hist)) : h1) > a.tol;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            publish_iter(a, st.k, run);
+            if (kFuse && (st.k == 1 || run)) a.hist[st.k - 1] = st.rr;
+            if (run)
+                stamp(a, st.k, kStampSpmv);
+            else
+                mark_end(a);
+        }
+        if (kFuse && run) st.beta = (st.k == 1) ? 0.0 : st.rr / h1;
+    }
+    if (!run) {
+        vm_wait(0);  // no DMA may land after the block's LDS is released
+        return;
+    }
+    const double* __restrict__ p = cur_p(a, st.k);
+    const double* __restrict__ pold = a.r;
+    if constexpr (kFuse) pold = (st.k == 1) ? a.r : cur_p(a, st.k - 1);
+    if (a.stage16)
+        stage_pair_windows_batched<kFuse>(a, st, P, p, pold, xs);
+    else
+        stage_pair_windows<kFuse>(a, st, P, p, pold, xs);
+    // raw barrier: __syncthreads() would drain the ring (vmcnt(0))
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int prow = half * kSliceRows + lrow;  // row within the pair
+    double sum[kRpt] = {0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < kW; j++) {
+        vm_wait((j + kR < kW ? j + kR : kW) - j - 1);  // slot j has landed
+        const d2v v = *reinterpret_cast<const d2v*>(ring + (j % kR) * 2 * kWave + 2 * lane);
+        const int c = prow + clv[j];
+        sum[0] = sum[0] + v.x * xs[c];
+        sum[1] = sum[1] + v.y * xs[c + 1];
+        asm volatile("" : "+v"(sum[0]), "+v"(sum[1]));  // keep the products here (else 220 VGPRs)
+        if (j + kR < kW) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry read before its refill lands
+            __builtin_amdgcn_global_load_lds((const void*)(vp + (size_t)(j + kR) * kSliceRows),
+                                             (lds_void*)(ring + (j % kR) * 2 * kWave), 16, 0, 2);
         }
     }
-    if (prologue) return;
-    // per-slice partials with block_sum<256>'s shape
-    const double wv = wave_sum(d);
-    const int lane = threadIdx.x & (kWave - 1);
-    if (lane == 0) wsum[threadIdx.x / kWave] = wv;
-    __syncthreads();
-    if (threadIdx.x >= kWave) return;
-    constexpr int kWh = kBlock / kWave;
-    double bs = 0.0;
-    if (lane < 2) {
-#pragma unroll
-        for (int i = 0; i < kWh; i++) bs += wsum[lane * kWh + i];
-    }
-    complete_dot_lanes(a, 2 * P, min(2, a.nslices - 2 * P), bs, kPAP, st.k);
+    pair_epilogue<kFuse>(a, st, prologue, P, s, have, lrow, xs, sum);
 }
 
 // Plain SpMV on a caller's x (kernel-level C ABI, HPC_sparsemv.cpp:68-89):
@@ -1305,6 +1516,27 @@ void launch_cg_pack(const CgArgs& a, const int* idx, int cnt, double* buf, bool 
 
 bool spmv_kernel_ok(int kernel) { return kernel >= kSpmvSell && kernel <= kSpmvPairs; }
 
+size_t a2_lds_bytes(int lds_doubles, int ring)
+{
+    if (ring <= 0) return (size_t)lds_doubles * sizeof(double);
+    return (size_t)((lds_doubles + 1) & ~1) * sizeof(double) + (size_t)(2 * kBlock / kWave) * ring * 2 * kWave * sizeof(double);
+}
+
+// The ring kernels may need more than the 64 KB default dynamic LDS.
+int a2_ring_prepare()
+{
+    const int lim = 160 * 1024 - 1024;
+    hipError_t e = hipSuccess;
+#define HPCCG_A2R_ATTR(R)                                                                                               \
+    if (e == hipSuccess)                                                                                                \
+        e = hipFuncSetAttribute((const void*)k_spmv_a2r<true, 27, R>, hipFuncAttributeMaxDynamicSharedMemorySize, lim); \
+    if (e == hipSuccess)                                                                                                \
+        e = hipFuncSetAttribute((const void*)k_spmv_a2r<false, 27, R>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    HPCCG_A2R_ATTR(1) HPCCG_A2R_ATTR(2) HPCCG_A2R_ATTR(3) HPCCG_A2R_ATTR(4)
+#undef HPCCG_A2R_ATTR
+    return e == hipSuccess ? 0 : -1;
+}
+
 // The SpMV of one CG iteration (or of the prologue). Template choice:
 //   kSpmvSell   k_spmv_sell, non-temporal above the Infinity Cache (a.nt)
 //   kSpmvDirect k_spmv_a: width 27 with 4 value slots and the offsets early,
@@ -1326,6 +1558,24 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     } while (0)
     switch (kernel) {
     case kSpmvPairs: {
+        if (a.a2_ring > 0) {
+            const size_t smem = a2_lds_bytes(a.alds2_doubles, a.a2_ring);
+#define HPCCG_A2R(R)                                                                                              \
+    do {                                                                                                          \
+        if (fuse)                                                                                                 \
+            hipLaunchKernelGGL((k_spmv_a2r<true, 27, R>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue); \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_spmv_a2r<false, 27, R>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue); \
+    } while (0)
+            switch (a.a2_ring) {
+            case 1: HPCCG_A2R(1); break;
+            case 2: HPCCG_A2R(2); break;
+            case 3: HPCCG_A2R(3); break;
+            default: HPCCG_A2R(4); break;
+            }
+#undef HPCCG_A2R
+            break;
+        }
         const size_t smem = (size_t)a.alds2_doubles * sizeof(double);
         if (fuse)
             hipLaunchKernelGGL((k_spmv_a2<true, true, 3>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue);

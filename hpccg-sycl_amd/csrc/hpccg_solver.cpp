@@ -219,6 +219,7 @@ struct hpccg_hip_matrix {
     int a_pre = -1;       // direct kernel prefetch depth (-1 auto: 4 at width 27, 7 at width 7)
     int lds_ep = 1;       // pair kernel: own p_k from the staged window
     int stage16 = 1;      // pair kernel: 16-B staging of row pairs
+    int a2_ring = kA2RingDefault;  // pair kernel: LDS-DMA value ring depth per wave (0: register loads; width 27 only)
     int tri = 1;          // direct kernel, width 7: x triple from adjacent lanes where the slice allows
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
@@ -810,6 +811,16 @@ int choose_kernel(const hpccg_hip_matrix* M)
     return kSpmvDirect;
 }
 
+// The pair kernel's LDS-DMA value ring (k_spmv_a2r): uniform width 27, and
+// the windows plus the ring within the CU's LDS.
+int a2_ring_effective(const hpccg_hip_matrix* M)
+{
+    if (M->kernel != kSpmvPairs || M->a2_ring <= 0 || M->a_width != kA2RingWidth) return 0;
+    if (a2_lds_bytes(M->alds2_doubles, M->a2_ring) > (size_t)(159 * 1024)) return 0;
+    static const int prepared = a2_ring_prepare();
+    return prepared == 0 ? M->a2_ring : 0;
+}
+
 // p = r + beta p formed inside the SpMV: the pair kernel (ghost rows from the
 // halo) on any rank count; the direct kernel on one rank (it reads r and
 // p_{k-1} at ghost columns, which the halo does not carry); never the SELL-512
@@ -964,6 +975,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.awin2 = M->d_awin2;
     a.awn2 = M->d_awn2;
     a.alds2_doubles = std::max(1, M->alds2_doubles);
+    a.a2_ring = a2_ring_effective(M);
     if (std::getenv("HPCCG_DEBUG_ADDR"))
         std::fprintf(stderr, "hpccg_hip addr: aval %p p %p pstride_B %lld r %p Ap %p x %p b %p\n", (void*)a.aval,
                      (void*)a.p, a.pstride * 8, (void*)a.r, (void*)a.Ap, (void*)a.x, (void*)a.b);
@@ -2271,6 +2283,10 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->tri = value ? 1 : 0;
     } else if (!std::strcmp(key, "stage16")) {
         M->stage16 = value ? 1 : 0;
+    } else if (!std::strcmp(key, "a2_ring")) {
+        if (value < -1 || value > 4)
+            return set_err(HPCCG_HIP_EINVAL, "a2_ring must be -1 (auto: 3), 0 (register loads) or 1..4");
+        M->a2_ring = value < 0 ? kA2RingDefault : (int)value;
     } else if (!std::strcmp(key, "a_pre")) {
         if (value != -1 && value != 0 && value != 3 && value != 4 && value != 7)
             return set_err(HPCCG_HIP_EINVAL, "a_pre must be -1 (auto), 0, 3 (width 7), 4 (width 27) or 7 (width 7)");
@@ -2311,6 +2327,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
     else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;
     else if (!std::strcmp(key, "stage16")) *value = M->stage16;
+    else if (!std::strcmp(key, "a2_ring")) *value = a2_ring_effective(M);
     else if (!std::strcmp(key, "tri")) *value = M->tri;
     else if (!std::strcmp(key, "overlap")) {
         int lo, hi;

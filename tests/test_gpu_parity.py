@@ -112,6 +112,13 @@ def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
         M.set_option("stage16", st16)
         M.set_option("lds_ep", ep)
         out[("pairs", fuse, st16, ep)] = solve_bits(hp, M, prob.b, 120)
+    # the pair kernel's value stream: register loads (0) or the LDS-DMA ring
+    # (width 27 only; inert at width 7)
+    for fuse, ring in itertools.product((0, -1), (-1, 0, 1, 2, 3, 4)):
+        M.set_option("fuse_p", fuse)
+        M.set_option("a2_ring", ring)
+        assert M.get_option("a2_ring") == (0 if s7 else (3 if ring < 0 else ring))
+        out[("ring", fuse, ring)] = solve_bits(hp, M, prob.b, 120)
     bad = [k for k, o in out.items() if o != out[(SELL, 0)]]
     assert not bad, bad
 

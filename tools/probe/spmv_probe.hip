@@ -160,6 +160,135 @@ __global__ __launch_bounds__(512) void k_la2(Args a)
                                       wsum[4 * threadIdx.x + 2] + wsum[4 * threadIdx.x + 3];
 }
 
+
+// ---- pair kernel with the value stream through wave-private LDS-DMA rings --
+// Each wave owns 128 rows of one slice; slots stream HBM -> LDS ring (kR 1-KB
+// entries, global_load_lds_dwordx4 nt, lane-linear) and are read back by the
+// same lane; the windows are staged as in k_la2 (register loads + ds_write).
+// kOrder 0: ring DMAs first, then the staging loads (which then wait for the
+// ring); 1: staging loads first, ring DMAs behind them (counted vmcnt).
+__device__ __forceinline__ void vm_wait(int n)
+{
+    switch (n) {
+#define W(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+        W(0) W(1) W(2) W(3) W(4) W(5) W(6) W(7) W(8) W(9) W(10) W(11) W(12) W(13) W(14) W(15)
+        W(16) W(17) W(18) W(19) W(20) W(21) W(22) W(23) W(24) W(25) W(26)
+#undef W
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int kR, int kOrder, bool kPipe = false>
+__global__ __launch_bounds__(512) void k_la2d(Args a)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ double wsum[8];
+    const int P = xcd_map(gridDim.x);
+    if (P >= a.npairs) return;
+    const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+    const int half = threadIdx.x / 256;
+    const int s = 2 * P + half;
+    const bool have = s < a.nslices;
+    const int lrow = (threadIdx.x % 256) * 2;
+    const double* vp = a.val + (size_t)(have ? s : 0) * kW * kS + lrow;
+    const int len = a.win_len, tot = kNW * len;
+    double* xs = lds;
+    double* ring = lds + tot + wave * kR * 128;
+    const int prow0 = 2 * P * kS;
+    const double beta = a.beta;
+    constexpr int kU = 5;  // staging d2v per thread (3 x 1428 doubles / 1024 per round)
+    d2v sr[kU], sp[kU];
+    auto stage_loads = [&]() {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int e = 2 * threadIdx.x + 1024 * u;
+            if (e < tot) {
+                const int w = e >= len ? (e >= 2 * len ? 2 : 1) : 0;
+                const int lo = w == 0 ? a.win_lo[0] : (w == 1 ? a.win_lo[1] : a.win_lo[2]);
+                const int l = prow0 + lo + (e - w * len);
+                sr[u] = ld2(a.r + l);
+                sp[u] = ld2(a.pold + l);
+            }
+        }
+    };
+    auto ring_dma = [&]() {
+#pragma unroll
+        for (int j = 0; j < kR; j++)
+            __builtin_amdgcn_global_load_lds((const void*)(vp + (size_t)j * kS), (lds_void*)(ring + j * 128), 16, 0, 2);
+    };
+    if (kOrder == 0) {
+        ring_dma();
+        stage_loads();
+        vm_wait(0);
+    } else {
+        stage_loads();
+        ring_dma();
+        vm_wait(kR);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+        const int e = 2 * threadIdx.x + 1024 * u;
+        if (e < tot) *(d2v*)(xs + e) = sr[u] + beta * sp[u];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    double d = 0.0;
+    const int prow = half * kS + lrow;
+    double s0 = 0.0, s1 = 0.0;
+    if constexpr (!kPipe) {
+#pragma unroll
+        for (int j = 0; j < kW; j++) {
+            vm_wait((j + kR < kW ? j + kR : kW) - j - 1);
+            const d2v v = *(const d2v*)(ring + (j % kR) * 128 + lane * 2);
+            const int c = prow + a.lds[j];
+            s0 = s0 + v.x * xs[c];
+            s1 = s1 + v.y * xs[c + 1];
+            asm volatile("" : "+v"(s0), "+v"(s1));
+            if (j + kR < kW) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_global_load_lds((const void*)(vp + (size_t)(j + kR) * kS), (lds_void*)(ring + (j % kR) * 128), 16, 0, 2);
+            }
+        }
+    } else {
+        // x of the slot read ahead (window data is ready after the barrier);
+        // the ring entry read as soon as it has landed, DMA re-issued right after
+        double xa = xs[prow + a.lds[0]], xb = xs[prow + a.lds[0] + 1];
+#pragma unroll
+        for (int j = 0; j < kW; j++) {
+            vm_wait((j + kR < kW ? j + kR : kW) - j - 1);
+            const d2v v = *(const d2v*)(ring + (j % kR) * 128 + lane * 2);
+            double xna = 0.0, xnb = 0.0;
+            if (j + 1 < kW) {
+                const int cn = prow + a.lds[j + 1];
+                xna = xs[cn];
+                xnb = xs[cn + 1];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xa), "+v"(xb) :: "memory");
+            if (j + kR < kW)
+                __builtin_amdgcn_global_load_lds((const void*)(vp + (size_t)(j + kR) * kS), (lds_void*)(ring + (j % kR) * 128), 16, 0, 2);
+            s0 = s0 + v.x * xa;
+            s1 = s1 + v.y * xb;
+            asm volatile("" : "+v"(s0), "+v"(s1));
+            xa = xna;
+            xb = xnb;
+        }
+    }
+    if (have) {
+        const int row = s * kS + lrow;
+        *(d2v*)(a.Ap + row) = d2v{s0, s1};
+        const d2v pv = ld2(a.r + row) + beta * ld2(a.pold + row);
+        *(d2v*)(a.p + row) = pv;
+        d = pv.x * s0 + pv.y * s1;
+    }
+    const double wv = wsum64(d);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x / 64] = wv;
+    __syncthreads();
+    if (threadIdx.x < 2 && 2 * P + (int)threadIdx.x < a.nslices)
+        a.part[2 * P + threadIdx.x] = wsum[4 * threadIdx.x] + wsum[4 * threadIdx.x + 1] +
+                                      wsum[4 * threadIdx.x + 2] + wsum[4 * threadIdx.x + 3];
+}
+
 // ---- persistent, pipelined: each block pulls pairs from its group's counter
 // (group = blockIdx % 8, i.e. one XCD under round-robin placement, for speed
 // only); while pair t streams from LDS buffer cur, the staging loads of the
@@ -635,14 +764,15 @@ int main(int argc, char** argv)
     run("stream values only", [&] { k_stream<false><<<gpair, 512>>>(a); }, false);
     run("stream compulsory", [&] { k_stream<true><<<gpair, 512>>>(a); }, false);
     run("la2 pre3 (replica)", [&] { k_la2<3, false><<<gpair, 512, lds1>>>(a); }, true);
-    run("la2x scal0 done0 tab0", [&] { k_la2x<0, 0, false><<<gpair, 512, lds1>>>(a); }, true);
-    run("la2x scal1 done0 tab0", [&] { k_la2x<1, 0, false><<<gpair, 512, lds1>>>(a); }, true);
-    run("la2x scal2 done0 tab0", [&] { k_la2x<2, 0, false><<<gpair, 512, lds1>>>(a); }, true);
-    run("la2x scal0 done1 tab0", [&] { k_la2x<0, 1, false><<<gpair, 512, lds1>>>(a); }, true);
-    run("la2x scal0 done0 tab1", [&] { k_la2x<0, 0, true><<<gpair, 512, lds1>>>(a); }, true);
-    run("la2x scal1 done1 tab1", [&] { k_la2x<1, 1, true><<<gpair, 512, lds1>>>(a); }, true);
-    run("la2x scal2 done1 tab1", [&] { k_la2x<2, 1, true><<<gpair, 512, lds1>>>(a); }, true);
-    run("la2x scal2 done0 tab1", [&] { k_la2x<2, 0, true><<<gpair, 512, lds1>>>(a); }, true);
+    auto ldsd = [&](int R) { return lds1 + (size_t)8 * R * 1024; };
+    run("la2d R1 o1", [&] { k_la2d<1, 1><<<gpair, 512, ldsd(1)>>>(a); }, true);
+    run("la2d R2 o1", [&] { k_la2d<2, 1><<<gpair, 512, ldsd(2)>>>(a); }, true);
+    run("la2d R3 o1", [&] { k_la2d<3, 1><<<gpair, 512, ldsd(3)>>>(a); }, true);
+    run("la2d R4 o1", [&] { k_la2d<4, 1><<<gpair, 512, ldsd(4)>>>(a); }, true);
+    run("la2d R2 o0", [&] { k_la2d<2, 0><<<gpair, 512, ldsd(2)>>>(a); }, true);
+    run("la2d R1 o1 pipe", [&] { k_la2d<1, 1, true><<<gpair, 512, ldsd(1)>>>(a); }, true);
+    run("la2d R2 o1 pipe", [&] { k_la2d<2, 1, true><<<gpair, 512, ldsd(2)>>>(a); }, true);
+    run("la2d R3 o1 pipe", [&] { k_la2d<3, 1, true><<<gpair, 512, ldsd(3)>>>(a); }, true);
     // CG-shaped: an update pass (r = r - alpha Ap) between SpMVs, SpMV timed alone
     auto cgrun = [&](const char* name, auto launch) {
         std::vector<hipEvent_t> ev(2 * reps);
@@ -672,9 +802,8 @@ int main(int argc, char** argv)
     };
     cgrun("stream compulsory", [&] { k_stream<true><<<gpair, 512>>>(a); });
     cgrun("la2 pre3 (replica)", [&] { k_la2<3, false><<<gpair, 512, lds1>>>(a); });
-    cgrun("la2x scal1 done1 tab1", [&] { k_la2x<1, 1, true><<<gpair, 512, lds1>>>(a); });
-    cgrun("la2x scal2 done1 tab1", [&] { k_la2x<2, 1, true><<<gpair, 512, lds1>>>(a); });
-    cgrun("la2x scal2 done0 tab1", [&] { k_la2x<2, 0, true><<<gpair, 512, lds1>>>(a); });
-    cgrun("la2x scal0 done0 tab0", [&] { k_la2x<0, 0, false><<<gpair, 512, lds1>>>(a); });
+    cgrun("la2d R2 o1", [&] { k_la2d<2, 1><<<gpair, 512, ldsd(2)>>>(a); });
+    cgrun("la2d R3 o1", [&] { k_la2d<3, 1><<<gpair, 512, ldsd(3)>>>(a); });
+    cgrun("la2d R2 o1 pipe", [&] { k_la2d<2, 1, true><<<gpair, 512, ldsd(2)>>>(a); });
     return 0;
 }
