@@ -92,6 +92,7 @@ struct CgArgs {
     int stage16;                  // pair kernel: stage row pairs with 16-B loads / LDS stores
     const unsigned char* atri;    // direct kernel: per slice, 1 = offsets in the width's triple plan (null: off)
     int alds2_doubles;            // dynamic LDS per two-slice block
+    int slots;                    // folded dots complete through self-validating slots (launch covers all units)
     int a2_ring;                  // pair kernel: value slots in flight per wave through its LDS-DMA ring (0: register loads)
 };
 
@@ -105,6 +106,8 @@ inline __host__ __device__ bool fold_of(const CgArgs& a, int which)
 // windows cut the union of a pair's offsets where neighbours are more than a
 // slice apart, at most kAWin windows and kALdsMax2 staged doubles per pair.
 constexpr int kAMax = 32;
+// An empty dot-partial / group-sum slot: a NaN payload no arithmetic produces.
+constexpr unsigned long long kSlotEmpty = 0x7FF4DEADBEEF0001ull;
 constexpr int kAWin = 8;
 constexpr int kALdsMax2 = 7936;  // 62 KB: within the 64 KB default dynamic LDS limit
 // Zeroed guard zone on each side of every p buffer and of r: a hole of row i

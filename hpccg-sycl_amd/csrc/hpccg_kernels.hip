@@ -239,15 +239,27 @@ __device__ __forceinline__ double* cur_p(const CgArgs& a, int k)
 // which = kPAP: p.Ap (HPCCG.cpp:381); kRR: r.r (HPCCG.cpp:353, 367), which
 // closes iteration k and advances kst[0].
 //
-// Folded (fold_of): completed inside the producing kernel. Every block
-// publishes its partial with a write-through (sc1) store, waits for it
-// (s_waitcnt vmcnt(0)) and takes a relaxed agent-scope ticket on its group;
-// the group's last arriver (told by the ticket value) acquires, reads the
-// group's partials with sc1 loads, publishes the group sum the same way and
-// takes a ticket on the top counter; the last group reducer forms the total
-// (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 payload, drained, then
-// the counter; the reader acquires). Otherwise k_finalize computes the same
-// two levels in a separate launch.
+// Folded (fold_of): completed inside the producing kernel, two ways.
+//  * Slots (a.slots, every launch that covers all units): every partial and
+//    group-sum slot holds kSlotEmpty (a NaN payload no arithmetic produces)
+//    until its value is stored. Producers store their partial with an
+//    agent-scope (sc1) store and leave -- no drain, no atomic. The group's
+//    member with the largest block index, i.e. the one dispatched last
+//    (group_last_unit), waits for the group's slots to fill, sums them, resets
+//    them to empty and stores the group sum; the group whose last member has
+//    the largest block index of all (top_group) then waits for every group
+//    sum and forms the total. A waiter only waits for blocks dispatched before
+//    it (dispatch is in block order on every XCD), so the wait always ends.
+//  * Tickets (launches over a unit subset: the eager halo overlap): every
+//    block publishes its partial (sc1), drains (s_waitcnt vmcnt(0)) and takes
+//    a relaxed agent-scope ticket on its group; the group's last arriver sums
+//    the group, tickets the top counter, whose last arriver forms the total
+//    (MI355X_MICROARCH.md, inter-workgroup visibility). It resets the slots it
+//    read as well, so the two ways mix freely.
+// Otherwise k_finalize computes the same two levels in a separate launch (and
+// resets the slots). Same shape every way: bitwise the same total.
+// 100^3 same-process A/B: the ticket's round trip made every block of the
+// short update kernel wait (update 10.3 -> 23.6 us with r.r folded by tickets).
 // ---------------------------------------------------------------------------
 constexpr int kGroup = 64;
 constexpr int kTopThreads = 256;
@@ -262,6 +274,54 @@ __device__ __forceinline__ double ld_sc1(const double* p)
 }
 
 __device__ __forceinline__ int ngroups_of(const CgArgs& a) { return (a.nslices + kGroup - 1) / kGroup; }
+
+__device__ __forceinline__ bool slot_full(double v) { return __double_as_longlong(v) != (long long)kSlotEmpty; }
+__device__ __forceinline__ double slot_empty() { return __longlong_as_double((long long)kSlotEmpty); }
+
+// How a launch deals its units (slices, or slice pairs: spu slices per unit)
+// to blocks: unit u = the x-th XCD eighth's i-th unit, run by block
+// kNumXcd * i + x (xcd_slice), or kNumXcd * (per - 1 - i) + x (xcd_slice_rev).
+struct UnitMap {
+    int units, per, spu;
+    bool rev;
+};
+__device__ __forceinline__ int unit_block(const UnitMap& m, int u)
+{
+    const int x = u / m.per, i = u % m.per;
+    return kNumXcd * (m.rev ? m.per - 1 - i : i) + x;
+}
+// Within one eighth the block index is monotone in u, so the largest is at an
+// end of the group or of an eighth inside it.
+__device__ __forceinline__ int group_last_unit(const UnitMap& m, int g)
+{
+    const int upg = kGroup / m.spu;
+    const int u0 = g * upg, u1 = min(m.units, u0 + upg) - 1;
+    int best = u0, bb = unit_block(m, u0);
+    auto cand = [&](int u) {
+        if (u >= u0 && u <= u1) {
+            const int b = unit_block(m, u);
+            if (b > bb) bb = b, best = u;
+        }
+    };
+    cand(u1);
+    for (int c = u0 / m.per + 1; c * m.per <= u1; c++) {
+        cand(c * m.per - 1);
+        cand(c * m.per);
+    }
+    return best;
+}
+__device__ __forceinline__ int top_group(const UnitMap& m)
+{
+    int best = 0, bb = -1;
+    for (int c = 0; c < kNumXcd && c * m.per < m.units; c++) {
+        const int us[2] = {c * m.per, min(m.units - 1, c * m.per + m.per - 1)};
+        for (int u : us) {
+            const int b = unit_block(m, u);
+            if (b > bb) bb = b, best = u;
+        }
+    }
+    return best * m.spu / kGroup;
+}
 
 // The same fixed top-level shape computed by one wave (virtual waves in order);
 // valid in lane 0. ld(i) reads group sum i. All loads are issued before the sums.
@@ -305,11 +365,9 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
 
 // Partials of slices s0 .. s0 + cnt - 1 (one group: s0 % kGroup + cnt <=
 // kGroup), the partial of slice s0 + j in lane j of wave 0; called by wave 0
-// only. Folded: the lanes publish their partials together, lane 0 takes one
-// ticket of cnt arrivals on the group; the group's last arriver then sums the
-// group and takes a ticket on the top counter, whose last arriver forms the
-// total. Not folded: plain stores for k_finalize.
-__device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, int s0, int cnt, double bs, int which, int k)
+// only; u: this block's unit under m. Not folded: plain stores for k_finalize.
+__device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMap& m, int u, int s0, int cnt, double bs,
+                                                   int which, int k)
 {
     const int lane = threadIdx.x;
     if (!fold_of(a, which)) {
@@ -318,8 +376,35 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, int s0, int 
     }
     const int ng = ngroups_of(a);
     double* gp = a.partial + a.nslices + which * ng;  // group sums of this dot
-    unsigned* gt = a.tickets + which * (ng + 1);      // group tickets, then the top one
     const int g = s0 / kGroup;
+    const int i = g * kGroup + lane;  // the group's slot of this lane
+    if (a.slots) {
+        if (lane < cnt) st_sc1(a.partial + s0 + lane, bs);
+        if (u != group_last_unit(m, g)) return;
+        double v;
+        for (;;) {  // the group's other members were dispatched before this block
+            v = i < a.nslices ? ld_sc1(a.partial + i) : 0.0;
+            if (__all(i >= a.nslices || slot_full(v))) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (i < a.nslices) st_sc1(a.partial + i, slot_empty());
+        v = wave_sum(v);
+        if (lane == 0) st_sc1(gp + g, v);
+        if (g != top_group(m)) return;
+        for (int j0 = 0; j0 < ng; j0 += kWave) {  // every other group's reducer came before
+            for (;;) {
+                const int j = j0 + lane;
+                const double w = j < ng ? ld_sc1(gp + j) : 0.0;
+                if (__all(j >= ng || slot_full(w))) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
+        for (int j = lane; j < ng; j += kWave) st_sc1(gp + j, slot_empty());
+        if (lane == 0) finish_dot(a, tot, which, k);
+        return;
+    }
+    unsigned* gt = a.tickets + which * (ng + 1);  // group tickets, then the top one
     int role = 0;
     if (lane < cnt) st_sc1(a.partial + s0 + lane, bs);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -335,8 +420,8 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, int s0, int 
     role = __shfl(role, 0, kWave);
     if (role == 0) return;
     // group reducer (this wave): sc1 loads of the group's partials
-    const int i = g * kGroup + lane;
     const double v = wave_sum(i < a.nslices ? ld_sc1(a.partial + i) : 0.0);
+    if (i < a.nslices) st_sc1(a.partial + i, slot_empty());
     if (lane == 0) {
         st_sc1(gp + g, v);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -351,6 +436,7 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, int s0, int 
     role = __shfl(role, 0, kWave);
     if (role != 2) return;
     const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
+    for (int j = lane; j < ng; j += kWave) st_sc1(gp + j, slot_empty());
     if (lane == 0) {
         finish_dot(a, tot, which, k);
         __hip_atomic_store(gt + ng, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
@@ -359,10 +445,22 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, int s0, int 
 
 // One slice's partial, valid in thread 0 (block_sum<256> shape). Only wave 0
 // takes part in the hand-off: the other waves of the block return right away.
-__device__ __forceinline__ void complete_dot(const CgArgs& a, int s, double bs, int which, int k)
+__device__ __forceinline__ void complete_dot(const CgArgs& a, const UnitMap& m, int u, int s, double bs, int which,
+                                             int k)
 {
     if (threadIdx.x >= kWave) return;
-    complete_dot_lanes(a, s, 1, bs, which, k);
+    complete_dot_lanes(a, m, u, s, 1, bs, which, k);
+}
+
+// The unit maps of the SpMV launches (all units, xcd_slice over sgrid; the
+// slot completion runs only on such launches) and of the update.
+__device__ __forceinline__ UnitMap spmv_units(const CgArgs& a, int spu)
+{
+    return UnitMap{a.sn0 + a.sn1, a.sgrid / kNumXcd, spu, false};
+}
+__device__ __forceinline__ UnitMap update_units(const CgArgs& a)
+{
+    return UnitMap{a.nslices, a.grid / kNumXcd, 1, a.rev != 0};
 }
 
 // The SpMV of iteration k publishes {k, run} (kst[4..5]) for the kernels that
@@ -584,7 +682,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(CgArgs a, bool prologue)
     const double d = spmv_rows_out<false>(a, st, prologue, row, sum);
     if (prologue) return;
     const double bs = block_sum<kBlock>(d);
-    complete_dot(a, s, bs, kPAP, st.k);
+    complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
 }
 
 // ---------------------------------------------------------------------------
@@ -686,7 +784,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
             const double d = spmv_rows_out<kFuse>(a, st, prologue, row, sum);
             if (prologue) return;
             const double bs = block_sum<kBlock>(d);
-            complete_dot(a, s, bs, kPAP, st.k);
+            complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
             return;
         }
     }
@@ -716,7 +814,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
     const double d = spmv_rows_out<kFuse>(a, st, prologue, row, sum);
     if (prologue) return;
     const double bs = block_sum<kBlock>(d);
-    complete_dot(a, s, bs, kPAP, st.k);
+    complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
 }
 
 // ---------------------------------------------------------------------------
@@ -866,7 +964,7 @@ __device__ __forceinline__ void pair_epilogue(const CgArgs& a, const IterState& 
 #pragma unroll
         for (int i = 0; i < kWh; i++) bs += wsum[lane * kWh + i];
     }
-    complete_dot_lanes(a, 2 * P, min(2, a.nslices - 2 * P), bs, kPAP, st.k);
+    complete_dot_lanes(a, spmv_units(a, 2), P, 2 * P, min(2, a.nslices - 2 * P), bs, kPAP, st.k);
 }
 
 // ---------------------------------------------------------------------------
@@ -1107,6 +1205,11 @@ __device__ __forceinline__ void finalize_groups(const CgArgs& a, int ng, bool in
             v[b] = (g0 + b * kWaves < ng && i < a.nslices) ? a.partial[i] : 0.0;
         }
 #pragma unroll
+        for (int b = 0; b < kB; b++) {  // the slots are empty again for the next producer
+            const int i = (g0 + b * kWaves) * kGroup + lane;
+            if (g0 + b * kWaves < ng && i < a.nslices) a.partial[i] = slot_empty();
+        }
+#pragma unroll
         for (int b = 0; b < kB; b++) {
             const double w = wave_sum(v[b]);
             const int g = g0 + b * kWaves;
@@ -1147,6 +1250,8 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
     if (threadIdx.x < kWave) {
         const double tot = in_lds ? top_sum_wave([&](int i) { return gs[i]; }, ng, lane)
                                   : top_sum_wave([gp](int i) { return gp[i]; }, ng, lane);
+        if (!in_lds)
+            for (int j = lane; j < ng; j += kWave) gp[j] = slot_empty();
         if (lane == 0) finish_dot(a, tot, which, k, false);
     }
 }
@@ -1242,7 +1347,7 @@ __global__ __launch_bounds__(kBlock) void k_update(CgArgs a)
     for (int i = 0; i < kRpt; i++)
         if (row + i < a.n) d += rn.v[i] * rn.v[i];
     const double bs = block_sum<kBlock>(d);
-    complete_dot(a, s, bs, kRR, k);
+    complete_dot(a, update_units(a), s, s, bs, kRR, k);
 }
 
 // Timestamp-only kernel around RCCL calls (multi-rank): one lane, one store.

@@ -160,22 +160,27 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     assert all(r == results[0] for r in results)
 
 
-def test_folded_dot_completion_stress(hp, gpu):
+@pytest.mark.parametrize("dims,reps", [((64, 64, 48), 12), ((96, 96, 100), 4)])
+def test_folded_dot_completion_stress(hp, gpu, dims, reps):
     """The in-kernel (fold) dot completion hands partials between workgroups on
-    different XCDs (sc1 publish + tickets). Any stale read would change a sum:
-    repeat many solves and compare every trace bitwise with the separate
-    k_finalize path (data handed over by a kernel boundary)."""
-    prob = hp.generate_matrix(64, 64, 48)  # 384 slices -> 6 groups, partial last group
+    different XCDs (self-validating slots, or sc1 publish + tickets for unit
+    subsets). Any stale read would change a sum: repeat many solves and compare
+    every trace bitwise with the separate k_finalize path (data handed over by
+    a kernel boundary). 96x96x100: 1800 slices, 29 groups that straddle the
+    XCD eighths of the grid (the waiting member is then not the group's last
+    slice)."""
+    prob = hp.generate_matrix(*dims)
     M = hp.Matrix.from_hpc(prob)
     for kernel in (DIRECT, PAIRS):
         M.set_option("spmv_kernel", kernel)
         M.set_option("fold", 0)
         ref = solve_bits(hp, M, prob.b, 150)
-        M.set_option("fold", 1)
-        for graph in (1, 0):
-            M.set_option("use_graph", graph)
-            for _ in range(12):
-                assert solve_bits(hp, M, prob.b, 150) == ref
+        for fold in (1, 2, 3):
+            M.set_option("fold", fold)
+            for graph in (1, 0):
+                M.set_option("use_graph", graph)
+                for _ in range(reps):
+                    assert solve_bits(hp, M, prob.b, 150) == ref, (kernel, fold, graph)
 
 
 def test_waxpby_bitwise_vs_reference(hp, gpu, golden):
