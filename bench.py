@@ -56,11 +56,13 @@ os.environ.setdefault("OMP_PLACES", "cores")
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 COPY_CEILING_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy, measured
-KERNEL_NAMES = {0: "k_spmv_sell", 1: "k_spmv_a", 2: "k_spmv_a2"}
+KERNEL_NAMES = {0: "k_spmv_sell", 1: "k_spmv_a", 2: "k_spmv_a2", 3: "k_spmv_a2r"}
 FORMAT_NAMES = {0: "SELL-512 (8 B value + 4 B int32 column per slot)",
                 1: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets",
                 2: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice "
-                   "pairs"}
+                   "pairs",
+                3: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice "
+                   "pairs, values streamed HBM -> LDS by per-wave LDS-DMA rings"}
 
 
 def load_pkg():
@@ -230,6 +232,7 @@ def main():
     x = torch.zeros(nrow, dtype=torch.float64, device=f"cuda:{local_rank}")
     torch.cuda.synchronize()
     kernel = M.get_option("spmv_kernel")
+    kfmt = 3 if (kernel == 2 and M.get_option("a2_ring") > 0) else kernel  # 3: the pair kernel's LDS-DMA ring form
     log(f"[rank {rank}] setup {time.time() - t0:.2f}s nnz={info['nnz']} slots={info['slots']} kernel={kernel} "
         f"device_bytes={M.get_option('device_bytes') / 1e9:.2f} GB")
 
@@ -310,7 +313,7 @@ def main():
     value = it_per_s * world
     ms_per_step = elapsed / args.steps * 1e3
     iter_bytes = 12.0 * info["nnz"] + 116.0 * nrow  # unfused reference sequence, SURVEY 8(d)
-    traffic, traffic_src = pmc_traffic(f"spmv_{args.stencil}pt_{n}", kernel, fused)
+    traffic, traffic_src = pmc_traffic(f"spmv_{args.stencil}pt_{n}", kfmt, fused)
 
     if rank == 0:
         out = {
@@ -332,11 +335,11 @@ def main():
                 "nx": n, "ny": n, "nz_per_gpu": n, "stencil": args.stencil,
                 "max_iter": args.max_iter, "parallelism": f"z-slab x{world} (RCCL)",
                 "nnz_per_gpu": info["nnz"], "matrix_slots_per_gpu": slots,
-                "spmv_kernel": kernel, "matrix_format": FORMAT_NAMES[kernel],
+                "spmv_kernel": kernel, "matrix_format": FORMAT_NAMES[kfmt],
                 "device_bytes_per_gpu": M.get_option("device_bytes"),
                 "graph_replay": bool(graph_used),
                 "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update",
-                                                         "overlap", "graph_chunk", "nt")},
+                                                         "overlap", "graph_chunk", "nt", "a2_ring", "nt_store")},
             },
             "cg_iterations_per_s_global": round(it_per_s, 3),
             "spmv_effective_gbs": round(achieved, 1),
@@ -351,7 +354,7 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
-                "kernel": "%s: %s + p.Ap%s" % (KERNEL_NAMES[kernel], FORMAT_NAMES[kernel],
+                "kernel": "%s: %s + p.Ap%s" % (KERNEL_NAMES[kfmt], FORMAT_NAMES[kfmt],
                                               " + p = r + beta p" if fused else ""),
                 "bytes_per_launch": format_bytes,
                 "bytes_formula": ("%g B per stored slot x %d slots + %d B per row (r, p_{k-1} read; p_k, Ap "

@@ -92,6 +92,7 @@ struct CgArgs {
     int stage16;                  // pair kernel: stage row pairs with 16-B loads / LDS stores
     const unsigned char* atri;    // direct kernel: per slice, 1 = offsets in the width's triple plan (null: off)
     int alds2_doubles;            // dynamic LDS per two-slice block
+    int nt_store;                 // CG vector stores non-temporal
     int slots;                    // folded dots complete through self-validating slots (launch covers all units)
     int a2_ring;                  // pair kernel: value slots in flight per wave through its LDS-DMA ring (0: register loads)
 };
@@ -129,9 +130,8 @@ void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s);  //
 void launch_cg_pack(const CgArgs& a, const int* idx, int cnt, double* buf, bool prologue, hipStream_t s);
 bool spmv_kernel_ok(int kernel);
 void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s);
-// Pair kernel with the LDS-DMA value ring (a2_ring > 0: uniform width 27 only):
+// Pair kernel with the LDS-DMA value ring (a2_ring > 0: uniform width 27 or 7):
 // dynamic LDS bytes, and the one-time attribute that lets it exceed 64 KB.
-constexpr int kA2RingWidth = 27;
 constexpr int kA2RingDefault = 3;
 size_t a2_lds_bytes(int lds_doubles, int ring);
 int a2_ring_prepare();

@@ -222,6 +222,21 @@ __device__ __forceinline__ void st_rows(double* __restrict__ base, int row, int 
     }
 }
 
+// The CG vectors (Ap, p_k, r, x) as streams: non-temporal stores when
+// a.nt_store, so they do not sit dirty in L2 when the kernel ends (every
+// kernel boundary writes back what is dirty, ~B / 6 TB/s).
+__device__ __forceinline__ void st_vec(const CgArgs& a, double* __restrict__ base, int row, const Rows& o)
+{
+    if (!a.nt_store) {
+        st_rows(base, row, a.n, o);
+    } else if (row + kRpt <= a.n) {
+        __builtin_nontemporal_store(d2v{o.v[0], o.v[1]}, reinterpret_cast<d2v*>(base + row));
+    } else {
+        for (int i = 0; i < kRpt; i++)
+            if (row + i < a.n) base[row + i] = o.v[i];
+    }
+}
+
 // p of iteration k lives in ring buffer k % nring: the update of p reads
 // p_{k-1} from the previous buffer, and with x deferral the last nring p's
 // stay available for the batched x update.
@@ -622,20 +637,20 @@ template <bool kFuse>
 __device__ __forceinline__ double spmv_rows_out(const CgArgs& a, const IterState& st, bool prologue, int row,
                                                 const double (&sum)[kRpt], const Rows* pk = nullptr)
 {
-    st_rows(a.Ap, row, a.n, Rows{{sum[0], sum[1]}});
+    st_vec(a, a.Ap, row, Rows{{sum[0], sum[1]}});
     if (prologue) return 0.0;  // HPCCG.cpp:351: the prologue SpMV has no p.Ap
     double* __restrict__ p = cur_p(a, st.k);
     Rows pv;
     if (pk) {
         pv = *pk;
-        if constexpr (kFuse) st_rows(p, row, a.n, pv);
+        if constexpr (kFuse) st_vec(a, p, row, pv);
     } else if constexpr (kFuse) {
         const double* __restrict__ pold = (st.k == 1) ? a.r : cur_p(a, st.k - 1);
         const Rows rv = ld(a.r + row);
         const Rows yv = ld(pold + row);
 #pragma unroll
         for (int i = 0; i < kRpt; i++) pv.v[i] = rv.v[i] + st.beta * yv.v[i];
-        st_rows(p, row, a.n, pv);
+        st_vec(a, p, row, pv);
     } else {
         pv = ld(p + row);
     }
@@ -1333,15 +1348,15 @@ __global__ __launch_bounds__(kBlock) void k_update(CgArgs a)
             Rows xn;
 #pragma unroll
             for (int i = 0; i < kRpt; i++) xn.v[i] = xv.v[i] + alpha * pv.v[i];
-            st_rows(a.x, row, a.n, xn);
+            st_vec(a, a.x, row, xn);
         } else if (k % a.nring == 0) {
             // deferred x update (HPCCG.cpp:383 for iterations k-nring+1 .. k)
             Rows xn = ld(a.x + row);
             x_accumulate(a, row, k - a.nring + 1, k, k, alpha, xn);
-            st_rows(a.x, row, a.n, xn);
+            st_vec(a, a.x, row, xn);
         }
     }
-    st_rows(a.r, row, a.n, rn);
+    st_vec(a, a.r, row, rn);
     double d = 0.0;
 #pragma unroll
     for (int i = 0; i < kRpt; i++)
@@ -1632,12 +1647,13 @@ int a2_ring_prepare()
 {
     const int lim = 160 * 1024 - 1024;
     hipError_t e = hipSuccess;
-#define HPCCG_A2R_ATTR(R)                                                                                               \
+#define HPCCG_A2R_ATTR(W, R)                                                                                               \
     if (e == hipSuccess)                                                                                                \
-        e = hipFuncSetAttribute((const void*)k_spmv_a2r<true, 27, R>, hipFuncAttributeMaxDynamicSharedMemorySize, lim); \
+        e = hipFuncSetAttribute((const void*)k_spmv_a2r<true, W, R>, hipFuncAttributeMaxDynamicSharedMemorySize, lim); \
     if (e == hipSuccess)                                                                                                \
-        e = hipFuncSetAttribute((const void*)k_spmv_a2r<false, 27, R>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    HPCCG_A2R_ATTR(1) HPCCG_A2R_ATTR(2) HPCCG_A2R_ATTR(3) HPCCG_A2R_ATTR(4)
+        e = hipFuncSetAttribute((const void*)k_spmv_a2r<false, W, R>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    HPCCG_A2R_ATTR(27, 1) HPCCG_A2R_ATTR(27, 2) HPCCG_A2R_ATTR(27, 3) HPCCG_A2R_ATTR(27, 4)
+    HPCCG_A2R_ATTR(7, 1) HPCCG_A2R_ATTR(7, 2) HPCCG_A2R_ATTR(7, 3) HPCCG_A2R_ATTR(7, 4)
 #undef HPCCG_A2R_ATTR
     return e == hipSuccess ? 0 : -1;
 }
@@ -1665,18 +1681,27 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     case kSpmvPairs: {
         if (a.a2_ring > 0) {
             const size_t smem = a2_lds_bytes(a.alds2_doubles, a.a2_ring);
-#define HPCCG_A2R(R)                                                                                              \
+#define HPCCG_A2R(W, R)                                                                                           \
     do {                                                                                                          \
         if (fuse)                                                                                                 \
-            hipLaunchKernelGGL((k_spmv_a2r<true, 27, R>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue); \
+            hipLaunchKernelGGL((k_spmv_a2r<true, W, R>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue); \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_spmv_a2r<false, 27, R>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue); \
+            hipLaunchKernelGGL((k_spmv_a2r<false, W, R>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue); \
     } while (0)
-            switch (a.a2_ring) {
-            case 1: HPCCG_A2R(1); break;
-            case 2: HPCCG_A2R(2); break;
-            case 3: HPCCG_A2R(3); break;
-            default: HPCCG_A2R(4); break;
+            if (a.a_width == 7) {
+                switch (a.a2_ring) {
+                case 1: HPCCG_A2R(7, 1); break;
+                case 2: HPCCG_A2R(7, 2); break;
+                case 3: HPCCG_A2R(7, 3); break;
+                default: HPCCG_A2R(7, 4); break;
+                }
+            } else {
+                switch (a.a2_ring) {
+                case 1: HPCCG_A2R(27, 1); break;
+                case 2: HPCCG_A2R(27, 2); break;
+                case 3: HPCCG_A2R(27, 3); break;
+                default: HPCCG_A2R(27, 4); break;
+                }
             }
 #undef HPCCG_A2R
             break;

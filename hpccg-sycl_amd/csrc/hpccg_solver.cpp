@@ -219,7 +219,8 @@ struct hpccg_hip_matrix {
     int a_pre = -1;       // direct kernel prefetch depth (-1 auto: 4 at width 27, 7 at width 7)
     int lds_ep = 1;       // pair kernel: own p_k from the staged window
     int stage16 = 1;      // pair kernel: 16-B staging of row pairs
-    int a2_ring = kA2RingDefault;  // pair kernel: LDS-DMA value ring depth per wave (0: register loads; width 27 only)
+    int nt_store = -1;    // CG vector stores non-temporal (-1 auto: nt_store_effective)
+    int a2_ring = kA2RingDefault;  // pair kernel: LDS-DMA value ring depth per wave (0: register loads; uniform widths 27 and 7)
     int tri = 1;          // direct kernel, width 7: x triple from adjacent lanes where the slice allows
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
@@ -811,14 +812,25 @@ int choose_kernel(const hpccg_hip_matrix* M)
     return kSpmvDirect;
 }
 
-// The pair kernel's LDS-DMA value ring (k_spmv_a2r): uniform width 27, and
+// The pair kernel's LDS-DMA value ring (k_spmv_a2r): uniform width 27 or 7, and
 // the windows plus the ring within the CU's LDS.
 int a2_ring_effective(const hpccg_hip_matrix* M)
 {
-    if (M->kernel != kSpmvPairs || M->a2_ring <= 0 || M->a_width != kA2RingWidth) return 0;
+    if (M->kernel != kSpmvPairs || M->a2_ring <= 0 || (M->a_width != 27 && M->a_width != 7)) return 0;
     if (a2_lds_bytes(M->alds2_doubles, M->a2_ring) > (size_t)(159 * 1024)) return 0;
     static const int prepared = a2_ring_prepare();
     return prepared == 0 ? M->a2_ring : 0;
+}
+
+// Non-temporal stores of the CG vectors where the direct kernel streams an
+// image beyond the Infinity Cache: its x reads at the +-1-plane offsets live
+// on L2 reuse, which dirty Ap / p_k / r lines would crowd out. Same-process
+// A/B, 7-pt 256^3: 2888 vs 2712 CG it/s (SpMV 253 vs 274 us); 200^3 (pair
+// ring kernel) 2644 vs 2650 and 100^3 19190 vs 19175: left off there.
+bool nt_store_effective(const hpccg_hip_matrix* M)
+{
+    if (M->nt_store >= 0) return M->nt_store != 0;
+    return M->kernel == kSpmvDirect && image_big(M);
 }
 
 // p = r + beta p formed inside the SpMV: the pair kernel (ghost rows from the
@@ -985,6 +997,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.alds2_doubles = std::max(1, M->alds2_doubles);
     a.a2_ring = a2_ring_effective(M);
     a.slots = 1;
+    a.nt_store = nt_store_effective(M) ? 1 : 0;
     if (std::getenv("HPCCG_DEBUG_ADDR"))
         std::fprintf(stderr, "hpccg_hip addr: aval %p p %p pstride_B %lld r %p Ap %p x %p b %p\n", (void*)a.aval,
                      (void*)a.p, a.pstride * 8, (void*)a.r, (void*)a.Ap, (void*)a.x, (void*)a.b);
@@ -1069,7 +1082,9 @@ int ensure_events(hpccg_hip_matrix* M, int slots)
 {
     while ((int)M->ev.size() < 4 * slots) {
         hipEvent_t e;
-        HIP_TRY(hipEventCreate(&e));
+        // no system-scope release at the record: a timed kernel's interval
+        // would otherwise include writing back the caches it left dirty
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         M->ev.push_back(e);
     }
     return 0;
@@ -2295,6 +2310,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->tri = value ? 1 : 0;
     } else if (!std::strcmp(key, "stage16")) {
         M->stage16 = value ? 1 : 0;
+    } else if (!std::strcmp(key, "nt_store")) {
+        M->nt_store = value < 0 ? -1 : (value ? 1 : 0);
     } else if (!std::strcmp(key, "a2_ring")) {
         if (value < -1 || value > 4)
             return set_err(HPCCG_HIP_EINVAL, "a2_ring must be -1 (auto: 3), 0 (register loads) or 1..4");
@@ -2340,6 +2357,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;
     else if (!std::strcmp(key, "stage16")) *value = M->stage16;
     else if (!std::strcmp(key, "a2_ring")) *value = a2_ring_effective(M);
+    else if (!std::strcmp(key, "nt_store")) *value = nt_store_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "tri")) *value = M->tri;
     else if (!std::strcmp(key, "overlap")) {
         int lo, hi;

@@ -113,11 +113,11 @@ def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
         M.set_option("lds_ep", ep)
         out[("pairs", fuse, st16, ep)] = solve_bits(hp, M, prob.b, 120)
     # the pair kernel's value stream: register loads (0) or the LDS-DMA ring
-    # (width 27 only; inert at width 7)
+    # (uniform widths 27 and 7)
     for fuse, ring in itertools.product((0, -1), (-1, 0, 1, 2, 3, 4)):
         M.set_option("fuse_p", fuse)
         M.set_option("a2_ring", ring)
-        assert M.get_option("a2_ring") == (0 if s7 else (3 if ring < 0 else ring))
+        assert M.get_option("a2_ring") == (3 if ring < 0 else ring)
         out[("ring", fuse, ring)] = solve_bits(hp, M, prob.b, 120)
     bad = [k for k, o in out.items() if o != out[(SELL, 0)]]
     assert not bad, bad
@@ -139,6 +139,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
             M.set_option("use_graph", graph)
             M.set_option("x_defer", defer)
             M.set_option("rev_update", (fold + defer) % 2)
+            M.set_option("nt_store", (fold + graph) % 2)
             assert M.get_option("fold") == fold
             # 119 iterations: x updates left for k_xflush
             results.append(solve_bits(hp, M, prob.b, 120))
@@ -148,6 +149,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     # rings of 2 .. 64, 119 iterations leave 1 .. 55 updates for k_xflush
     M.set_option("x_defer", 1)
     M.set_option("fold", -1)
+    M.set_option("nt_store", -1)
     for ring, graph in ((2, 1), (5, 0), (16, 1), (32, 1), (64, 0), (8, 1), (-1, 1)):
         M.set_option("x_ring", ring)
         M.set_option("use_graph", graph)

@@ -27,6 +27,8 @@ FORMATS = {
     "k_spmv_sell": "SELL-512 (8 B value + int32 column per slot)",
     "k_spmv_a": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets",
     "k_spmv_a2": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice pairs",
+    "k_spmv_a2r": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice pairs, "
+                  "values streamed HBM -> LDS by per-wave LDS-DMA rings",
 }
 
 
@@ -85,15 +87,18 @@ def main():
     f_stream, _ = pick(fetch, "k_stream_a", "FETCH_SIZE")
     w_stream, _ = pick(write, "k_stream_a", "WRITE_SIZE")
     fetch_factor = stream_read / (f_stream * 1024.0)
-    SPMV = ("k_spmv_sell<", "k_spmv_a<", "k_spmv_a2<")
+    SPMV = ("k_spmv_sell<", "k_spmv_a<", "k_spmv_a2<", "k_spmv_a2r<")
     f_spmv, kname = pick(fetch, SPMV, "FETCH_SIZE")
     w_spmv, _ = pick(write, SPMV, "WRITE_SIZE")
     spmv_read = f_spmv * 1024.0 * fetch_factor
     spmv_write = w_spmv * 1024.0
     targs = re.search(r"k_spmv\w*<([^>]*)>", kname).group(1).split(",")
-    # k_spmv_a<kW, kNT, kFuse, kPre>, k_spmv_a2<kNT, kFuse, kPre>, k_spmv_sell<kNT> (never fused)
+    # k_spmv_a<kW, kNT, kFuse, kPre>, k_spmv_a2<kNT, kFuse, kPre>, k_spmv_a2r<kFuse, kW, kR>,
+    # k_spmv_sell<kNT> (never fused)
     if "k_spmv_a<" in kname:
         fuse_p = targs[2].strip() == "true"
+    elif "k_spmv_a2r<" in kname:
+        fuse_p = targs[0].strip() == "true"
     elif "k_spmv_a2<" in kname:
         fuse_p = targs[1].strip() == "true"
     else:
