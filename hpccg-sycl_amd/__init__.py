@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
         "hpccg_hip_kernel_times": (ip, [vp, PD]),
         "hpccg_hip_kernel_times_iter": (ip, [vp, PD, ip]),
         "hpccg_hip_diag_spmv": (ip, [vp, ip, ip, PD]),
+        "hpccg_hip_diag_slot_plan": (ip, [ip, ip, ip, ip, PI, ip, PI]),
         "hpccg_hip_sparsemv": (ip, [vp, vp, vp]),
         "hpccg_hip_ddot": (ip, [ip, vp, vp, PD]),
         "hpccg_hip_waxpby": (ip, [ip, dp, vp, dp, vp, vp]),
@@ -503,6 +504,18 @@ def sell_build(row_ptr, cols, vals, col_base=0, ncol_ext=None):
     if r < 0:
         raise HPCCGError("sell_build: column outside the halo plan")
     return sb, sc[:slots], sv[:slots]
+
+
+def slot_plan(units: int, grid: int, spu: int = 1, rev: bool = False):
+    """The folded dot completion's plan for one launch shape (host only): per
+    group of 64 slices the unit whose block waits for the group, and the top
+    group (hpccg_hip_diag_slot_plan)."""
+    cap = (units * spu + 63) // 64
+    out = (C.c_int * max(cap, 1))()
+    top = C.c_int(-1)
+    n = lib().hpccg_hip_diag_slot_plan(units, grid, spu, int(rev), out, cap, C.byref(top))
+    _check(n if n < 0 else 0, "diag_slot_plan")
+    return list(out[:n]), top.value
 
 
 def halo_plan(row_ptr, cols, start_row, total_nrow):

@@ -160,6 +160,8 @@ void launch_sparsemv(const CgArgs& a, const double* xext, double* y, hipStream_t
 // Diagnostic: the SELL-512-A values streamed like the SpMV, known bytes (FETCH calibration).
 constexpr int kDiagStreamA = 9;
 void launch_stream_a(const CgArgs& a, hipStream_t s);
+// Slot completion plan (host): per group the unit that waits, and the top group; returns the group count.
+int slot_plan(int units, int grid, int spu, int rev, int* last_unit, int* top);
 
 // Device generator: writes the SELL-512 image, b, xexact.
 void launch_generate(int nx, int ny, int nz, int rank, int size, int use_7pt, long long col_base,

@@ -300,17 +300,18 @@ struct UnitMap {
     int units, per, spu;
     bool rev;
 };
-__device__ __forceinline__ int unit_block(const UnitMap& m, int u)
+__host__ __device__ constexpr int min_i(int a, int b) { return a < b ? a : b; }
+__host__ __device__ __forceinline__ int unit_block(const UnitMap& m, int u)
 {
     const int x = u / m.per, i = u % m.per;
     return kNumXcd * (m.rev ? m.per - 1 - i : i) + x;
 }
 // Within one eighth the block index is monotone in u, so the largest is at an
 // end of the group or of an eighth inside it.
-__device__ __forceinline__ int group_last_unit(const UnitMap& m, int g)
+__host__ __device__ __forceinline__ int group_last_unit(const UnitMap& m, int g)
 {
     const int upg = kGroup / m.spu;
-    const int u0 = g * upg, u1 = min(m.units, u0 + upg) - 1;
+    const int u0 = g * upg, u1 = min_i(m.units, u0 + upg) - 1;
     int best = u0, bb = unit_block(m, u0);
     auto cand = [&](int u) {
         if (u >= u0 && u <= u1) {
@@ -325,11 +326,11 @@ __device__ __forceinline__ int group_last_unit(const UnitMap& m, int g)
     }
     return best;
 }
-__device__ __forceinline__ int top_group(const UnitMap& m)
+__host__ __device__ __forceinline__ int top_group(const UnitMap& m)
 {
     int best = 0, bb = -1;
     for (int c = 0; c < kNumXcd && c * m.per < m.units; c++) {
-        const int us[2] = {c * m.per, min(m.units - 1, c * m.per + m.per - 1)};
+        const int us[2] = {c * m.per, min_i(m.units - 1, c * m.per + m.per - 1)};
         for (int u : us) {
             const int b = unit_block(m, u);
             if (b > bb) bb = b, best = u;
@@ -337,6 +338,7 @@ __device__ __forceinline__ int top_group(const UnitMap& m)
     }
     return best * m.spu / kGroup;
 }
+
 
 // The same fixed top-level shape computed by one wave (virtual waves in order);
 // valid in lane 0. ld(i) reads group sum i. All loads are issued before the sums.
@@ -1740,6 +1742,18 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         break;
     }
 #undef HPCCG_A
+}
+
+// Host restatement check of the slot completion's waiter choice (the same
+// functions the kernels run): for each group, its waiting unit; the top group.
+int slot_plan(int units, int grid, int spu, int rev, int* last_unit, int* top)
+{
+    if (units < 1 || grid < units || grid % kNumXcd || (spu != 1 && spu != 2)) return -1;
+    const UnitMap m{units, grid / kNumXcd, spu, rev != 0};
+    const int ng = (units * spu + kGroup - 1) / kGroup;
+    for (int g = 0; g < ng; g++) last_unit[g] = group_last_unit(m, g);
+    *top = top_group(m);
+    return ng;
 }
 
 void launch_stream_a(const CgArgs& a, hipStream_t s)

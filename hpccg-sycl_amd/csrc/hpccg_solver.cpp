@@ -2447,6 +2447,16 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_u
     return 0;
 }
 
+int hpccg_hip_diag_slot_plan(int units, int grid, int spu, int rev, int* last_unit, int cap, int* top_group)
+{
+    if (!last_unit || !top_group || units < 1) return set_err(HPCCG_HIP_EINVAL, "bad argument");
+    const int ng = (units * spu + 63) / 64;
+    if (ng > cap) return set_err(HPCCG_HIP_EINVAL, "cap %d < %d groups", cap, ng);
+    const int r = slot_plan(units, grid, spu, rev, last_unit, top_group);
+    if (r < 0) return set_err(HPCCG_HIP_EINVAL, "bad launch shape");
+    return r;
+}
+
 int hpccg_hip_kernel_times(const hpccg_hip_matrix* M, double out[4])
 {
     if (!M || !out) return set_err(HPCCG_HIP_EINVAL, "NULL argument");

@@ -185,6 +185,13 @@ int hpccg_hip_kernel_times_iter(const hpccg_hip_matrix* M, double* out, int cap)
  * resident p; kernel 9 streams the SELL-512-A values alone (8 B x slots read,
  * 8 B x n written: the rocprofv3 FETCH_SIZE calibration). */
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_us);
+/* Diagnostic (host only, no GPU): the folded dot completion's plan for a
+ * launch of `units` units (spu = 1 slice or 2 slices each) on `grid` blocks
+ * dealt over the 8 XCDs (rev: the update's reversed order): for each group of
+ * 64 slices the unit whose block waits for the group (the group's largest
+ * block index), and the top group. Returns the group count. Replaces nothing
+ * in the reference (ddot.cpp:60-88 sums on one thread). */
+int hpccg_hip_diag_slot_plan(int units, int grid, int spu, int rev, int* last_unit, int cap, int* top_group);
 
 /* ---- in-process rank group --------------------------------------------------
  * The z-slab decomposition of one process's RCCL job (make_local_matrix.cpp
