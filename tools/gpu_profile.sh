@@ -1,5 +1,6 @@
 #!/bin/bash
-# rocprofv3 evidence for the round: kernel-trace stats of the bench command,
+# rocprofv3 evidence for the round: kernel-trace stats of the default bench
+# command (its JSON line lands in $OUT/stats.log),
 # then FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md HBM
 # section) over the SpMV and the known-bytes streaming kernel used to
 # calibrate them. Stops at the first crash/timeout; no retries.
@@ -18,7 +19,10 @@ step() {
 }
 
 S=${STENCIL:-27}
-step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --stencil $S --steps 3 --warmup 1 --no-cpu-baseline
+# the committed bench line comes from this same process (same allocations as
+# the kernel stats: the per-process placement spread, DESIGN.md 4, cannot
+# separate the two), CPU baseline included
+step stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --stencil $S
 step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python tools/pmc_workload.py --n $N --stencil $S
 step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python tools/pmc_workload.py --n $N --stencil $S
 find $OUT -name "*.csv" | head -20
