@@ -289,6 +289,135 @@ __global__ __launch_bounds__(512) void k_la2d(Args a)
                                       wsum[4 * threadIdx.x + 2] + wsum[4 * threadIdx.x + 3];
 }
 
+
+// ---- persistent pair kernel, one continuous LDS-DMA value ring per wave ----
+// Grid = one block per CU. Block b of XCD x = b % 8 takes pairs x*PX + b/8 +
+// 32 t of its XCD's eighth (the XCD's 32 blocks advance side by side: a
+// compact front, so the +-1-plane windows hit L2). The ring runs on across
+// pairs (pair t + 1's first slots are issued during pair t's last ones); the
+// windows are double-buffered: pair t + 1's staging loads are issued when
+// pair t starts and land in the other buffer after its slots. Counted waits:
+// at slot j < kR of a pair the younger VMEM ops are the ring's other kR - 1
+// entries, the previous pair's epilogue (E: r, p_old loads, Ap, p stores) and
+// this pair's staging loads (S, per wave); afterwards only ring entries.
+template <int kR>
+__global__ __launch_bounds__(512) void k_la2dp(Args a)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ double wsum[2][8];
+    const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+    const int half = threadIdx.x / 256;
+    const int lrow = (threadIdx.x % 256) * 2;
+    const int len = a.win_len, tot = kNW * len;
+    double* ring = lds + 2 * tot + wave * kR * 128;
+    const double beta = a.beta;
+    const int x = blockIdx.x % 8, nb = gridDim.x / 8, bi = blockIdx.x / 8;
+    const int PX = (a.npairs + 7) / 8;
+    const int p0 = x * PX + bi, pend = min(a.npairs, (x + 1) * PX);
+    const int cnt = p0 < pend ? (pend - p0 + nb - 1) / nb : 0;
+    if (cnt == 0) return;
+    auto pair_of = [&](int t) { return p0 + nb * t; };
+    auto vrow = [&](int P) {
+        const int sl = min(2 * P + half, a.nslices - 1);
+        return a.val + (size_t)sl * kW * kS + lrow;
+    };
+    constexpr int kU = 5;
+    // staging loads of this wave: rounds u with 128 wave + 1024 u < tot, two arrays
+    int S = 0;
+    for (int u = 0; u < kU; u++)
+        if (128 * wave + 1024 * u < tot) S += 2;
+    d2v sr[kU], sp[kU];
+    auto stage_loads = [&](int P) {
+        const int prow0 = 2 * P * kS;
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int e = 2 * threadIdx.x + 1024 * u;
+            if (e < tot) {
+                const int w = e >= len ? (e >= 2 * len ? 2 : 1) : 0;
+                const int lo = w == 0 ? a.win_lo[0] : (w == 1 ? a.win_lo[1] : a.win_lo[2]);
+                const int l = prow0 + lo + (e - w * len);
+                sr[u] = ld2(a.r + l);
+                sp[u] = ld2(a.pold + l);
+            }
+        }
+    };
+    auto stage_store = [&](double* buf) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int e = 2 * threadIdx.x + 1024 * u;
+            if (e < tot) *(d2v*)(buf + e) = sr[u] + beta * sp[u];
+        }
+    };
+    // prologue: pair 0's first ring entries and windows
+    {
+        const double* vp = vrow(pair_of(0));
+#pragma unroll
+        for (int j = 0; j < kR; j++)
+            __builtin_amdgcn_global_load_lds((const void*)(vp + (size_t)j * kS), (lds_void*)(ring + j * 128), 16, 0, 2);
+        stage_loads(pair_of(0));
+        vm_wait(0);
+        stage_store(lds);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    int E = 0;  // epilogue VMEM ops of the previous pair (younger than this pair's first ring entries)
+    for (int t = 0; t < cnt; t++) {
+        const int cur = t & 1;
+        const int P = pair_of(t);
+        const bool more = t + 1 < cnt;
+        const int Pn = more ? pair_of(t + 1) : P;
+        const double* vp = vrow(P);
+        const double* vn = vrow(Pn);
+        const double* xs = lds + cur * tot;
+        const int S_t = more ? S : 0;
+        if (more) stage_loads(Pn);
+        const int rbase = (t * kW) % kR;  // ring entry of this pair's slot 0
+        const int prow = half * kS + lrow;
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < kW; j++) {
+            int younger;
+            if (j < kR)
+                younger = kR - 1 + E + S_t;
+            else
+                younger = kR - 1;
+            if (!more && j + kR >= kW) younger = min(younger, kW - 1 - j + (j < kR ? E + S_t : 0));
+            vm_wait(younger);
+            const int ent = (rbase + j) % kR;
+            const d2v v = *(const d2v*)(ring + ent * 128 + lane * 2);
+            const int c = prow + a.lds[j];
+            s0 = s0 + v.x * xs[c];
+            s1 = s1 + v.y * xs[c + 1];
+            asm volatile("" : "+v"(s0), "+v"(s1));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (j + kR < kW)
+                __builtin_amdgcn_global_load_lds((const void*)(vp + (size_t)(j + kR) * kS), (lds_void*)(ring + ent * 128), 16, 0, 2);
+            else if (more)
+                __builtin_amdgcn_global_load_lds((const void*)(vn + (size_t)(j + kR - kW) * kS), (lds_void*)(ring + ent * 128), 16, 0, 2);
+        }
+        const int s = 2 * P + half;
+        double d = 0.0;
+        E = 0;
+        if (s < a.nslices) {
+            const int row = s * kS + lrow;
+            const d2v pv = ld2(a.r + row) + beta * ld2(a.pold + row);
+            *(d2v*)(a.Ap + row) = d2v{s0, s1};
+            *(d2v*)(a.p + row) = pv;
+            d = pv.x * s0 + pv.y * s1;
+            E = 4;
+        }
+        const double wv = wsum64(d);
+        if (lane == 0) wsum[cur][wave] = wv;
+        if (more) stage_store(lds + (1 - cur) * tot);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (threadIdx.x < 2 && 2 * P + (int)threadIdx.x < a.nslices)
+            a.part[2 * P + threadIdx.x] = wsum[cur][4 * threadIdx.x] + wsum[cur][4 * threadIdx.x + 1] +
+                                          wsum[cur][4 * threadIdx.x + 2] + wsum[cur][4 * threadIdx.x + 3];
+    }
+    vm_wait(0);
+}
+
 // ---- persistent, pipelined: each block pulls pairs from its group's counter
 // (group = blockIdx % 8, i.e. one XCD under round-robin placement, for speed
 // only); while pair t streams from LDS buffer cur, the staging loads of the
@@ -771,6 +900,15 @@ int main(int argc, char** argv)
     run("la2d R4 o1", [&] { k_la2d<4, 1><<<gpair, 512, ldsd(4)>>>(a); }, true);
     run("la2d R2 o0", [&] { k_la2d<2, 0><<<gpair, 512, ldsd(2)>>>(a); }, true);
     run("la2d R1 o1 pipe", [&] { k_la2d<1, 1, true><<<gpair, 512, ldsd(1)>>>(a); }, true);
+    auto ldsp = [&](int R) { return 2 * lds1 + (size_t)8 * R * 1024; };
+    CK(hipFuncSetAttribute((const void*)k_la2dp<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
+    CK(hipFuncSetAttribute((const void*)k_la2dp<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
+    CK(hipFuncSetAttribute((const void*)k_la2dp<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
+    CK(hipFuncSetAttribute((const void*)k_la2dp<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
+    run("la2dp R3 (persistent)", [&] { k_la2dp<3><<<cus, 512, ldsp(3)>>>(a); }, true);
+    run("la2dp R4 (persistent)", [&] { k_la2dp<4><<<cus, 512, ldsp(4)>>>(a); }, true);
+    run("la2dp R6 (persistent)", [&] { k_la2dp<6><<<cus, 512, ldsp(6)>>>(a); }, true);
+    run("la2dp R8 (persistent)", [&] { k_la2dp<8><<<cus, 512, ldsp(8)>>>(a); }, true);
     run("la2d R2 o1 pipe", [&] { k_la2d<2, 1, true><<<gpair, 512, ldsd(2)>>>(a); }, true);
     run("la2d R3 o1 pipe", [&] { k_la2d<3, 1, true><<<gpair, 512, ldsd(3)>>>(a); }, true);
     // CG-shaped: an update pass (r = r - alpha Ap) between SpMVs, SpMV timed alone
@@ -805,5 +943,7 @@ int main(int argc, char** argv)
     cgrun("la2d R2 o1", [&] { k_la2d<2, 1><<<gpair, 512, ldsd(2)>>>(a); });
     cgrun("la2d R3 o1", [&] { k_la2d<3, 1><<<gpair, 512, ldsd(3)>>>(a); });
     cgrun("la2d R2 o1 pipe", [&] { k_la2d<2, 1, true><<<gpair, 512, ldsd(2)>>>(a); });
+    cgrun("la2dp R4 (persistent)", [&] { k_la2dp<4><<<cus, 512, ldsp(4)>>>(a); });
+    cgrun("la2dp R6 (persistent)", [&] { k_la2dp<6><<<cus, 512, ldsp(6)>>>(a); });
     return 0;
 }
