@@ -12,12 +12,15 @@
 //
 // Kernels of one CG iteration (HPCCG.cpp:358-386), one workgroup per 512-row
 // slice (two for the pair kernel), XCD-aware slice order:
-//   SpMV      k_spmv_a2 (SELL-512-A, LDS windows shared by slice pairs) |
+//   SpMV      k_spmv_a2r (SELL-512-A, LDS windows shared by slice pairs, the
+//             values streamed HBM -> LDS by per-wave LDS-DMA rings) |
+//             k_spmv_a2 (the same with register loads: non-uniform widths) |
 //             k_spmv_a (SELL-512-A, x read at the slice's offsets) |
 //             k_spmv_sell (SELL-512, int32 columns: any matrix)
-//             + p = r + beta p formed on the fly (fused) + p.Ap slice partials
-//   update    k_update: x (deferred), r = r - alpha Ap, r.r slice partials
-//   finalize  k_finalize: the fixed-shape total of a dot (unless folded)
+//             + p = r + beta p formed on the fly (fused) + p.Ap, completed
+//             in the kernel (self-validating slots)
+//   update    k_update: x (deferred), r = r - alpha Ap, r.r completed the same way
+//   finalize  k_finalize: the fixed-shape total of a dot (fold 0 only)
 #include <climits>
 
 #include "hpccg_internal.h"
