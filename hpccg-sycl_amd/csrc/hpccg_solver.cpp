@@ -1262,7 +1262,10 @@ thread_local bool g_capturing = false;
 
 bool overlap_ok(const Ranks& R)
 {
-    if (g_capturing) return false;
+    // nor in the eager tail of a graph-replayed solve: there the first
+    // overlapped iterations after the replays took ~60 ms each in an
+    // in-process group (tools/probe/ovl_probe.py: 258 vs 75 ms per 100^3 solve)
+    if (g_capturing || R.M[0]->graph_used) return false;
     for (int r = 0; r < R.P; r++) {
         const hpccg_hip_matrix* M = R.M[r];
         int lo, hi;
