@@ -855,7 +855,9 @@ int fold_effective(const hpccg_hip_matrix* M) { return (M->fold >= 0 && M->fold 
 // x_ring auto: the long ring where the matrix image is far beyond the 256 MB
 // Infinity Cache (7-pt 256^3 update 93 vs 103 us with 32 vs 8); near it, the 32
 // p buffers cycled through the cache evict the image (100^3: 14290 vs 14160
-// it/s with 8 vs 32).
+// it/s with 8 vs 32). A ring of 2 at 100^3 looked +4 % in one process (the
+// ring buffers of an 8-ring allocation) and measured -2.8 % across fresh
+// processes (tools/ab_bench_opts.sh: 18361 vs 18899 it/s, 4 rounds each).
 int x_ring_effective(const hpccg_hip_matrix* M)
 {
     if (M->x_ring > 0) return M->x_ring;
