@@ -192,6 +192,8 @@ def main():
     ap.add_argument("--overlap", type=int, default=-1, help="multi-rank: halo beside the interior SpMV")
     ap.add_argument("--a-pre", type=int, default=-1, help="direct kernel: value slots loaded before the test")
     ap.add_argument("--use-graph", type=int, default=-1, help="hipGraph replay (-1 default on)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VAL",
+                    help="any other solver option (hpccg_hip_set_option), e.g. --set nt_store=0")
     ap.add_argument("--event-steps", type=int, default=1,
                     help="timed steps launched eagerly with hipEvents around every SpMV (the roofline's kernel "
                          "time); the other timed steps replay hipGraphs")
@@ -227,6 +229,9 @@ def main():
                      ("use_graph", args.use_graph)):
         if val != -1:
             M.set_option(opt, val)
+    for kv in args.set:
+        key, _, val = kv.partition("=")
+        M.set_option(key.strip(), int(val))
     b, x0, _ = M.vectors()
     nrow = n * n * n
     x = torch.zeros(nrow, dtype=torch.float64, device=f"cuda:{local_rank}")
