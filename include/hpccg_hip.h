@@ -144,8 +144,9 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   update (hpccg_hip_kernel_times)
  *   "fuse_p"        -1 auto / 0 off: p = r + beta p formed inside the SpMV
  *                   (pair kernel: any rank count; direct kernel: one rank)
- *   "fold"          dots completed by the last block of the producing kernel:
- *                   0 neither, 1 both, 2 p.Ap only (auto), 3 r.r only
+ *   "fold"          dots completed inside the producing kernel (self-validating
+ *                   slots; tickets on unit-subset launches): 0 neither
+ *                   (k_finalize), 1 both (auto), 2 p.Ap only, 3 r.r only
  *   "x_defer"       1 = x += alpha p batched every x_ring iterations (default)
  *   "x_ring"        p ring length = x deferral depth, 2..64; -1 auto: 32 for
  *                   matrix images over 512 MB, else 8
@@ -154,6 +155,11 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   stream beside the interior SpMV (default 0; hipGraph
  *                   replays always run the halo in line on the main stream --
  *                   see DESIGN.md section 6 for the measurements)
+ *   "a2_ring"       pair kernel: value slots in flight per wave through its
+ *                   LDS-DMA ring, -1 auto (3), 0 register loads, 1..4
+ *                   (uniform widths 27 and 7)
+ *   "nt_store"      CG vector stores non-temporal: -1 auto (direct kernel on
+ *                   an image beyond the Infinity Cache), 0, 1
  *   "lds_ep"        pair kernel: the rows' own p_k taken from the staged
  *                   window instead of reloading r and p_{k-1} (default 1)
  *   "stage16"       pair kernel: windows staged as row pairs with 16-B loads
