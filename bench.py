@@ -147,17 +147,18 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=10.0, budget_1t_s=5.0):
     return out
 
 
-def pmc_traffic(tag, kernel, fused):
+def pmc_traffic(tag, kernel, fused, xdefer):
     """HBM bytes per SpMV launch from the committed rocprofv3 FETCH/WRITE
     passes of the same kernel configuration (profiles/pmc_<tag>.json; matched
-    by kernel template name and fusion), else (None, None)."""
+    by kernel template name, fusion and x deferral), else (None, None)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         d = json.load(f)
     name = d.get("kernel", "")
-    if KERNEL_NAMES[kernel] + "<" not in name or bool(d.get("fuse_p")) != bool(fused):
+    if KERNEL_NAMES[kernel] + "<" not in name or bool(d.get("fuse_p")) != bool(fused) or \
+            d.get("x_defer", 1) != xdefer:
         return None, None
     return d.get("spmv_hbm_bytes_per_launch"), f"profiles/pmc_{tag}.json ({d.get('tag', '?')}), matched by kernel name"
 
@@ -302,7 +303,12 @@ def main():
     # also 4 B of column), p or (r, p_{k-1}) once, p_k and Ap written
     slot_bytes = 12.0 if kernel == 0 else 8.0
     vec_bytes = (32.0 if fused else 16.0) * nrow
-    format_bytes = slot_bytes * slots + vec_bytes
+    # x_defer 2: the launch's trailing blocks apply the deferred x terms of
+    # 1/q of the rows (q = x_ring - 1): x read and written, q p's read
+    xside = M.get_option("x_defer") == 2
+    q = M.get_option("x_ring") - 1
+    side_bytes = (16.0 + 8.0 * q) / q * nrow if xside else 0.0
+    format_bytes = slot_bytes * slots + vec_bytes + side_bytes
     # SURVEY 8(d) credited bytes: HPC_sparsemv 12 nnz + 20 n, ddot(p, Ap) 16 n,
     # with the fused p update the waxpby p = r + beta p, 24 n
     credited = 12.0 * info["nnz"] + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fused else 0.0)
@@ -318,7 +324,7 @@ def main():
     value = it_per_s * world
     ms_per_step = elapsed / args.steps * 1e3
     iter_bytes = 12.0 * info["nnz"] + 116.0 * nrow  # unfused reference sequence, SURVEY 8(d)
-    traffic, traffic_src = pmc_traffic(f"spmv_{args.stencil}pt_{n}", kfmt, fused)
+    traffic, traffic_src = pmc_traffic(f"spmv_{args.stencil}pt_{n}", kfmt, fused, M.get_option("x_defer"))
 
     if rank == 0:
         out = {
@@ -365,7 +371,9 @@ def main():
                 "bytes_formula": ("%g B per stored slot x %d slots + %d B per row (r, p_{k-1} read; p_k, Ap "
                                   "written)" % (slot_bytes, slots, 32) if fused else
                                   "%g B per stored slot x %d slots + 16 B per row (p read, Ap written)" %
-                                  (slot_bytes, slots)),
+                                  (slot_bytes, slots)) +
+                                 (" + (16 + 8 q) / q B per row, q = %d (side blocks: x read and written, q p's read "
+                                  "for 1/q of the rows)" % q if xside else ""),
                 "credited_bytes_per_launch": credited,
                 "credited_frac": round(credited / spmv_avg_s / 1e9 / HBM_PEAK_GBS, 4),
                 "credited_formula": "SURVEY 8(d): 12 nnz + 20 n (SpMV) + 16 n (ddot p.Ap)" +

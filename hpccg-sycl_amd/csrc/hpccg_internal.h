@@ -58,7 +58,7 @@ struct CgArgs {
     double* p;             // local rows of ring buffer 0; p - ghost_lo .. p + n + ghost_hi valid
     long long pstride;     // distance between ring buffers of p (doubles)
     int nring;             // p_k lives in ring buffer k % nring
-    int xdefer;            // 1: x += alpha_j p_j applied every nring iterations
+    int xdefer;            // deferred x += alpha_j p_j: 1 every nring-th update, all rows; 2 beside the SpMV (side_flush)
     int rev;               // 1: the update kernel walks each XCD's slices backwards
     int s0, sn0, s1, sn1;  // SpMV launch: units [s0, s0 + sn0) then [s1, s1 + sn1) (slices; pairs for kSpmvPairs)
     int sgrid;             // SpMV launch grid (sn0 + sn1 rounded up to a multiple of kNumXcd)
@@ -95,6 +95,7 @@ struct CgArgs {
     int nt_store;                 // CG vector stores non-temporal
     int slots;                    // folded dots complete through self-validating slots (launch covers all units)
     int a2_ring;                  // pair kernel: value slots in flight per wave through its LDS-DMA ring (0: register loads)
+    int xside;                    // x_defer 2: this SpMV launch carries the side-flush blocks
 };
 
 // Is dot `which` (kRR / kPAP) completed inside its producing kernel?

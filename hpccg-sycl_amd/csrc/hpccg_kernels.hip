@@ -628,6 +628,7 @@ __global__ __launch_bounds__(256) void k_pack(CgArgs a, const int* __restrict__ 
 // iteration that overlaps its halo exchange. -1: no unit.
 __device__ __forceinline__ int unit_of(const CgArgs& a)
 {
+    if ((int)blockIdx.x >= a.sgrid) return -1;  // x_defer 2: a side-flush block
     const int i = xcd_slice(a.sgrid);
     if (i >= a.sn0 + a.sn1) return -1;
     return i < a.sn0 ? a.s0 + i : a.s1 + (i - a.sn0);
@@ -674,6 +675,60 @@ __device__ __forceinline__ double spmv_rows_out(const CgArgs& a, const IterState
 // gathered through L1/L2/MALL from p_k (computed by k_p_update). Padding slots
 // (col -1, value 0) add +0, which never changes a row sum that starts at +0.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// x_defer 2: the deferred x update beside the SpMV. The SpMV launch of
+// iteration k carries trailing blocks (index >= sgrid: dispatched last, they
+// take the CUs the SpMV's last blocks leave idle) that apply x += alpha_j p_j
+// for j = max(1, k - q) .. k - 1 (q = nring - 1) to the slices whose turn it
+// is (s % q == k % q), in order, one rounding per term (HPCCG.cpp:383). The
+// SpMV writes only ring buffer k % nring, which holds none of those p_j, and
+// alpha_j (j < k) is in ahist; k_xflush applies the rest after the loop. Per
+// row the same terms in the same order as every iteration's waxpby: same bits.
+// kSpu: slices per block (512-thread pair kernels 2, else 1); kB: p loads in
+// flight per thread, as many as the host kernel's occupancy leaves VGPRs for
+// (the ring pair kernel's is set by its LDS, 2 blocks per CU: 16; the direct
+// kernel keeps its own VGPR count: 8 at width 7, 4 at width 27).
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int side_blocks(int nslices, int nring, int spu)
+{
+    return ((nslices + nring - 2) / (nring - 1) + spu - 1) / spu;
+}
+
+template <int kSpu, int kB>
+__device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
+{
+    if ((int)blockIdx.x < a.sgrid) return false;
+    if (prologue) return true;
+    const int k = a.kst[0];
+    if (k < 2 || !cg_run(a, k, false)) return true;
+    const int q = a.nring - 1;
+    const int s = k % q + q * (kSpu * ((int)blockIdx.x - a.sgrid) + (int)threadIdx.x / kBlock);
+    if (s >= a.nslices) return true;
+    const int row = s * kSliceRows + (threadIdx.x % kBlock) * kRpt;
+    // streamed once: non-temporal, so they do not displace the SpMV's window rows from L2
+    Rows xn = ld_m<true>(a.x + row);
+    for (int j0 = max(1, k - q); j0 < k; j0 += kB) {
+        Rows pj[kB];
+        double aj[kB];
+#pragma unroll
+        for (int b = 0; b < kB; b++) {
+            const int j = min(j0 + b, k - 1);
+            pj[b] = ld_m<true>(cur_p(a, j) + row);
+            aj[b] = sld(a.ahist + j);  // written by earlier updates: scalar loads
+        }
+#pragma unroll
+        for (int b = 0; b < kB; b++)
+            if (j0 + b < k)
+#pragma unroll
+                for (int i = 0; i < kRpt; i++) xn.v[i] = xn.v[i] + aj[b] * pj[b].v[i];
+    }
+    if (row + kRpt <= a.n)
+        __builtin_nontemporal_store(d2v{xn.v[0], xn.v[1]}, reinterpret_cast<d2v*>(a.x + row));
+    else
+        st_rows(a.x, row, a.n, xn);
+    return true;
+}
+
 template <bool kNT>
 __global__ __launch_bounds__(kBlock) void k_spmv_sell(CgArgs a, bool prologue)
 {
@@ -744,6 +799,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
             for (int j = 0; j < kW; j++) offp[j] = a.aoff[(size_t)s * kAMax + j];
         }
     }
+    if (side_flush<1, kW == 7 ? 8 : 4>(a, prologue)) return;
     IterState st;
     if (!spmv_begin<kFuse>(a, prologue, st)) return;
     if (s < 0) return;
@@ -1078,6 +1134,7 @@ constexpr int kA2RingMax = 4;
 template <bool kFuse, int kW, int kR>
 __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2r(CgArgs a, bool prologue)
 {
+    if (side_flush<2, 16>(a, prologue)) return;
     static_assert(kR >= 1 && kR <= kA2RingMax && kR <= kW, "ring depth");
     extern __shared__ __attribute__((aligned(16))) double xs[];
     const int P = unit_of(a);
@@ -1354,7 +1411,7 @@ __global__ __launch_bounds__(kBlock) void k_update(CgArgs a)
 #pragma unroll
             for (int i = 0; i < kRpt; i++) xn.v[i] = xv.v[i] + alpha * pv.v[i];
             st_vec(a, a.x, row, xn);
-        } else if (k % a.nring == 0) {
+        } else if (a.xdefer == 1 && k % a.nring == 0) {
             // deferred x update (HPCCG.cpp:383 for iterations k-nring+1 .. k)
             Rows xn = ld(a.x + row);
             x_accumulate(a, row, k - a.nring + 1, k, k, alpha, xn);
@@ -1391,11 +1448,20 @@ __global__ void k_end(CgArgs a) { mark_end(a); }
 // update (niters = kst[0] - 1 is final here).
 __global__ __launch_bounds__(kBlock) void k_xflush(CgArgs a)
 {
+    if (!a.xdefer) return;
     const int niters = a.kst[0] - 1;
-    const int first = (niters / a.nring) * a.nring + 1;
-    if (!a.xdefer || first > niters) return;
     const int s = xcd_slice(a.grid);
     if (s >= a.nslices) return;
+    // the last term already applied to this slice's x (0: none)
+    int last;
+    if (a.xdefer == 1) {
+        last = (niters / a.nring) * a.nring;
+    } else {  // beside the SpMV: the SpMV of iteration kp applied terms up to kp - 1
+        const int q = a.nring - 1, ph = s % q == 0 ? q : s % q;
+        last = niters >= ph ? niters - (niters - ph) % q - 1 : 0;
+    }
+    const int first = last + 1;
+    if (first > niters) return;
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     Rows xn = ld(a.x + row);
     x_accumulate(a, row, first, niters, -1, 0.0, xn);
@@ -1671,16 +1737,21 @@ int a2_ring_prepare()
 void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
 {
     const bool fuse = a.fuse_p && !prologue;
+    // x_defer 2: the side-flush blocks trail the units (one launch per iteration carries them)
+    const bool side = !prologue && a.xdefer == 2 && a.xside &&
+                      ((kernel == kSpmvPairs && a.a2_ring > 0) || kernel == kSpmvDirect);
+    const int spu = kernel == kSpmvPairs ? 2 : 1;
+    const dim3 sg(a.sgrid + (side ? side_blocks(a.nslices, a.nring, spu) : 0));
 #define HPCCG_A(W, NT, PRE)                                                                                       \
     do {                                                                                                          \
         if (a.atri && tri_groups(W) > 0 && PRE > 0 && fuse)                                                     \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE, true>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue); \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE, true>), sg, dim3(kBlock), 0, s, a, prologue); \
         else if (a.atri && tri_groups(W) > 0 && PRE > 0)                                                        \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE, true>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue); \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE, true>), sg, dim3(kBlock), 0, s, a, prologue); \
         else if (fuse)                                                                                            \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue);       \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE>), sg, dim3(kBlock), 0, s, a, prologue);       \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue);      \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE>), sg, dim3(kBlock), 0, s, a, prologue);      \
     } while (0)
     switch (kernel) {
     case kSpmvPairs: {
@@ -1689,9 +1760,9 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
 #define HPCCG_A2R(W, R)                                                                                           \
     do {                                                                                                          \
         if (fuse)                                                                                                 \
-            hipLaunchKernelGGL((k_spmv_a2r<true, W, R>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue); \
+            hipLaunchKernelGGL((k_spmv_a2r<true, W, R>), sg, dim3(2 * kBlock), smem, s, a, prologue); \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_spmv_a2r<false, W, R>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue); \
+            hipLaunchKernelGGL((k_spmv_a2r<false, W, R>), sg, dim3(2 * kBlock), smem, s, a, prologue); \
     } while (0)
             if (a.a_width == 7) {
                 switch (a.a2_ring) {
@@ -1713,9 +1784,9 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         }
         const size_t smem = (size_t)a.alds2_doubles * sizeof(double);
         if (fuse)
-            hipLaunchKernelGGL((k_spmv_a2<true, true, 3>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue);
+            hipLaunchKernelGGL((k_spmv_a2<true, true, 3>), sg, dim3(2 * kBlock), smem, s, a, prologue);
         else
-            hipLaunchKernelGGL((k_spmv_a2<true, false, 3>), dim3(a.sgrid), dim3(2 * kBlock), smem, s, a, prologue);
+            hipLaunchKernelGGL((k_spmv_a2<true, false, 3>), sg, dim3(2 * kBlock), smem, s, a, prologue);
         break;
     }
     case kSpmvDirect:
@@ -1739,9 +1810,9 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         break;
     default:
         if (a.nt)
-            hipLaunchKernelGGL((k_spmv_sell<true>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue);
+            hipLaunchKernelGGL((k_spmv_sell<true>), sg, dim3(kBlock), 0, s, a, prologue);
         else
-            hipLaunchKernelGGL((k_spmv_sell<false>), dim3(a.sgrid), dim3(kBlock), 0, s, a, prologue);
+            hipLaunchKernelGGL((k_spmv_sell<false>), sg, dim3(kBlock), 0, s, a, prologue);
         break;
     }
 #undef HPCCG_A

@@ -246,7 +246,7 @@ struct hpccg_hip_matrix {
     double* d_p = nullptr;     // local rows of ring buffer 0
     long long pstride = 0;
     double* d_ahist = nullptr;
-    int x_defer = 1;
+    int x_defer = 2;      // deferred x: beside the SpMV where the kernel carries it, else batched (x_defer_effective)
     int x_ring = -1;
     int rev_update = 1;
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
@@ -944,6 +944,15 @@ int ensure_hist(hpccg_hip_matrix* M, int max_iter)
 
 int grid_of(int units) { return std::max(kNumXcd, (units + kNumXcd - 1) / kNumXcd * kNumXcd); }
 
+// x_defer 2 (x terms applied by trailing blocks of the SpMV launch) is built
+// into the LDS-DMA ring pair kernel and the direct kernel; elsewhere it means 1.
+int x_defer_effective(const hpccg_hip_matrix* M)
+{
+    const bool side = (M->kernel == kSpmvPairs && a2_ring_effective(M) > 0) || M->kernel == kSpmvDirect;
+    if (M->x_defer == 2 && !side) return 1;
+    return M->x_defer;
+}
+
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
 {
     CgArgs a;
@@ -962,7 +971,8 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.p = M->d_p;
     a.pstride = M->pstride;
     a.fuse_p = fuse_p_effective(M) ? 1 : 0;
-    a.xdefer = M->x_defer ? 1 : 0;
+    a.xdefer = x_defer_effective(M);
+    a.xside = 1;
     a.rev = M->rev_update ? 1 : 0;
     a.nring = a.xdefer ? x_ring_effective(M) : (a.fuse_p ? 2 : 1);
     const int units = M->kernel == kSpmvPairs ? (M->nslices + 1) / 2 : M->nslices;
@@ -1018,6 +1028,7 @@ CgArgs unit_range(const CgArgs& a, int s0, int n0, int s1, int n1)
     // a subset of the units: a group's members may sit in another launch,
     // so the folded dots take tickets
     b.slots = (s0 == 0 && n1 == 0 && n0 == a.sn0 + a.sn1) ? a.slots : 0;
+    b.xside = 0;  // the caller gives the side-flush blocks to one of its launches
     return b;
 }
 
@@ -1322,7 +1333,9 @@ int enqueue_spmv_overlapped(const Ranks& R, int slot, int k_host)
         const int units = a.sn0 + a.sn1;
         const int mid = units - lo - hi;
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
-        launch_cg_spmv(unit_range(a, lo, mid, 0, 0), M->kernel, false, M->stream);
+        CgArgs ai = unit_range(a, lo, mid, 0, 0);
+        ai.xside = a.xside;
+        launch_cg_spmv(ai, M->kernel, false, M->stream);
         HIP_TRY(hipStreamWaitEvent(M->stream, M->ev_halo, 0));
         if (lo + hi > 0) launch_cg_spmv(unit_range(a, 0, lo, units - hi, hi), M->kernel, false, M->stream);
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
@@ -2284,6 +2297,9 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "fuse_p")) {
         M->fuse_p = value < 0 ? -1 : (value ? 1 : 0);
     } else if (!std::strcmp(key, "x_defer")) {
+        if (value < 0 || value > 2)
+            return set_err(HPCCG_HIP_EINVAL, "x_defer must be 0 (every iteration), 1 (batched in the update) or 2 "
+                                             "(beside the SpMV)");
         M->x_defer = (int)value;
     } else if (!std::strcmp(key, "x_ring")) {
         if (value != -1 && (value < 2 || value > kXRingMax))
@@ -2351,7 +2367,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "event_timing")) *value = M->event_timing;
     else if (!std::strcmp(key, "fuse_p")) *value = fuse_p_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "fold")) *value = fold_effective(M);
-    else if (!std::strcmp(key, "x_defer")) *value = M->x_defer;
+    else if (!std::strcmp(key, "x_defer")) *value = x_defer_effective(M);
     else if (!std::strcmp(key, "x_ring")) *value = x_ring_effective(M);
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);

@@ -147,7 +147,11 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *   "fold"          dots completed inside the producing kernel (self-validating
  *                   slots; tickets on unit-subset launches): 0 neither
  *                   (k_finalize), 1 both (auto), 2 p.Ap only, 3 r.r only
- *   "x_defer"       1 = x += alpha p batched every x_ring iterations (default)
+ *   "x_defer"       x += alpha p deferred over the p ring: 1 = every x_ring-th
+ *                   update applies it to all rows; 2 (default) = trailing blocks
+ *                   of every SpMV launch apply it to the 1/(x_ring-1) of the
+ *                   slices whose turn it is (SELL-512-A kernels; reads back 1
+ *                   with the others); 0 = every iteration (same bits all ways)
  *   "x_ring"        p ring length = x deferral depth, 2..64; -1 auto: 32 for
  *                   matrix images over 512 MB, else 8
  *   "rev_update"    1 = the update kernel walks each XCD's slices backwards

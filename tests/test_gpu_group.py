@@ -65,7 +65,7 @@ def test_group_kernel_variants_bitwise(hp, gpu):
     finally:
         hp.set_keep_sell(False)
     ref = None
-    for kernel, fold, fuse, defer, ovl, graph in itertools.product((2, 1, 0), (0, 1, 2), (0, -1), (0, 1),
+    for kernel, fold, fuse, defer, ovl, graph in itertools.product((2, 1, 0), (0, 1, 2), (0, -1), (0, 1, 2),
                                                                    (0, 1), (0, 1)):
         for M in Ms:
             M.set_option("spmv_kernel", kernel)
@@ -93,7 +93,7 @@ def test_group_kernel_variants_bitwise(hp, gpu):
             M.set_option("spmv_kernel", -1)
             M.set_option("fuse_p", -1)
             M.set_option("overlap", 1)
-            M.set_option("x_defer", 1)
+            M.set_option("x_defer", 1 + ring % 2)  # batched / staggered
             M.set_option("x_ring", ring)
             M.set_option("graph_chunk", chunk)
             M.set_option("fold", fold)

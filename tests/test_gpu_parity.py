@@ -119,6 +119,31 @@ def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
         M.set_option("a2_ring", ring)
         assert M.get_option("a2_ring") == (3 if ring < 0 else ring)
         out[("ring", fuse, ring)] = solve_bits(hp, M, prob.b, 120)
+    # x_defer 2: the deferred x terms applied by trailing blocks of the ring
+    # kernel's launch (119 iterations: a different remainder per slice for k_xflush)
+    for fuse, xring, graph in ((-1, 32, 1), (0, 32, 0), (-1, 2, 1), (-1, 5, 0), (0, 9, 1)):
+        M.set_option("fuse_p", fuse)
+        M.set_option("a2_ring", -1)
+        M.set_option("x_defer", 2)
+        M.set_option("x_ring", xring)
+        M.set_option("use_graph", graph)
+        assert M.get_option("x_defer") == 2
+        out[("side", fuse, xring, graph)] = solve_bits(hp, M, prob.b, 120)
+    M.set_option("a2_ring", 0)
+    assert M.get_option("x_defer") == 1  # register-load pair kernel: batched in the update
+    M.set_option("a2_ring", -1)
+    # and by trailing blocks of the direct kernel's launch
+    M.set_option("spmv_kernel", DIRECT)
+    for fuse, xring, pre in ((-1, 32, -1), (0, 8, 0), (-1, 3, -1)):
+        M.set_option("fuse_p", fuse)
+        M.set_option("x_ring", xring)
+        M.set_option("a_pre", pre)
+        assert M.get_option("x_defer") == 2
+        out[("side-direct", fuse, xring, pre)] = solve_bits(hp, M, prob.b, 120)
+    M.set_option("spmv_kernel", SELL)
+    assert M.get_option("x_defer") == 1
+    M.set_option("x_defer", 1)
+    M.set_option("use_graph", 1)
     bad = [k for k, o in out.items() if o != out[(SELL, 0)]]
     assert not bad, bad
 
@@ -133,7 +158,7 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     results = []
     for kernel in (DIRECT, PAIRS):
         M.set_option("spmv_kernel", kernel)
-        for fuse, fold, graph, defer in itertools.product((0, -1), (0, 1, 2, 3), (0, 1), (0, 1)):
+        for fuse, fold, graph, defer in itertools.product((0, -1), (0, 1, 2, 3), (0, 1), (0, 1, 2)):
             M.set_option("fuse_p", fuse)
             M.set_option("fold", fold)
             M.set_option("use_graph", graph)
@@ -147,10 +172,11 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
                 assert M.get_option("graph_used") == 1
     # the x-deferral depth (p ring length) only moves when x is written:
     # rings of 2 .. 64, 119 iterations leave 1 .. 55 updates for k_xflush
-    M.set_option("x_defer", 1)
+    # (staggered: a different remainder per slice)
     M.set_option("fold", -1)
     M.set_option("nt_store", -1)
-    for ring, graph in ((2, 1), (5, 0), (16, 1), (32, 1), (64, 0), (8, 1), (-1, 1)):
+    for i, (ring, graph) in enumerate(((2, 1), (5, 0), (16, 1), (32, 1), (64, 0), (8, 1), (-1, 1), (32, 0), (5, 1))):
+        M.set_option("x_defer", 1 + i % 2)
         M.set_option("x_ring", ring)
         M.set_option("use_graph", graph)
         assert M.get_option("x_ring") == (ring if ring > 0 else 8)  # auto: 8 for a small image

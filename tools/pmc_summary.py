@@ -107,6 +107,19 @@ def main():
     # the bytes the format must move: 8 B per stored slot, + r, p_{k-1} read and
     # p_k, Ap written (fused) or p read and Ap written
     compulsory = 8.0 * slots + (32.0 if fuse_p else 16.0) * nrow
+    # x_defer 2: trailing blocks of every launch but the first iteration's
+    # apply the deferred x terms of 1/q of the rows (x read and written, q p's)
+    bench = None
+    if bench_log and os.path.exists(bench_log):
+        lines = [l for l in open(bench_log) if l.startswith("{")]
+        bench = json.loads(lines[-1]) if lines else None
+    opts = bench["config"]["options"] if bench else {}
+    side = 0.0
+    if opts.get("x_defer") == 2:
+        q = opts["x_ring"] - 1
+        launches = len(fetch[(kname, "FETCH_SIZE")])
+        side = (16.0 + 8.0 * q) / q * nrow * (launches - 1) / launches
+        compulsory += side
 
     avg_ns = None
     calls = -1
@@ -123,6 +136,8 @@ def main():
         "fuse_p": fuse_p,
         "bytes_formula": "12 nnz + 20 n + 16 n" + (" + 24 n" if fuse_p else ""),
         "format_compulsory_bytes_per_launch": compulsory,
+        "x_defer": opts.get("x_defer"),
+        "side_flush_bytes_per_launch": side,
         "fetch_size_kib_raw": f_spmv,
         "write_size_kib_raw": w_spmv,
         "fetch_calibration": {"kernel": "k_stream_a", "known_read_bytes": stream_read,
@@ -150,13 +165,10 @@ def main():
                              "read_bytes": round(sum(v) / len(v) * 1024.0 * fetch_factor),
                              "write_bytes": round(sum(wv) / len(wv) * 1024.0)}
     out["per_kernel_hbm_bytes_per_launch"] = per_kernel
-    if bench_log and os.path.exists(bench_log):
-        lines = [l for l in open(bench_log) if l.startswith("{")]
-        if lines:
-            b = json.loads(lines[-1])
-            out["bench_avg_launch_us"] = b["roofline"]["avg_launch_us"]
-            out["bench_value"] = b["value"]
-            shutil.copy(bench_log, os.path.join(outdir, "bench_line.json"))
+    if bench:
+        out["bench_avg_launch_us"] = bench["roofline"]["avg_launch_us"]
+        out["bench_value"] = bench["value"]
+        shutil.copy(bench_log, os.path.join(outdir, "bench_line.json"))
     with open(os.path.join(ROOT, "profiles", f"pmc_spmv_{stencil}pt_{n}.json"), "w") as f:
         json.dump(out, f, indent=1)
     with open(os.path.join(outdir, "summary.json"), "w") as f:

@@ -12,7 +12,7 @@ from bench import load_pkg  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=200)
-ap.add_argument("--iters", type=int, default=12)
+ap.add_argument("--iters", type=int, default=32)  # x_defer 2: every launch but the first carries side blocks
 ap.add_argument("--stencil", type=int, default=27, choices=[27, 7])
 ap.add_argument("--kernel", type=int, default=-1, help="SpMV kernel (-1: the library's choice)")
 ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1: default)")
@@ -30,4 +30,5 @@ b, _, _ = M.vectors()
 x = torch.zeros(args.n ** 3, dtype=torch.float64, device="cuda:0")
 M.set_option("use_graph", 0)
 hp.HPCCG(M, b, x, max_iter=args.iters, device=True)
-print("fuse_p", M.get_option("fuse_p"), "kernel", M.get_option("spmv_kernel"), "slots", M.info()["slots"])
+print("fuse_p", M.get_option("fuse_p"), "kernel", M.get_option("spmv_kernel"), "slots", M.info()["slots"],
+      "x_defer", M.get_option("x_defer"), "x_ring", M.get_option("x_ring"))
