@@ -43,7 +43,8 @@ def main():
     x = torch.zeros(args.n ** 3, dtype=torch.float64, device="cuda:0")
     variants = [parse(v) for v in args.variants.split(";")]
     keys = sorted({k for v in variants for k in v})
-    defaults = {k: -1 for k in keys}
+    # each key's value before any variant touches it (-1 is not valid for every option)
+    defaults = {k: M.get_option(k) for k in keys}
 
     def apply(v):
         for k in keys:
