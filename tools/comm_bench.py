@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--7pt", dest="s7", action="store_true")
     ap.add_argument("--variants", default="0:0:1,1:0:1,2:0:1,2:1:1,2:0:0,2:1:0",
-                    help="force_comm:overlap:use_graph triples")
+                    help="force_comm:overlap:use_graph triples, optionally :spmv_kernel")
     args = ap.parse_args()
     import torch
     hp = load_pkg()
@@ -40,7 +40,9 @@ def main():
         base = None
         traces = {}
         for v in args.variants.split(","):
-            fc, ovl, graph = (int(t) for t in v.split(":"))
+            f = [int(t) for t in v.split(":")]
+            fc, ovl, graph = f[:3]
+            M.set_option("spmv_kernel", f[3] if len(f) > 3 else -1)
             M.set_option("force_comm", fc)
             M.set_option("overlap", ovl)
             M.set_option("use_graph", graph)
@@ -63,7 +65,8 @@ def main():
                               "use_graph": graph, "us_per_iter": round(us, 2),
                               "added_us_per_iter": round(us - base, 2),
                               "overlap_in_use": M.get_option("overlap"), "graph_used": M.get_option("graph_used"),
-                              "kernel": M.get_option("spmv_kernel"), "niters": it,
+                              "kernel": M.get_option("spmv_kernel"), "fuse_p": M.get_option("fuse_p"),
+                              "niters": it,
                               "trace_equal_first": traces[v] == next(iter(traces.values()))}), flush=True)
         M.close()
     finally:
