@@ -266,7 +266,7 @@ struct hpccg_hip_matrix {
     // hipGraph of graph_chunk iterations (kernel arguments are baked in)
     hipGraphExec_t graph_exec = nullptr;
     int graph_chunk = 0;
-    int graph_iters = 8;
+    int graph_iters = 32;  // 100^3 same-process A/B: 20 442 vs 20 198 it/s at 8 (200^3 +0.15 %); 499 (one graph per solve) 20 033
     std::vector<CgArgs> graph_args;
     int graph_kernel = -1;
     int graph_failed = 0;      // capture refused here (e.g. RCCL inside a graph): eager from then on

@@ -138,7 +138,7 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *   "use_graph"     replay CG iterations from hipGraphs (default 1; every rank
  *                   count, RCCL calls captured; falls back to eager launches if
  *                   the capture is refused); get "graph_used": the last solve did
- *   "graph_chunk"   iterations per graph (default 8; a multiple of the p ring
+ *   "graph_chunk"   iterations per graph (default 32; a multiple of the p ring
  *                   when a halo is exchanged)
  *   "event_timing"  1 = eager launches with hipEvents around every SpMV and
  *                   update (hpccg_hip_kernel_times)
