@@ -124,7 +124,7 @@ def main():
     avg_ns = None
     calls = -1
     # the kernel the PMC passes measured (the stats run may also hold other
-    # SpMV kernels, e.g. bench's SELL-512-V secondary figure)
+    # SpMV kernels, e.g. the prologue's unfused launch)
     for row in csv.DictReader(open(stats)):
         if row["Name"] == kname and int(row["Calls"]) > calls:
             avg_ns, calls = float(row["AverageNs"]), int(row["Calls"])
