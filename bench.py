@@ -97,7 +97,7 @@ def host_cpu():
     return info
 
 
-def cpu_baseline(nx, ny, nz, use_7pt, budget_s=10.0, budget_1t_s=5.0):
+def cpu_baseline(nx, ny, nz, use_7pt, budget_s=30.0, budget_1t_s=15.0):
     """The reference (oracle/_ref: its own sources compiled in this repo's
     recipe) on the host cores, bounded: the first iterations of one HPCCG()
     solve of the same matrix, OpenMP with the host's threads and serial."""

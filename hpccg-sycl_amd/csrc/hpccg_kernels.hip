@@ -18,8 +18,10 @@
 //             k_spmv_a (SELL-512-A, x read at the slice's offsets) |
 //             k_spmv_sell (SELL-512, int32 columns: any matrix)
 //             + p = r + beta p formed on the fly (fused) + p.Ap, completed
-//             in the kernel (self-validating slots)
-//   update    k_update: x (deferred), r = r - alpha Ap, r.r completed the same way
+//             in the kernel (self-validating slots); trailing blocks apply
+//             the deferred x terms of 1/(x_ring-1) of the slices (side_flush)
+//   update    k_update: r = r - alpha Ap (x too with x_defer 0 / 1), r.r
+//             completed the same way
 //   finalize  k_finalize: the fixed-shape total of a dot (fold 0 only)
 #include <climits>
 
