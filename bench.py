@@ -147,7 +147,7 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=30.0, budget_1t_s=15.0):
     return out
 
 
-def pmc_traffic(tag, kernel, fused, xdefer):
+def pmc_traffic(tag, kernel, fused, xdefer, fupd):
     """HBM bytes per SpMV launch from the committed rocprofv3 FETCH/WRITE
     passes of the same kernel configuration (profiles/pmc_<tag>.json; matched
     by kernel template name, fusion and x deferral), else (None, None)."""
@@ -158,7 +158,7 @@ def pmc_traffic(tag, kernel, fused, xdefer):
         d = json.load(f)
     name = d.get("kernel", "")
     if KERNEL_NAMES[kernel] + "<" not in name or bool(d.get("fuse_p")) != bool(fused) or \
-            d.get("x_defer", 1) != xdefer:
+            d.get("x_defer", 1) != xdefer or d.get("fuse_update", 0) != fupd:
         return None, None
     return d.get("spmv_hbm_bytes_per_launch"), f"profiles/pmc_{tag}.json ({d.get('tag', '?')}), matched by kernel name"
 
@@ -308,7 +308,10 @@ def main():
     xside = M.get_option("x_defer") == 2
     q = M.get_option("x_ring") - 1
     side_bytes = (16.0 + 8.0 * q) / q * nrow if xside else 0.0
-    format_bytes = slot_bytes * slots + vec_bytes + side_bytes
+    # fused update: the launch's trailing blocks also run the update (r, Ap read; r written)
+    fupd = M.get_option("fuse_update") == 1
+    upd_bytes = 24.0 * nrow if fupd else 0.0
+    format_bytes = slot_bytes * slots + vec_bytes + side_bytes + upd_bytes
     # SURVEY 8(d) credited bytes: HPC_sparsemv 12 nnz + 20 n, ddot(p, Ap) 16 n,
     # with the fused p update the waxpby p = r + beta p, 24 n
     credited = 12.0 * info["nnz"] + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fused else 0.0)
@@ -324,7 +327,8 @@ def main():
     value = it_per_s * world
     ms_per_step = elapsed / args.steps * 1e3
     iter_bytes = 12.0 * info["nnz"] + 116.0 * nrow  # unfused reference sequence, SURVEY 8(d)
-    traffic, traffic_src = pmc_traffic(f"spmv_{args.stencil}pt_{n}", kfmt, fused, M.get_option("x_defer"))
+    traffic, traffic_src = pmc_traffic(f"spmv_{args.stencil}pt_{n}", kfmt, fused, M.get_option("x_defer"),
+                                       M.get_option("fuse_update"))
 
     if rank == 0:
         out = {
@@ -350,7 +354,8 @@ def main():
                 "device_bytes_per_gpu": M.get_option("device_bytes"),
                 "graph_replay": bool(graph_used),
                 "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update",
-                                                         "overlap", "graph_chunk", "nt", "a2_ring", "nt_store")},
+                                                         "overlap", "graph_chunk", "nt", "a2_ring", "nt_store",
+                                                         "fuse_update")},
             },
             "cg_iterations_per_s_global": round(it_per_s, 3),
             "spmv_effective_gbs": round(achieved, 1),
@@ -373,7 +378,8 @@ def main():
                                   "%g B per stored slot x %d slots + 16 B per row (p read, Ap written)" %
                                   (slot_bytes, slots)) +
                                  (" + (16 + 8 q) / q B per row, q = %d (side blocks: x read and written, q p's read "
-                                  "for 1/q of the rows)" % q if xside else ""),
+                                  "for 1/q of the rows)" % q if xside else "") +
+                                 (" + 24 B per row (fused update blocks: r and Ap read, r written)" if fupd else ""),
                 "credited_bytes_per_launch": credited,
                 "credited_frac": round(credited / spmv_avg_s / 1e9 / HBM_PEAK_GBS, 4),
                 "credited_formula": "SURVEY 8(d): 12 nnz + 20 n (SpMV) + 16 n (ddot p.Ap)" +
@@ -381,7 +387,8 @@ def main():
                 "avg_launch_us": round(spmv_avg_s * 1e6, 2),
                 "timing": timing_src,
             },
-            "update_kernel_avg_us": round(upd_ms / upd_n * 1e3, 2) if upd_n else None,
+            # fused update: no update launch (its work is inside the SpMV launch above)
+            "update_kernel_avg_us": round(upd_ms / upd_n * 1e3, 2) if (upd_n and not fupd) else None,
             "check": {"x_minus_xexact_inf": chk[0].item(), "final_normr_over_initial": chk[1].item(),
                       "niters_per_solve": it},
             # per-solve wall times on rank 0 (first/cold and median of the solves);

@@ -96,6 +96,11 @@ struct CgArgs {
     int slots;                    // folded dots complete through self-validating slots (launch covers all units)
     int a2_ring;                  // pair kernel: value slots in flight per wave through its LDS-DMA ring (0: register loads)
     int xside;                    // x_defer 2: this SpMV launch carries the side-flush blocks
+    int fupd;                     // fused update: the SpMV launch's trailing blocks run the update (one rank,
+                                  // direct kernel); k lives in kst[0] / kst[2] by parity (kpar)
+    int kpar;                     // fused update: parity of the iteration this launch runs
+    int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
+    double* pready;               // fused update: self-validating slot of the p.Ap total
 };
 
 // Is dot `which` (kRR / kPAP) completed inside its producing kernel?

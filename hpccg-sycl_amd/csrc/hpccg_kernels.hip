@@ -379,7 +379,13 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
 {
     a.loc[which] = s;
     if (!a.allreduce) a.g[which] = s;
-    if (which == kRR) a.kst[0] = k + 1;
+    if (which == kRR) a.kst[a.fupd && ((k + 1) & 1) ? 2 : 0] = k + 1;
+    if (a.fupd) {
+        if (which == kPAP)
+            st_sc1(a.pready, s);  // the launch's update blocks wait for it
+        else
+            st_sc1(a.pready, slot_empty());  // every update block has read it
+    }
     if (stamp_fin) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
     // the local sum is done, the all-reduce comes next (t4 class)
     if (a.allreduce) stamp(a, k, which == kRR ? kStampArRR : kStampArPAP);
@@ -499,6 +505,22 @@ __device__ __forceinline__ bool iter_of(const CgArgs& a, int& k)
     return v.y != 0;
 }
 
+// The iteration a launch runs. Fused update (a.fupd): the launch's own r.r
+// completion writes the next k, so k is kept in two slots by parity (kst[0]
+// even, kst[2] odd; a.kpar from the host's count): no block of a launch can
+// read the value its launch writes. kst[1] (end stamped) makes every later
+// launch a no-op (max_iter fails the loop test).
+template <bool kFU>
+__device__ __forceinline__ int iter_k(const CgArgs& a)
+{
+    if constexpr (!kFU) {
+        return a.kst[0];
+    } else {
+        if (a.kst[1]) return a.max_iter;
+        return a.kst[a.kpar ? 2 : 0];
+    }
+}
+
 // Iteration state every SpMV kernel reads first: k, and for the fused p update
 // r_{k-1}.r_{k-1} and beta. Returns false when the solve has ended.
 struct IterState {
@@ -507,14 +529,14 @@ struct IterState {
     double beta;
 };
 
-template <bool kFuse>
+template <bool kFuse, bool kFU = false>
 __device__ __forceinline__ bool spmv_begin(const CgArgs& a, bool prologue, IterState& st)
 {
     st.k = 0;
     st.rr = 0.0;
     st.beta = 0.0;
     if (prologue) return true;
-    st.k = a.kst[0];
+    st.k = iter_k<kFU>(a);
     if (kFuse) st.rr = a.g[kRR];
     const bool run = cg_run(a, st.k, kFuse, st.rr);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -641,11 +663,19 @@ __device__ __forceinline__ int unit_of(const CgArgs& a)
 // deferred x and the next iteration); the rows' p.Ap terms in order.
 // pk (optional): the rows' p_k as the caller already holds it (the pair
 // kernel's staged window; fused, the same expression, so the same bits).
-template <bool kFuse>
+template <bool kFuse, bool kFU = false>
 __device__ __forceinline__ double spmv_rows_out(const CgArgs& a, const IterState& st, bool prologue, int row,
                                                 const double (&sum)[kRpt], const Rows* pk = nullptr)
 {
-    st_vec(a, a.Ap, row, Rows{{sum[0], sum[1]}});
+    if (kFU) {  // read by this launch's update blocks on any XCD: write-through
+        // one 16-B sc1 store (rows past n are padding; their holes sum to 0);
+        // inline asm: the agent-scope atomic stores of st_sc1 made the
+        // compiler hoist the unrolled slot loop's loads (255 VGPRs)
+        const d2v v = {sum[0], sum[1]};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(a.Ap + row), "v"(v));
+    } else {
+        st_vec(a, a.Ap, row, Rows{{sum[0], sum[1]}});
+    }
     if (prologue) return 0.0;  // HPCCG.cpp:351: the prologue SpMV has no p.Ap
     double* __restrict__ p = cur_p(a, st.k);
     Rows pv;
@@ -696,12 +726,12 @@ __host__ __device__ constexpr int side_blocks(int nslices, int nring, int spu)
     return ((nslices + nring - 2) / (nring - 1) + spu - 1) / spu;
 }
 
-template <int kSpu, int kB>
+template <int kSpu, int kB, bool kFU = false>
 __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
 {
-    if ((int)blockIdx.x < a.sgrid) return false;
+    if ((int)blockIdx.x < a.sgrid || (kFU && (int)blockIdx.x >= a.ubase)) return false;
     if (prologue) return true;
-    const int k = a.kst[0];
+    const int k = iter_k<kFU>(a);
     if (k < 2 || !cg_run(a, k, false)) return true;
     const int q = a.nring - 1;
     const int s = k % q + q * (kSpu * ((int)blockIdx.x - a.sgrid) + (int)threadIdx.x / kBlock);
@@ -728,6 +758,59 @@ __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
         __builtin_nontemporal_store(d2v{xn.v[0], xn.v[1]}, reinterpret_cast<d2v*>(a.x + row));
     else
         st_rows(a.x, row, a.n, xn);
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Fused update (a.fupd; one rank, direct kernel): the SpMV launch of iteration
+// k ends with a.grid update blocks (index >= a.ubase, dispatched after every
+// unit and side block) that do k_update's work -- r = r - alpha Ap and the r.r
+// partial (HPCCG.cpp:382-384, 367), the same expressions in the same order --
+// once the launch's p.Ap total is in its self-validating slot (a.pready).
+// Every unit block is dispatched before them and none waits on them, so the
+// wait ends. Ap comes from this launch's unit blocks on any XCD: stored
+// write-through, drained before their partials are published, read with
+// agent-scope loads. r is prefetched before the wait. Saves the update's
+// launch and ramp; bitwise the unfused iteration.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue)
+{
+    if ((int)blockIdx.x < a.ubase) return false;
+    if (prologue) return true;
+    const int k = iter_k<true>(a);
+    const double rr = a.g[kRR];  // r_{k-1}.r_{k-1}: the previous launch's
+    if (!cg_run(a, k, true, rr)) return true;
+    const int bl = (int)blockIdx.x - a.ubase;  // a.ubase is a multiple of kNumXcd
+    const int per = a.grid / kNumXcd;
+    const int s = (bl % kNumXcd) * per + (a.rev ? per - 1 - bl / kNumXcd : bl / kNumXcd);
+    if (s >= a.nslices) return true;
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    const Rows rv = ld(a.r + row);
+    __shared__ double pap_s;
+    if (threadIdx.x == 0) {  // one poller per block
+        double v;
+        while (!slot_full(v = ld_sc1(a.pready))) __builtin_amdgcn_s_sleep(8);
+        pap_s = v;
+    }
+    __syncthreads();
+    const double alpha = rr / pap_s;
+    if (bl == 0 && threadIdx.x == 0) {
+        a.ahist[k] = alpha;
+        stamp(a, k, kStampUpdate);
+    }
+    Rows apv;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) apv.v[i] = ld_sc1(a.Ap + row + i);
+    Rows rn;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
+    st_vec(a, a.r, row, rn);
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++)
+        if (row + i < a.n) d += rn.v[i] * rn.v[i];
+    const double bs = block_sum<kBlock>(d);
+    complete_dot(a, update_units(a), s, s, bs, kRR, k);
     return true;
 }
 
@@ -784,7 +867,7 @@ __host__ __device__ constexpr int tri_groups(int w) { return w == 7 ? 5 : 0; }
 __host__ __device__ constexpr int tri_first(int w, int g) { return g <= 2 ? g : g + 2; }
 __host__ __device__ constexpr int tri_size(int w, int g) { return g == 2 ? 3 : 1; }
 
-template <int kW, bool kNT, bool kFuse, int kPre, bool kTri = false>
+template <int kW, bool kNT, bool kFuse, int kPre, bool kTri = false, bool kFU = false>
 __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 {
     static_assert(kPre == 0 || (kW > 0 && kPre <= kW), "early loads need the uniform width");
@@ -801,9 +884,12 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
             for (int j = 0; j < kW; j++) offp[j] = a.aoff[(size_t)s * kAMax + j];
         }
     }
-    if (side_flush<1, kW == 7 ? 8 : 4>(a, prologue)) return;
+    if constexpr (kFU) {
+        if (fused_update(a, prologue)) return;
+    }
+    if (side_flush<1, kW == 7 ? 8 : 4, kFU>(a, prologue)) return;
     IterState st;
-    if (!spmv_begin<kFuse>(a, prologue, st)) return;
+    if (!spmv_begin<kFuse, kFU>(a, prologue, st)) return;
     if (s < 0) return;
     const int wdt = kW > 0 ? kW : (int)(a.abase[s + 1] - a.abase[s]);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
@@ -859,7 +945,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
                     triple(val(j0), val(j0 + 1), val(j0 + 2), offp[j0 + 1]);
                 }
             }
-            const double d = spmv_rows_out<kFuse>(a, st, prologue, row, sum);
+            const double d = spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
             if (prologue) return;
             const double bs = block_sum<kBlock>(d);
             complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
@@ -889,7 +975,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 #pragma unroll
         for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xv.v[i];
     }
-    const double d = spmv_rows_out<kFuse>(a, st, prologue, row, sum);
+    const double d = spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
     if (prologue) return;
     const double bs = block_sum<kBlock>(d);
     complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
@@ -1451,7 +1537,7 @@ __global__ void k_end(CgArgs a) { mark_end(a); }
 __global__ __launch_bounds__(kBlock) void k_xflush(CgArgs a)
 {
     if (!a.xdefer) return;
-    const int niters = a.kst[0] - 1;
+    const int niters = (a.fupd ? max(a.kst[0], a.kst[2]) : a.kst[0]) - 1;
     const int s = xcd_slice(a.grid);
     if (s >= a.nslices) return;
     // the last term already applied to this slice's x (0: none)
@@ -1743,17 +1829,27 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     const bool side = !prologue && a.xdefer == 2 && a.xside &&
                       ((kernel == kSpmvPairs && a.a2_ring > 0) || kernel == kSpmvDirect);
     const int spu = kernel == kSpmvPairs ? 2 : 1;
-    const dim3 sg(a.sgrid + (side ? side_blocks(a.nslices, a.nring, spu) : 0));
+    const int nside = side ? side_blocks(a.nslices, a.nring, spu) : 0;
+    // fused update: a.grid update blocks after the side blocks, from a block
+    // index that is a multiple of kNumXcd (their XCD-aware slice order)
+    const bool fu = !prologue && a.fupd && kernel == kSpmvDirect && fuse;
+    CgArgs b = a;
+    b.ubase = fu ? (a.sgrid + nside + kNumXcd - 1) / kNumXcd * kNumXcd : 0;
+    const dim3 sg(fu ? b.ubase + a.grid : a.sgrid + nside);
 #define HPCCG_A(W, NT, PRE)                                                                                       \
     do {                                                                                                          \
-        if (a.atri && tri_groups(W) > 0 && PRE > 0 && fuse)                                                     \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE, true>), sg, dim3(kBlock), 0, s, a, prologue); \
+        if (fu && a.atri && tri_groups(W) > 0 && PRE > 0)                                                       \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE, true, true>), sg, dim3(kBlock), 0, s, b, prologue); \
+        else if (fu)                                                                                              \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE, false, true>), sg, dim3(kBlock), 0, s, b, prologue); \
+        else if (a.atri && tri_groups(W) > 0 && PRE > 0 && fuse)                                                \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE, true>), sg, dim3(kBlock), 0, s, b, prologue); \
         else if (a.atri && tri_groups(W) > 0 && PRE > 0)                                                        \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE, true>), sg, dim3(kBlock), 0, s, a, prologue); \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE, true>), sg, dim3(kBlock), 0, s, b, prologue); \
         else if (fuse)                                                                                            \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE>), sg, dim3(kBlock), 0, s, a, prologue);       \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, true, PRE>), sg, dim3(kBlock), 0, s, b, prologue);       \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE>), sg, dim3(kBlock), 0, s, a, prologue);      \
+            hipLaunchKernelGGL((k_spmv_a<W, NT, false, PRE>), sg, dim3(kBlock), 0, s, b, prologue);      \
     } while (0)
     switch (kernel) {
     case kSpmvPairs: {

@@ -120,6 +120,8 @@ def main():
         launches = len(fetch[(kname, "FETCH_SIZE")])
         side = (16.0 + 8.0 * q) / q * nrow * (launches - 1) / launches
         compulsory += side
+    upd = 24.0 * nrow if opts.get("fuse_update") == 1 else 0.0  # fused update blocks: r, Ap read; r written
+    compulsory += upd
 
     avg_ns = None
     calls = -1
@@ -138,6 +140,8 @@ def main():
         "format_compulsory_bytes_per_launch": compulsory,
         "x_defer": opts.get("x_defer"),
         "side_flush_bytes_per_launch": side,
+        "fuse_update": opts.get("fuse_update", 0),
+        "fused_update_bytes_per_launch": upd,
         "fetch_size_kib_raw": f_spmv,
         "write_size_kib_raw": w_spmv,
         "fetch_calibration": {"kernel": "k_stream_a", "known_read_bytes": stream_read,
