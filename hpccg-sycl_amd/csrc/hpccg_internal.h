@@ -13,6 +13,7 @@ namespace hpccg {
 // (deterministic sums).
 constexpr int kSliceRows = 512;
 constexpr int kNumXcd = 8;  // MI355X: 8 XCDs, blocks dealt round-robin
+constexpr int kReadyStride = 16;  // doubles between the fused update's p.Ap ready slots (128 B)
 
 // Indices into the device scalar block.
 enum Scalar : int { kRR = 0, kPAP = 1 };
@@ -100,7 +101,7 @@ struct CgArgs {
                                   // direct kernel); k lives in kst[0] / kst[2] by parity (kpar)
     int kpar;                     // fused update: parity of the iteration this launch runs
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
-    double* pready;               // fused update: self-validating slot of the p.Ap total
+    double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
 };
 
 // Is dot `which` (kRR / kPAP) completed inside its producing kernel?

@@ -380,11 +380,10 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
     a.loc[which] = s;
     if (!a.allreduce) a.g[which] = s;
     if (which == kRR) a.kst[a.fupd && ((k + 1) & 1) ? 2 : 0] = k + 1;
-    if (a.fupd) {
-        if (which == kPAP)
-            st_sc1(a.pready, s);  // the launch's update blocks wait for it
-        else
-            st_sc1(a.pready, slot_empty());  // every update block has read it
+    if (a.fupd) {  // one copy per XCD group of update blocks, 128 B apart (no single hot line)
+        for (int j = 0; j < kNumXcd; j++)
+            st_sc1(a.pready + kReadyStride * j, which == kPAP ? s : slot_empty());  // p.Ap: the update blocks
+                                                                                       // wait for it; r.r: all read it
     }
     if (stamp_fin) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
     // the local sum is done, the all-reduce comes next (t4 class)
@@ -789,7 +788,8 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue)
     __shared__ double pap_s;
     if (threadIdx.x == 0) {  // one poller per block
         double v;
-        while (!slot_full(v = ld_sc1(a.pready))) __builtin_amdgcn_s_sleep(8);
+        const double* slot = a.pready + kReadyStride * (bl % kNumXcd);
+        while (!slot_full(v = ld_sc1(slot))) __builtin_amdgcn_s_sleep(8);
         pap_s = v;
     }
     __syncthreads();

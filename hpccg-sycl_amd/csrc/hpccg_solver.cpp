@@ -902,7 +902,7 @@ int alloc_workspace(hpccg_hip_matrix* M)
     TRY(dev_alloc(M, &M->d_b, M->npad, true));
     const int ngroups = (M->nslices + 63) / 64;  // kGroup in hpccg_kernels.hip
     {
-        const size_t np = 2 * (size_t)std::max(1, M->nslices) + 2 * ngroups + 8;
+        const size_t np = 2 * (size_t)std::max(1, M->nslices) + 2 * ngroups + 8 + kNumXcd * kReadyStride;
         M->npartial = np;
         TRY(dev_alloc(M, &M->d_partial, np));
         const std::vector<unsigned long long> empty(np, kSlotEmpty);  // every dot slot starts empty
@@ -959,8 +959,8 @@ int x_defer_effective(const hpccg_hip_matrix* M)
 // Fused update: one rank (no all-reduce between p.Ap and the update), the
 // direct kernel with the p update fused, both dots completed in-kernel
 // through slots, x deferred beside the SpMV. Auto: where the image fits the
-// Infinity Cache (same-process A/B, 100^3: 20 354 vs 19 753 CG it/s; 7-pt
-// 256^3, beyond it: 2681 vs 2803 -- the write-through Ap and its agent-scope
+// Infinity Cache (same-process A/B, 100^3: 20 286 vs 19 505 CG it/s; 7-pt
+// 256^3, beyond it: 2825 vs 2896 -- the write-through Ap and its agent-scope
 // reads cost more than the launch they save).
 bool image_big(const hpccg_hip_matrix* M);
 bool fuse_update_effective(const hpccg_hip_matrix* M)
@@ -991,7 +991,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.xdefer = x_defer_effective(M);
     a.xside = 1;
     a.fupd = fuse_update_effective(M) ? 1 : 0;
-    a.pready = M->d_partial + (M->npartial - 1);
+    a.pready = M->d_partial + (M->npartial - kNumXcd * kReadyStride);
     a.rev = M->rev_update ? 1 : 0;
     a.nring = a.xdefer ? x_ring_effective(M) : (a.fuse_p ? 2 : 1);
     const int units = M->kernel == kSpmvPairs ? (M->nslices + 1) / 2 : M->nslices;
