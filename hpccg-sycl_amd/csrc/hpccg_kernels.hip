@@ -671,7 +671,10 @@ __device__ __forceinline__ double spmv_rows_out(const CgArgs& a, const IterState
         // inline asm: the agent-scope atomic stores of st_sc1 made the
         // compiler hoist the unrolled slot loop's loads (255 VGPRs)
         const d2v v = {sum[0], sum[1]};
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(a.Ap + row), "v"(v));
+        if (a.nt_store)  // streamed once: keep it out of the L2 the x reads live on
+            asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" : : "v"(a.Ap + row), "v"(v));
+        else
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(a.Ap + row), "v"(v));
     } else {
         st_vec(a, a.Ap, row, Rows{{sum[0], sum[1]}});
     }
@@ -798,9 +801,11 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue)
         a.ahist[k] = alpha;
         stamp(a, k, kStampUpdate);
     }
-    Rows apv;
-#pragma unroll
-    for (int i = 0; i < kRpt; i++) apv.v[i] = ld_sc1(a.Ap + row + i);
+    // one 16-B agent-coherent load (sc1: not served by a stale L2 line); the
+    // compiler does not count an asm load, so its wait is explicit
+    d2v apw;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(apw) : "v"(a.Ap + row) : "memory");
+    const Rows apv{{apw.x, apw.y}};
     Rows rn;
 #pragma unroll
     for (int i = 0; i < kRpt; i++) rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];

@@ -959,8 +959,8 @@ int x_defer_effective(const hpccg_hip_matrix* M)
 // Fused update: one rank (no all-reduce between p.Ap and the update), the
 // direct kernel with the p update fused, both dots completed in-kernel
 // through slots, x deferred beside the SpMV. Auto: where the image fits the
-// Infinity Cache (same-process A/B, 100^3: 20 286 vs 19 505 CG it/s; 7-pt
-// 256^3, beyond it: 2825 vs 2896 -- the write-through Ap and its agent-scope
+// Infinity Cache (same-process A/B, 100^3: 21 145 vs 20 380 CG it/s; 7-pt
+// 256^3, beyond it: 2772 vs 2812 -- the write-through Ap and its agent-scope
 // reads cost more than the launch they save).
 bool image_big(const hpccg_hip_matrix* M);
 bool fuse_update_effective(const hpccg_hip_matrix* M)
