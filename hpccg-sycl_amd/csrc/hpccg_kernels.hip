@@ -768,12 +768,13 @@ __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
 // k ends with a.grid update blocks (index >= a.ubase, dispatched after every
 // unit and side block) that do k_update's work -- r = r - alpha Ap and the r.r
 // partial (HPCCG.cpp:382-384, 367), the same expressions in the same order --
-// once the launch's p.Ap total is in its self-validating slot (a.pready).
-// Every unit block is dispatched before them and none waits on them, so the
-// wait ends. Ap comes from this launch's unit blocks on any XCD: stored
-// write-through, drained before their partials are published, read with
-// agent-scope loads. r is prefetched before the wait. Saves the update's
-// launch and ramp; bitwise the unfused iteration.
+// once the launch's p.Ap total is in its self-validating slots (a.pready:
+// kNumXcd copies 128 B apart, block b polls copy b mod kNumXcd, so no single
+// line takes every poll). Every unit block is dispatched before them and none
+// waits on them, so the wait ends. Ap comes from this launch's unit blocks on
+// any XCD: stored write-through, drained before their partials are
+// published, read with agent-scope loads. r is prefetched before the wait.
+// Saves the update's launch and ramp; bitwise the unfused iteration.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue)
 {
