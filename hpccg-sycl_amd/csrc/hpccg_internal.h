@@ -100,6 +100,7 @@ struct CgArgs {
     int fupd;                     // fused update: the SpMV launch's trailing blocks run the update (one rank,
                                   // direct kernel); k lives in kst[0] / kst[2] by parity (kpar)
     int kpar;                     // fused update: parity of the iteration this launch runs
+    int fu2;                      // fused update: two slices per update block (four rows per thread)
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
 };

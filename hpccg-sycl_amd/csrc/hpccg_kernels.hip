@@ -784,11 +784,17 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue)
     const double rr = a.g[kRR];  // r_{k-1}.r_{k-1}: the previous launch's
     if (!cg_run(a, k, true, rr)) return true;
     const int bl = (int)blockIdx.x - a.ubase;  // a.ubase is a multiple of kNumXcd
-    const int per = a.grid / kNumXcd;
-    const int s = (bl % kNumXcd) * per + (a.rev ? per - 1 - bl / kNumXcd : bl / kNumXcd);
-    if (s >= a.nslices) return true;
+    const int spu = a.fu2 ? 2 : 1;
+    const int units = (a.nslices + spu - 1) / spu;
+    const int ugrid = (units + kNumXcd - 1) / kNumXcd * kNumXcd;
+    const int per = ugrid / kNumXcd;
+    const int u = (bl % kNumXcd) * per + (a.rev ? per - 1 - bl / kNumXcd : bl / kNumXcd);
+    if (u >= units) return true;
+    const int s = u * spu;  // first slice of the unit
+    const int nsl = min(spu, a.nslices - s);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     const Rows rv = ld(a.r + row);
+    const Rows rv2 = nsl > 1 ? ld(a.r + row + kSliceRows) : Rows{{0.0, 0.0}};
     __shared__ double pap_s;
     if (threadIdx.x == 0) {  // one poller per block
         double v;
@@ -804,19 +810,42 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue)
     }
     // one 16-B agent-coherent load (sc1: not served by a stale L2 line); the
     // compiler does not count an asm load, so its wait is explicit
-    d2v apw;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(apw) : "v"(a.Ap + row) : "memory");
-    const Rows apv{{apw.x, apw.y}};
-    Rows rn;
+    d2v apw, apw2 = {0.0, 0.0};
+    if (nsl > 1)
+        asm volatile("global_load_dwordx4 %0, %2, off sc1\n\tglobal_load_dwordx4 %1, %3, off sc1\n\t"
+                     "s_waitcnt vmcnt(0)"
+                     : "=&v"(apw), "=&v"(apw2) : "v"(a.Ap + row), "v"(a.Ap + row + kSliceRows) : "memory");
+    else
+        asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(apw) : "v"(a.Ap + row) : "memory");
+    // each slice exactly as k_update forms it: r, its partial with block_sum<256>'s shape
+    // (wave sums, then the four in wave order), both slices through one barrier
+    auto slice = [&](const Rows& r_, const d2v& ap_, int rw) -> double {
+        Rows rn;
+        rn.v[0] = r_.v[0] + (-alpha) * ap_.x;
+        rn.v[1] = r_.v[1] + (-alpha) * ap_.y;
+        st_vec(a, a.r, rw, rn);
+        double d = 0.0;
 #pragma unroll
-    for (int i = 0; i < kRpt; i++) rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
-    st_vec(a, a.r, row, rn);
-    double d = 0.0;
+        for (int i = 0; i < kRpt; i++)
+            if (rw + i < a.n) d += rn.v[i] * rn.v[i];
+        return wave_sum(d);
+    };
+    __shared__ double ws2[2][kBlock / kWave];
+    const double wa = slice(rv, apw, row);
+    const double wb = nsl > 1 ? slice(rv2, apw2, row + kSliceRows) : 0.0;
+    const int lane = threadIdx.x & (kWave - 1);
+    if (lane == 0) {
+        ws2[0][threadIdx.x / kWave] = wa;
+        ws2[1][threadIdx.x / kWave] = wb;
+    }
+    __syncthreads();
+    if (threadIdx.x >= kWave) return true;
+    double bsj = 0.0;  // lane j: slice s + j's partial
+    if (lane < 2) {
 #pragma unroll
-    for (int i = 0; i < kRpt; i++)
-        if (row + i < a.n) d += rn.v[i] * rn.v[i];
-    const double bs = block_sum<kBlock>(d);
-    complete_dot(a, update_units(a), s, s, bs, kRR, k);
+        for (int i = 0; i < kBlock / kWave; i++) bsj += ws2[lane][i];
+    }
+    complete_dot_lanes(a, UnitMap{units, per, spu, a.rev != 0}, u, s, nsl, bsj, kRR, k);
     return true;
 }
 
@@ -1841,7 +1870,9 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     const bool fu = !prologue && a.fupd && kernel == kSpmvDirect && fuse;
     CgArgs b = a;
     b.ubase = fu ? (a.sgrid + nside + kNumXcd - 1) / kNumXcd * kNumXcd : 0;
-    const dim3 sg(fu ? b.ubase + a.grid : a.sgrid + nside);
+    // update units: one slice per block, or two (a.fu2: four rows per thread)
+    const int ugrid = a.fu2 ? (((a.nslices + 1) / 2 + kNumXcd - 1) / kNumXcd * kNumXcd) : a.grid;
+    const dim3 sg(fu ? b.ubase + ugrid : a.sgrid + nside);
 #define HPCCG_A(W, NT, PRE)                                                                                       \
     do {                                                                                                          \
         if (fu && a.atri && tri_groups(W) > 0 && PRE > 0)                                                       \

@@ -217,6 +217,7 @@ struct hpccg_hip_matrix {
     int use_graph = 1;
     int fuse_p = -1;      // -1 auto: on where the kernel forms p_k itself
     int fuse_update = -1; // the update as trailing blocks of the SpMV launch; -1 auto (fuse_update_effective)
+    int fused_update_slices = 2;  // slices per update block of the fused update (1 or 2)
     size_t npartial = 0;  // dot slots (the last one: the fused update's p.Ap total)
     int a_pre = -1;       // direct kernel prefetch depth (-1 auto: 4 at width 27, 7 at width 7)
     int lds_ep = 1;       // pair kernel: own p_k from the staged window
@@ -958,14 +959,14 @@ int x_defer_effective(const hpccg_hip_matrix* M)
 
 // Fused update: one rank (no all-reduce between p.Ap and the update), the
 // direct kernel with the p update fused, both dots completed in-kernel
-// through slots, x deferred beside the SpMV. Auto: where the image fits the
-// Infinity Cache (same-process A/B, 100^3: 21 145 vs 20 380 CG it/s; 7-pt
-// 256^3, beyond it: 2772 vs 2812 -- the write-through Ap and its agent-scope
-// reads cost more than the launch they save).
-bool image_big(const hpccg_hip_matrix* M);
+// through slots, x deferred beside the SpMV. On by default: same-process
+// A/B with two slices per update block (fused_update_slices 2), 100^3
+// 21 485 vs 20 261 CG it/s, 7-pt 256^3 2838 vs 2807 (one slice per update
+// block: 20 865 / 2748 -- the update blocks inherit the SpMV's occupancy, so
+// each needs more rows in flight).
 bool fuse_update_effective(const hpccg_hip_matrix* M)
 {
-    const bool want = M->fuse_update < 0 ? !image_big(M) : M->fuse_update != 0;
+    const bool want = M->fuse_update != 0;
     return want && M->nranks == 1 && !M->in_group && !M->force_comm && M->kernel == kSpmvDirect &&
            fuse_p_effective(M) && fold_effective(M) == 1 && x_defer_effective(M) == 2;
 }
@@ -991,6 +992,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.xdefer = x_defer_effective(M);
     a.xside = 1;
     a.fupd = fuse_update_effective(M) ? 1 : 0;
+    a.fu2 = M->fused_update_slices == 2 ? 1 : 0;
     a.pready = M->d_partial + (M->npartial - kNumXcd * kReadyStride);
     a.rev = M->rev_update ? 1 : 0;
     a.nring = a.xdefer ? x_ring_effective(M) : (a.fuse_p ? 2 : 1);
@@ -2345,6 +2347,9 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
                 return rc;
             }
         }
+    } else if (!std::strcmp(key, "fused_update_slices")) {
+        if (value != 1 && value != 2) return set_err(HPCCG_HIP_EINVAL, "fused_update_slices must be 1 or 2");
+        M->fused_update_slices = (int)value;
     } else if (!std::strcmp(key, "fuse_update")) {
         M->fuse_update = value < 0 ? -1 : (value ? 1 : 0);
     } else if (!std::strcmp(key, "rev_update")) {
@@ -2403,6 +2408,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "x_ring")) *value = x_ring_effective(M);
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "fuse_update")) *value = fuse_update_effective(M) ? 1 : 0;
+    else if (!std::strcmp(key, "fused_update_slices")) *value = M->fused_update_slices;
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
     else if (!std::strcmp(key, "graph_chunk")) *value = M->graph_iters;
     else if (!std::strcmp(key, "graph_used")) *value = M->graph_used;

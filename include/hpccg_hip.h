@@ -147,10 +147,10 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *   "fold"          dots completed inside the producing kernel (self-validating
  *                   slots; tickets on unit-subset launches): 0 neither
  *                   (k_finalize), 1 both (auto), 2 p.Ap only, 3 r.r only
- *   "fuse_update"   -1 auto (on where the matrix image fits the Infinity
- *                   Cache) / 0 / 1: one rank, direct kernel: the update runs
- *                   as trailing blocks of the SpMV launch (one launch per
+ *   "fuse_update"   -1 auto (on) / 0 / 1: one rank, direct kernel: the update
+ *                   runs as trailing blocks of the SpMV launch (one launch per
  *                   iteration; same bits)
+ *   "fused_update_slices"  1 or 2 (default): slices per fused update block
  *   "x_defer"       x += alpha p deferred over the p ring: 1 = every x_ring-th
  *                   update applies it to all rows; 2 (default) = trailing blocks
  *                   of every SpMV launch apply it to the 1/(x_ring-1) of the

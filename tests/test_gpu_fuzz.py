@@ -35,6 +35,7 @@ OPTIONS = {
     "rev_update": (0, 1),
     "nt_store": (0, 1, -1),
     "fuse_update": (0, 1),
+    "fused_update_slices": (1, 2),
 }
 
 

@@ -143,16 +143,18 @@ def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
     # the update as trailing blocks of the direct kernel's launch (fused update)
     M.set_option("x_ring", -1)
     M.set_option("a_pre", -1)
-    for graph, chunk, tri in ((1, 32, 1), (0, 8, 1), (1, 7, 0), (1, 3, 1)):
+    for graph, chunk, tri, spu in ((1, 32, 1, 1), (0, 8, 1, 2), (1, 7, 0, 1), (1, 3, 1, 2), (0, 32, 0, 2)):
         M.set_option("fuse_p", -1)
         M.set_option("fold", 1)
         M.set_option("use_graph", graph)
         M.set_option("graph_chunk", chunk)
         M.set_option("tri", tri)
         M.set_option("fuse_update", 1)
+        M.set_option("fused_update_slices", spu)
         assert M.get_option("fuse_update") == 1
-        out[("fused-update", graph, chunk, tri)] = solve_bits(hp, M, prob.b, 120)
+        out[("fused-update", graph, chunk, tri, spu)] = solve_bits(hp, M, prob.b, 120)
     M.set_option("fuse_update", 0)
+    M.set_option("fused_update_slices", 1)
     M.set_option("graph_chunk", 32)
     M.set_option("spmv_kernel", SELL)
     assert M.get_option("x_defer") == 1
