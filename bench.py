@@ -29,9 +29,18 @@ roofline (the SpMV kernel, 84 % of the reference's time):
   (profiles/pmc_spmv_<stencil>pt_<n>.json), or null. credited_frac keeps
   SURVEY 8(d)'s fixed formula (12 nnz + 20 n SpMV + ddot/waxpby bytes the
   fused kernel absorbs), which can pass 1.0 because the format moves less.
-cpu_baseline: the reference compiled from its own sources (oracle/_ref:
-  OpenMP build with the host's threads, and the serial build) on a bounded
-  sample of the same problem, rank 0, N = 1 only.
+cpu_baseline: the reference compiled from its own sources (oracle/_ref) on
+  a bounded sample of the same problem, rank 0, N = 1 only, three legs: the
+  OpenMP build with one thread per physical core of this process's CPU mask
+  (the full-host bar, the headline value), the OpenMP build with the box's
+  thread share (OMP_NUM_THREADS), and the serial build.
+
+Multi-GPU runs describe themselves: every rank logs its stages on stderr
+(comm init, setup, first solve, timed steps), the line carries what RCCL
+reports (ncclCommCount, versions, the loaded RCCL / HIP objects, every rank's
+PCI bus id) and the per-iteration halo / all-reduce time, and a watchdog ends
+a rank (exit 124) whose run outlives --timeout; the parent that starts
+torch.distributed.run kills the job at the same limit.
 """
 from __future__ import annotations
 
@@ -97,29 +106,51 @@ def host_cpu():
     return info
 
 
-def cpu_baseline(nx, ny, nz, use_7pt, budget_s=30.0, budget_1t_s=15.0):
+def physical_cores():
+    """Physical cores (distinct package/core ids) among this process's CPUs."""
+    cores = set()
+    for c in os.sched_getaffinity(0):
+        t = f"/sys/devices/system/cpu/cpu{c}/topology"
+        try:
+            with open(f"{t}/physical_package_id") as f1, open(f"{t}/core_id") as f2:
+                cores.add((f1.read().strip(), f2.read().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    return len(cores)
+
+
+def cpu_baseline(nx, ny, nz, use_7pt, budget_s=15.0, budget_1t_s=10.0):
     """The reference (oracle/_ref: its own sources compiled in this repo's
     recipe) on the host cores, bounded: the first iterations of one HPCCG()
-    solve of the same matrix, OpenMP with the host's threads and serial."""
+    solve of the same matrix; OpenMP with one thread per physical core of the
+    process's CPU mask (full host), OpenMP with the box's thread share, serial."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
     import oracle  # test infrastructure: baseline leg only
-    threads = int(os.environ["OMP_NUM_THREADS"])
+    share = int(os.environ["OMP_NUM_THREADS"])
+    phys = physical_cores()
     A = oracle.generate(nx, ny, nz, use_7pt=use_7pt)
     out = {"unit": "CG iterations/s", "host": host_cpu()}
+    out["host"]["physical_cores_in_affinity"] = phys
     legs = []
     if os.path.exists(oracle.REF_OMP_SO):
-        legs.append(("omp", threads, budget_s))
+        legs.append(("full_host", phys, budget_s))
+        if share != phys:
+            legs.append(("box_share", share, budget_s))
     if os.path.exists(oracle.REF_SO):
         legs.append(("serial", 1, budget_1t_s))
     if not legs:
         raise RuntimeError("oracle/_ref is not built (make -C oracle ref)")
+    gomp = ctypes.CDLL("libgomp.so.1") if os.path.exists(oracle.REF_OMP_SO) else None  # the ref build's runtime
     # the reference prints residual lines on fd 1: keep bench stdout to one JSON line
     saved = os.dup(1)
     null = os.open(os.devnull, os.O_WRONLY)
     os.dup2(null, 1)
     try:
         for leg, nthreads, budget in legs:
-            M = oracle.ref_from_csr(A, omp=(leg == "omp"))
+            if leg != "serial":
+                gomp.omp_set_num_threads(nthreads)
+            M = oracle.ref_from_csr(A, omp=(leg != "serial"))
             probe = 3
             t = oracle.ref_hpccg(M, A.b, max_iter=probe + 1)["times"][0]
             per_it = max(t / probe, 1e-6)
@@ -129,21 +160,23 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=30.0, budget_1t_s=15.0):
             its = res["niters"] / res["times"][0]
             sample = (f"{nx}x{ny}x{nz} {'7' if use_7pt else '27'}-pt, first {res['niters']} CG iterations of one "
                       f"reference HPCCG() solve ({res['times'][0]:.1f} s)")
-            if leg == "omp":
-                out.update({"value": its, "cores": nthreads, "kind": "reference",
-                            "sample": sample + f", OpenMP {nthreads} threads (OMP_PROC_BIND="
-                                                f"{os.environ.get('OMP_PROC_BIND')}, OMP_PLACES="
-                                                f"{os.environ.get('OMP_PLACES')})"})
-            else:
-                out["single_thread"] = {"value": its, "cores": 1, "kind": "reference", "sample": sample + ", serial"}
+            desc = (f", OpenMP {nthreads} threads (OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
+                    f"OMP_PLACES={os.environ.get('OMP_PLACES')})" if leg != "serial" else ", serial")
+            out.setdefault("legs", {})[leg] = {"value": its, "threads": nthreads, "physical_cores": phys,
+                                               "kind": "reference", "sample": sample + desc}
+            if leg == "serial":
+                out["single_thread"] = {"value": its, "cores": 1, "kind": "reference", "sample": sample + desc}
     finally:
         import ctypes
         ctypes.CDLL(None).fflush(None)
         os.dup2(saved, 1)
         os.close(null)
         os.close(saved)
-    if "value" not in out:  # only the serial build
-        out.update({k: out["single_thread"][k] for k in ("value", "cores", "kind", "sample")})
+    # headline: the fastest leg (the strongest CPU bar on this host)
+    best_leg = max(out["legs"], key=lambda k: out["legs"][k]["value"])
+    best = out["legs"][best_leg]
+    out.update({"value": best["value"], "cores": best["threads"], "threads": best["threads"],
+                "physical_cores": phys, "kind": "reference", "leg": best_leg, "sample": best["sample"]})
     return out
 
 
@@ -165,13 +198,49 @@ def pmc_traffic(tag, kernel, fused, xdefer, fupd):
 
 def relaunch_distributed(args):
     """--gpus N > 1 without a launcher: start torch.distributed.run as a child
-    (nothing has touched the GPU yet) and exit with its code."""
+    (nothing has touched the GPU yet) and exit with its code; past --timeout
+    the whole job (its own process group) is killed and the exit code is 124."""
+    import signal
     port = 29400 + (os.getpid() % 500)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     log("launching:", " ".join(cmd))
-    return subprocess.call(cmd, env=env)
+    p = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return p.wait(timeout=args.timeout)
+    except subprocess.TimeoutExpired:
+        log(f"bench: job exceeded --timeout {args.timeout:.0f} s; killing process group {p.pid}")
+        os.killpg(p.pid, signal.SIGTERM)
+        try:
+            p.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+        return 124
+
+
+class Stages:
+    """Per-rank progress on stderr, and a watchdog: a rank whose run outlives
+    the limit reports the stage it is stuck in and exits (124) instead of
+    leaving a hung job that records nothing."""
+
+    def __init__(self, rank, limit_s):
+        import threading
+        self.rank, self.t0, self.stage = rank, time.time(), "start"
+        self.done = threading.Event()
+        if limit_s > 0:
+            threading.Thread(target=self._watch, args=(limit_s,), daemon=True).start()
+
+    def __call__(self, stage, **kv):
+        self.stage = stage
+        extra = " ".join(f"{k}={v}" for k, v in kv.items())
+        log(f"[rank {self.rank}] +{time.time() - self.t0:7.2f}s {stage} {extra}".rstrip())
+
+    def _watch(self, limit_s):
+        if not self.done.wait(limit_s):
+            log(f"[rank {self.rank}] watchdog: still in stage '{self.stage}' after {limit_s:.0f} s; exiting 124")
+            os._exit(124)
 
 
 def main():
@@ -195,6 +264,9 @@ def main():
     ap.add_argument("--use-graph", type=int, default=-1, help="hipGraph replay (-1 default on)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VAL",
                     help="any other solver option (hpccg_hip_set_option), e.g. --set nt_store=0")
+    ap.add_argument("--timeout", type=float, default=1200.0,
+                    help="seconds before the run is abandoned (exit 124): the parent kills a relaunched job, "
+                         "each rank's watchdog ends a run that outlives it (0: no limit)")
     ap.add_argument("--event-steps", type=int, default=1,
                     help="timed steps launched eagerly with hipEvents around every SpMV (the roofline's kernel "
                          "time); the other timed steps replay hipGraphs")
@@ -208,6 +280,8 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
+    stage = Stages(rank, args.timeout)
+    stage("start", pid=os.getpid(), local_rank=local_rank, world=world)
     import torch
     import torch.distributed as dist
     hp = load_pkg()
@@ -218,6 +292,23 @@ def main():
         obj = [hp.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         hp.comm_init(obj[0], world, rank)
+    try:
+        rt = hp.runtime_info()
+    except AttributeError:  # an older library under A/B (HPCCG_HIP_LIB)
+        rt = {"rccl_nranks": None, "pci_bus_id": None, "rccl_version": None, "rccl_rank": rank}
+    stage("comm_init", rccl_nranks=rt["rccl_nranks"], pci=rt["pci_bus_id"], rccl=rt["rccl_version"])
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (rt["pci_bus_id"], rt["rccl_nranks"], rt["rccl_rank"]))
+        rt["pci_bus_ids"] = [g[0] for g in gathered]
+        rt["rccl_ranks_seen"] = [g[2] for g in gathered]
+        rt["distinct_devices"] = len(set(rt["pci_bus_ids"]))
+        if rt["rccl_nranks"] != world or rt["distinct_devices"] != world:
+            log(f"[rank {rank}] WARNING: RCCL counts {rt['rccl_nranks']} ranks on {rt['distinct_devices']} distinct "
+                f"devices for WORLD_SIZE={world}")
+    else:
+        rt["pci_bus_ids"] = [rt["pci_bus_id"]]
+        rt["distinct_devices"] = 1
 
     n = args.n
     use_7pt = args.stencil == 7
@@ -239,8 +330,8 @@ def main():
     torch.cuda.synchronize()
     kernel = M.get_option("spmv_kernel")
     kfmt = 3 if (kernel == 2 and M.get_option("a2_ring") > 0) else kernel  # 3: the pair kernel's LDS-DMA ring form
-    log(f"[rank {rank}] setup {time.time() - t0:.2f}s nnz={info['nnz']} slots={info['slots']} kernel={kernel} "
-        f"device_bytes={M.get_option('device_bytes') / 1e9:.2f} GB")
+    stage("setup", seconds=f"{time.time() - t0:.2f}", nnz=info["nnz"], slots=info["slots"], kernel=kernel,
+          device_gb=f"{M.get_option('device_bytes') / 1e9:.2f}")
 
     def step(events):
         M.set_option("event_timing", 1 if events else 0)
@@ -253,6 +344,7 @@ def main():
         step(i == 0)
         if i == 0:
             cold_s = time.perf_counter() - t0  # first solve: graph build, cold caches
+            stage("first_solve", seconds=f"{cold_s:.3f}")
 
     def barrier():
         if world > 1:
@@ -285,6 +377,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
+    stage("timed", steps=args.steps, seconds=f"{elapsed:.3f}")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -346,7 +439,7 @@ def main():
             "data": "synthetic (generate_matrix stencil on the device; deterministic, no RNG)",
             "config": {
                 "workload": f"HPCCG solve, {args.stencil}-pt {n}x{n}x{n} per GPU, z-stacked, "
-                            f"max_iter={args.max_iter} (499 CG iterations), tolerance 0",
+                            f"max_iter={args.max_iter} ({args.max_iter - 1} CG iterations), tolerance 0",
                 "nx": n, "ny": n, "nz_per_gpu": n, "stencil": args.stencil,
                 "max_iter": args.max_iter, "parallelism": f"z-slab x{world} (RCCL)",
                 "nnz_per_gpu": info["nnz"], "matrix_slots_per_gpu": slots,
@@ -369,6 +462,12 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                # FETCH_SIZE / WRITE_SIZE count the L2 <-> fabric bytes: Infinity
+                # Cache (MALL) hits are in them. An image under 256 MB (100^3)
+                # may be served partly by the MALL, so "hbm" is its upper bound.
+                "traffic_note": "L2-fabric bytes (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE), Infinity Cache hits "
+                                "included",
+                "image_fits_infinity_cache": not bool(M.get_option("nt")),
                 "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
                 "kernel": "%s: %s + p.Ap%s" % (KERNEL_NAMES[kfmt], FORMAT_NAMES[kfmt],
                                               " + p = r + beta p" if fused else ""),
@@ -402,6 +501,11 @@ def main():
             "times_per_step_s": {"total": times_acc[0] / args.steps, "ddot": times_acc[1] / args.steps,
                                  "waxpby": times_acc[2] / args.steps, "sparsemv": times_acc[3] / args.steps,
                                  "allreduce": times_acc[4] / args.steps, "halo": times_acc[5] / args.steps},
+            # rank 0's device stamps (HPCCG.cpp:71-72 classes t4, t5) per CG iteration
+            "per_iteration_us": {"allreduce": round(times_acc[4] / max(1, niters_total) * 1e6, 3),
+                                 "halo": round(times_acc[5] / max(1, niters_total) * 1e6, 3),
+                                 "total": round(elapsed / max(1, niters_total) * 1e6, 3)},
+            "runtime": rt,
             "cpu_baseline": None,
         }
         if traffic:
@@ -418,6 +522,7 @@ def main():
     if world > 1:
         hp.comm_destroy()
         dist.destroy_process_group()
+    stage.done.set()
 
 
 if __name__ == "__main__":

@@ -80,6 +80,7 @@ def lib() -> C.CDLL:
         "hpccg_hip_comm_size": (ip, [PI, PI]),
         "hpccg_hip_comm_allreduce_host": (ip, [PD, ip, ip]),
         "hpccg_hip_device_name": (ip, [C.c_char_p, ip, PI]),
+        "hpccg_hip_runtime_info": (ip, [PI, C.c_char_p, ip, C.c_char_p, C.c_char_p, ip]),
         "hpccg_generate_matrix": (ip, [ip, ip, ip, ip, ip, ip, C.POINTER(C.POINTER(_HPCMatrix)),
                                        C.POINTER(PD), C.POINTER(PD), C.POINTER(PD)]),
         "hpccg_free_problem": (None, [C.POINTER(_HPCMatrix), PD, PD, PD]),
@@ -119,6 +120,8 @@ def lib() -> C.CDLL:
                                        PD, PD]),
     }
     for name, (res, args) in sig.items():
+        if path != LIB_PATH and not hasattr(L, name):
+            continue  # an older build under A/B (HPCCG_HIP_LIB): bind what it has
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -470,6 +473,21 @@ def comm_allreduce_host(vals, op: str = "sum") -> np.ndarray:
 
 def comm_destroy() -> None:
     lib().hpccg_hip_comm_destroy()
+
+
+def runtime_info() -> dict:
+    """What this process runs on: RCCL's own rank count (ncclCommCount) and
+    rank, RCCL / HIP versions, the device's PCI bus id, and the shared objects
+    the library's RCCL and HIP symbols resolved to."""
+    ints = (C.c_int * 6)()
+    pci = C.create_string_buffer(64)
+    rccl, hip = C.create_string_buffer(512), C.create_string_buffer(512)
+    _check(lib().hpccg_hip_runtime_info(ints, pci, 64, rccl, hip, 512), "runtime_info")
+    v = ints[2]
+    return {"rccl_nranks": ints[0], "rccl_rank": ints[1],
+            "rccl_version": f"{v // 10000}.{v // 100 % 100}.{v % 100}" if v >= 10000 else str(v),
+            "hip_runtime_version": ints[3], "hip_driver_version": ints[4], "device": ints[5],
+            "pci_bus_id": pci.value.decode(), "rccl_lib": rccl.value.decode(), "hip_lib": hip.value.decode()}
 
 
 def device_name() -> tuple[str, int]:

@@ -71,7 +71,7 @@ struct CgArgs {
     int fold;              // dots completed in the producing kernel: 0 none, 1 both, 2 p.Ap only, 3 r.r only
     unsigned int* tickets; // [2 x (ngroups + 1)] arrival counters (fold): groups, top
     double* Ap;
-    double* partial;       // [nslices] slice partials, then 2 x ngroups group sums
+    double* partial;       // [2 x nslices] slice partials (p.Ap, r.r), then 2 x ngroups group sums
     double* g;             // [2] dot results after the all-reduce
     double* loc;           // [2] local dot results
     double* hist;          // [max_iter + 1]: hist[j] = r_j . r_j (global)
@@ -103,7 +103,35 @@ struct CgArgs {
     int fu2;                      // fused update: two slices per update block (four rows per thread)
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
+    int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
 };
+
+// Bounded in-kernel waits: a wait that outlives the spin budget (s_memrealtime
+// ticks, 100 MHz) records itself in the device error record and ends the
+// solve (later launches fail the loop test); the host turns it into an error
+// return. The record lives in device memory behind the iteration state,
+// err = kst + kErrBase, and kst is found from a.partial (kKstDoubles below):
+// the waits are a cold path and must not hold registers in the hot one.
+//   err[0] code, [1] block, [2] group / slot, [3] iteration k, [4] dot (kRR /
+//   kPAP), [5] the maximum code over the ranks of an RCCL job (all-reduced
+//   after the solve), [6] the spin budget in ticks (u32, at most 42 s; set by the host).
+constexpr int kErrBase = 8;
+constexpr int kErrWords = 8;
+// The state block precedes the dot slots in one allocation: kst = (int*)
+// (partial - kKstDoubles). 256 B, so no slot shares a cache line with kst:
+// every block reads k there at its start, and the slots' sc1 stores drop
+// their line from the XCD's L2.
+constexpr int kKstDoubles = 32;
+static_assert(kKstDoubles * 2 >= kErrBase + kErrWords, "state block");
+constexpr int kErrAllRanks = 5;
+constexpr int kErrBudget = 6;
+enum DevError : int {
+    kErrNone = 0,
+    kErrGroupWait = 1,  // a group's waiter: slice partials missing
+    kErrTopWait = 2,    // the top waiter: group sums missing
+    kErrReadyWait = 3,  // a fused update block: the launch's p.Ap total missing
+};
+constexpr long long kSpinTicksDefault = 100000000;  // 1 s
 
 // Is dot `which` (kRR / kPAP) completed inside its producing kernel?
 inline __host__ __device__ bool fold_of(const CgArgs& a, int which)

@@ -293,10 +293,72 @@ __device__ __forceinline__ double ld_sc1(const double* p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ int ld_sc1_i(const int* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_i(int* p, int v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ int ngroups_of(const CgArgs& a) { return (a.nslices + kGroup - 1) / kGroup; }
+
+// Slot layout: each dot has its own slice-partial slots (p.Ap, then r.r) and
+// its own group sums after both. The fused update completes both dots in one
+// launch: with separate ranges no slot is reused within a launch, so a
+// waiter's resets need no drain before it publishes (they only have to land
+// before the next launch, which the kernel boundary guarantees).
+__device__ __forceinline__ double* slice_slots(const CgArgs& a, int which) { return a.partial + which * a.nslices; }
+__device__ __forceinline__ double* group_slots(const CgArgs& a, int which, int ng)
+{
+    return a.partial + 2 * a.nslices + which * ng;
+}
 
 __device__ __forceinline__ bool slot_full(double v) { return __double_as_longlong(v) != (long long)kSlotEmpty; }
 __device__ __forceinline__ double slot_empty() { return __longlong_as_double((long long)kSlotEmpty); }
+
+// Every in-kernel wait is bounded (HIP promises no dispatch order; the slot
+// protocol below relies on the order observed on gfx950). Called after a
+// failed poll, wave-uniform: true once another waiter has given up (the solve
+// is void, leave at once) or this wait has outlived a.spin_ticks.
+// The iteration state as the waits see it: derived from a.partial, which every
+// waiter holds anyway (a.kst would be one more live register pair).
+__device__ __forceinline__ int* kst_of(const CgArgs& a) { return reinterpret_cast<int*>(a.partial - kKstDoubles); }
+
+__device__ __forceinline__ bool wait_expired(const CgArgs& a, unsigned& t0)
+{
+    const int* err = kst_of(a) + kErrBase;
+    if (ld_sc1_i(err) != kErrNone) return true;
+    const unsigned t = (unsigned)now_ticks() | 1u;  // 32 bits of the 100 MHz clock (42 s wrap), never 0
+    if (t0 == 0) {
+        t0 = t;
+        return false;
+    }
+    return t - t0 > (unsigned)err[kErrBudget];
+}
+
+// One lane: record the first failed wait and end the solve. k >= max_iter
+// fails every later loop test, and the iteration's published run flag is
+// cleared so the kernels that follow this launch in the same iteration (the
+// unfused update, k_finalize) do nothing either. The host reads err after the
+// solve (HPCCG_HIP_EHIP) and empties every slot before the next one.
+__device__ __forceinline__ void abort_solve(const CgArgs& a, int code, int slot, int k, int which)
+{
+    int* const kst = kst_of(a);
+    int* const err = kst + kErrBase;
+    int none = kErrNone;  // relaxed: the record is read by the host after the solve
+    if (__hip_atomic_compare_exchange_strong(err, &none, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+        st_sc1_i(err + 1, (int)blockIdx.x);
+        st_sc1_i(err + 2, slot);
+        st_sc1_i(err + 3, k);
+        st_sc1_i(err + 4, which);
+    }
+    st_sc1_i(kst + 0, a.max_iter);
+    st_sc1_i(kst + 2, a.max_iter);
+    st_sc1_i(kst + 5, 0);
+}
 
 // How a launch deals its units (slices, or slice pairs: spu slices per unit)
 // to blocks: unit u = the x-th XCD eighth's i-th unit, run by block
@@ -397,24 +459,31 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
                                                    int which, int k)
 {
     const int lane = threadIdx.x;
+    double* const sp = slice_slots(a, which);
     if (!fold_of(a, which)) {
-        if (lane < cnt) a.partial[s0 + lane] = bs;
+        if (lane < cnt) sp[s0 + lane] = bs;
         return;
     }
     const int ng = ngroups_of(a);
-    double* gp = a.partial + a.nslices + which * ng;  // group sums of this dot
+    double* const gp = group_slots(a, which, ng);
     const int g = s0 / kGroup;
     const int i = g * kGroup + lane;  // the group's slot of this lane
     if (a.slots) {
-        if (lane < cnt) st_sc1(a.partial + s0 + lane, bs);
+        // (a.dbg_withhold: the guard test's missing partial)
+        if (lane < cnt && !(which == kPAP && s0 + lane == a.dbg_withhold - 1)) st_sc1(sp + s0 + lane, bs);
         if (u != group_last_unit(m, g)) return;
         double v;
+        unsigned t0 = 0, polls = 0;
         for (;;) {  // the group's other members were dispatched before this block
-            v = i < a.nslices ? ld_sc1(a.partial + i) : 0.0;
+            v = i < a.nslices ? ld_sc1(sp + i) : 0.0;
             if (__all(i >= a.nslices || slot_full(v))) break;
+            if ((++polls & 15) == 0 && wait_expired(a, t0)) {  // every 16th failed poll
+                if (lane == 0) abort_solve(a, kErrGroupWait, g, k, which);
+                return;
+            }
             __builtin_amdgcn_s_sleep(1);
         }
-        if (i < a.nslices) st_sc1(a.partial + i, slot_empty());
+        if (i < a.nslices) st_sc1(sp + i, slot_empty());
         v = wave_sum(v);
         if (lane == 0) st_sc1(gp + g, v);
         if (g != top_group(m)) return;
@@ -423,6 +492,10 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
                 const int j = j0 + lane;
                 const double w = j < ng ? ld_sc1(gp + j) : 0.0;
                 if (__all(j >= ng || slot_full(w))) break;
+                if ((++polls & 15) == 0 && wait_expired(a, t0)) {
+                    if (lane == 0) abort_solve(a, kErrTopWait, j0, k, which);
+                    return;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -433,7 +506,7 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
     }
     unsigned* gt = a.tickets + which * (ng + 1);  // group tickets, then the top one
     int role = 0;
-    if (lane < cnt) st_sc1(a.partial + s0 + lane, bs);
+    if (lane < cnt) st_sc1(sp + s0 + lane, bs);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
         const unsigned glen = (unsigned)min(kGroup, a.nslices - g * kGroup);
@@ -447,8 +520,8 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
     role = __shfl(role, 0, kWave);
     if (role == 0) return;
     // group reducer (this wave): sc1 loads of the group's partials
-    const double v = wave_sum(i < a.nslices ? ld_sc1(a.partial + i) : 0.0);
-    if (i < a.nslices) st_sc1(a.partial + i, slot_empty());
+    const double v = wave_sum(i < a.nslices ? ld_sc1(sp + i) : 0.0);
+    if (i < a.nslices) st_sc1(sp + i, slot_empty());
     if (lane == 0) {
         st_sc1(gp + g, v);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -796,13 +869,25 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue)
     const Rows rv = ld(a.r + row);
     const Rows rv2 = nsl > 1 ? ld(a.r + row + kSliceRows) : Rows{{0.0, 0.0}};
     __shared__ double pap_s;
+    __shared__ int gave_up;
     if (threadIdx.x == 0) {  // one poller per block
         double v;
         const double* slot = a.pready + kReadyStride * (bl % kNumXcd);
-        while (!slot_full(v = ld_sc1(slot))) __builtin_amdgcn_s_sleep(8);
+        unsigned t0 = 0, polls = 0;
+        int bail = 0;
+        while (!slot_full(v = ld_sc1(slot))) {
+            if ((++polls & 15) == 0 && wait_expired(a, t0)) {
+                abort_solve(a, kErrReadyWait, bl % kNumXcd, k, kPAP);
+                bail = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
         pap_s = v;
+        gave_up = bail;
     }
     __syncthreads();
+    if (gave_up) return true;
     const double alpha = rr / pap_s;
     if (bl == 0 && threadIdx.x == 0) {
         a.ahist[k] = alpha;
@@ -1393,7 +1478,8 @@ constexpr int kFinLdsGroups = 2048;  // group sums kept in LDS up to 128 K slice
 // kB groups per wave per round, every load of a round issued before the sums
 // (one round up to 16 x kB groups: 200^3 has 245, 7-pt 256^3 512).
 template <int kB>
-__device__ __forceinline__ void finalize_groups(const CgArgs& a, int ng, bool in_lds, double* gs, double* gp)
+__device__ __forceinline__ void finalize_groups(const CgArgs& a, double* sp, int ng, bool in_lds, double* gs,
+                                                double* gp)
 {
     const int lane = threadIdx.x & (kWave - 1);
     constexpr int kWaves = kFinalizeThreads / kWave;
@@ -1402,12 +1488,12 @@ __device__ __forceinline__ void finalize_groups(const CgArgs& a, int ng, bool in
 #pragma unroll
         for (int b = 0; b < kB; b++) {
             const int i = (g0 + b * kWaves) * kGroup + lane;
-            v[b] = (g0 + b * kWaves < ng && i < a.nslices) ? a.partial[i] : 0.0;
+            v[b] = (g0 + b * kWaves < ng && i < a.nslices) ? sp[i] : 0.0;
         }
 #pragma unroll
         for (int b = 0; b < kB; b++) {  // the slots are empty again for the next producer
             const int i = (g0 + b * kWaves) * kGroup + lane;
-            if (g0 + b * kWaves < ng && i < a.nslices) a.partial[i] = slot_empty();
+            if (g0 + b * kWaves < ng && i < a.nslices) sp[i] = slot_empty();
         }
 #pragma unroll
         for (int b = 0; b < kB; b++) {
@@ -1428,7 +1514,8 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
     __shared__ double gs[kFinLdsGroups];
     const int ng = ngroups_of(a);
     const bool in_lds = ng <= kFinLdsGroups;
-    double* gp = a.partial + a.nslices + which * ng;
+    double* const sp = slice_slots(a, which);
+    double* const gp = group_slots(a, which, ng);
     const int lane = threadIdx.x & (kWave - 1);
     int k = 0;
     bool run = true;
@@ -1436,11 +1523,11 @@ __global__ __launch_bounds__(kFinalizeThreads) void k_finalize(CgArgs a, int whi
     // stamped unconditionally: stamps after the end stamp are dropped on the host
     if (threadIdx.x == 0) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
     if (ng <= 4 * (kFinalizeThreads / kWave))
-        finalize_groups<4>(a, ng, in_lds, gs, gp);
+        finalize_groups<4>(a, sp, ng, in_lds, gs, gp);
     else if (ng <= 16 * (kFinalizeThreads / kWave))
-        finalize_groups<16>(a, ng, in_lds, gs, gp);
+        finalize_groups<16>(a, sp, ng, in_lds, gs, gp);
     else
-        finalize_groups<32>(a, ng, in_lds, gs, gp);
+        finalize_groups<32>(a, sp, ng, in_lds, gs, gp);
     if (!run) {
         if (threadIdx.x == 0) mark_end(a);
         return;

@@ -3,6 +3,7 @@
 // driver (HPCCG.cpp:312-402) replayed from hipGraphs, the z-slab halo exchange
 // and scalar all-reduces over RCCL (exchange_externals.cpp:51-131,
 // ddot.cpp:75-85), the in-process rank group, and the C ABI.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -254,11 +255,14 @@ struct hpccg_hip_matrix {
     int rev_update = 1;
     double *d_r = nullptr, *d_Ap = nullptr, *d_x = nullptr, *d_b = nullptr;
     double* d_rbuf = nullptr;
-    double* d_partial = nullptr;
+    double* d_partial = nullptr;  // inside the d_kst block (not freed on its own)
     unsigned int* d_tickets = nullptr;
     int ntickets = 0;
     double* d_scal = nullptr;  // g[2], loc[2], spare
-    int* d_kst = nullptr;
+    int* d_kst = nullptr;      // [0, kErrBase) iteration state, then the device error record (kErrWords)
+    long long spin_us = kSpinTicksDefault / 100;  // bound of every in-kernel wait (option spin_budget_us)
+    int dbg_withhold = 0;      // debug: slice + 1 whose p.Ap partial is withheld (guard test)
+    int solve_dirty = 0;       // a solve started and did not finish cleanly: reset the dot slots first
     double* d_hist = nullptr;
     unsigned long long* d_stamps = nullptr;
     double* d_emul = nullptr;  // force_comm 2: self-exchange receive buffer
@@ -313,7 +317,7 @@ int free_matrix(hpccg_hip_matrix* M)
     if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
     void* ptrs[] = {M->d_slice_base, M->d_cols,   M->d_vals,      M->d_aval,    M->d_aoff,     M->d_abase,
                     M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_adiag2,     M->d_atri,      M->d_pbuf,    M->d_ahist,    M->d_rbuf,
-                    M->d_Ap,         M->d_x,      M->d_b,         M->d_partial, M->d_tickets,  M->d_scal,
+                    M->d_Ap,         M->d_x,      M->d_b,         M->d_tickets,  M->d_scal,
                     M->d_kst,        M->d_hist,   M->d_stamps,    M->d_gen_b,   M->d_gen_x0,   M->d_gen_xexact,
                     M->d_send_idx,   M->d_send_buf,  M->d_emul};
     for (void* p : ptrs)
@@ -905,14 +909,19 @@ int alloc_workspace(hpccg_hip_matrix* M)
     {
         const size_t np = 2 * (size_t)std::max(1, M->nslices) + 2 * ngroups + 8 + kNumXcd * kReadyStride;
         M->npartial = np;
-        TRY(dev_alloc(M, &M->d_partial, np));
+        // one block: the iteration state and error record (kKstDoubles), then
+        // the slots -- the kernels' bounded waits find the record from
+        // a.partial, which they hold anyway (kst_of in hpccg_kernels.hip)
+        double* blk = nullptr;
+        TRY(dev_alloc(M, &blk, kKstDoubles + np, true));
+        M->d_kst = reinterpret_cast<int*>(blk);
+        M->d_partial = blk + kKstDoubles;
         const std::vector<unsigned long long> empty(np, kSlotEmpty);  // every dot slot starts empty
         HIP_TRY(hipMemcpy(M->d_partial, empty.data(), np * sizeof(double), hipMemcpyHostToDevice));
     }
     M->ntickets = 2 * (ngroups + 1);
     TRY(dev_alloc(M, &M->d_tickets, M->ntickets, true));
     TRY(dev_alloc(M, &M->d_scal, 8, true));
-    TRY(dev_alloc(M, &M->d_kst, 8, true));
     return 0;
 }
 
@@ -1013,6 +1022,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.loc = M->d_scal + 2;
     a.hist = M->d_hist;
     a.kst = M->d_kst;
+    a.dbg_withhold = M->dbg_withhold;
     a.stamps = M->d_stamps;
     a.slice_base = M->d_slice_base;
     a.cols = M->d_cols;
@@ -1557,6 +1567,60 @@ void stamps_to_times(const std::vector<unsigned long long>& st, int max_iter, do
     times[5] = t5;
 }
 
+// Iteration state and error record zeroed, the spin budget (ticks) set.
+int clear_state(hpccg_hip_matrix* M)
+{
+    const long long ticks = M->spin_us * 100;  // s_memrealtime: 100 MHz
+    HIP_TRY(hipMemsetAsync(M->d_kst, 0, sizeof(int) * (kErrBase + kErrWords), M->stream));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(M->d_kst + kErrBase + kErrBudget), (int)ticks, 1, M->stream));
+    return 0;
+}
+
+// After a failed solve: every dot slot empty again, tickets re-armed, the
+// error record cleared, so the next solve starts from the allocation state.
+int reset_dot_state(hpccg_hip_matrix* M)
+{
+    HIP_TRY(hipSetDevice(M->device));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    const std::vector<unsigned long long> empty(M->npartial, kSlotEmpty);
+    HIP_TRY(hipMemcpyAsync(M->d_partial, empty.data(), M->npartial * sizeof(double), hipMemcpyHostToDevice, M->stream));
+    HIP_TRY(hipMemsetAsync(M->d_tickets, 0, sizeof(unsigned int) * M->ntickets, M->stream));
+    TRY(clear_state(M));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    return 0;
+}
+
+// The device error record of every rank (err0: rank 0's, already on the host):
+// a bounded wait that gave up voids the solve (HPCCG_HIP_EHIP). The reference
+// aborts on a failed exchange (exchange_externals.cpp:119-125); this returns.
+int check_device_error(hpccg_hip_matrix* const* Ms, int P, const int* err0)
+{
+    static const char* what[] = {"", "slice partials of a dot group", "group sums of a dot",
+                                 "the p.Ap total (fused update)"};
+    int bad_rank = -1, e[kErrWords];
+    for (int r = 0; r < P && bad_rank < 0; r++) {
+        if (r == 0) {
+            std::memcpy(e, err0, sizeof e);
+        } else {
+            HIP_TRY(hipSetDevice(Ms[r]->device));
+            HIP_TRY(hipMemcpy(e, Ms[r]->d_kst + kErrBase, sizeof e, hipMemcpyDeviceToHost));
+        }
+        if (e[0] != kErrNone || (P == 1 && e[kErrAllRanks] != kErrNone)) bad_rank = r;
+    }
+    if (bad_rank < 0) return 0;
+    for (int r = 0; r < P; r++) TRY(reset_dot_state(Ms[r]));
+    HIP_TRY(hipSetDevice(Ms[0]->device));
+    const int rank = Ms[bad_rank]->rank;
+    if (e[0] == kErrNone)
+        return set_err(HPCCG_HIP_EHIP, "rank %d: a device wait timed out on another rank (code %d); solve abandoned",
+                       rank, e[kErrAllRanks]);
+    return set_err(HPCCG_HIP_EHIP,
+                   "rank %d: device wait timed out after %.0f us waiting for %s (block %d, group %d, iteration %d, "
+                   "dot %s); solve abandoned, dot slots reset",
+                   rank, (double)Ms[bad_rank]->spin_us, e[0] > 0 && e[0] <= 3 ? what[e[0]] : "?", e[1], e[2], e[3],
+                   e[4] == kPAP ? "p.Ap" : "r.r");
+}
+
 // Solve on the ranks Ms[0..P) (P > 1: an in-process group; P == 1: this
 // process's matrix, exchanging through RCCL when the communicator has peers).
 int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, double* const* x_dev, int max_iter,
@@ -1594,7 +1658,10 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     for (int r = 0; r < P; r++) {
         HIP_TRY(hipSetDevice(Ms[r]->device));
         av[r] = make_args(Ms[r], b_dev[r], x_dev[r], max_iter, tol);
-        HIP_TRY(hipMemsetAsync(Ms[r]->d_kst, 0, sizeof(int) * 8, Ms[r]->stream));  // iteration state
+        // the last solve returned an error part-way: its slots may hold partials
+        if (Ms[r]->solve_dirty) TRY(reset_dot_state(Ms[r]));
+        Ms[r]->solve_dirty = 1;
+        TRY(clear_state(Ms[r]));  // iteration state, error record, spin budget
         HIP_TRY(hipMemsetAsync(Ms[r]->d_tickets, 0, sizeof(unsigned int) * Ms[r]->ntickets, Ms[r]->stream));
         HIP_TRY(hipMemsetAsync(Ms[r]->d_stamps, 0,
                                sizeof(unsigned long long) * (size_t)(max_iter + 2) * kNumStampSlots, Ms[r]->stream));
@@ -1661,13 +1728,18 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
         if (r > 0) HIP_TRY(hipStreamSynchronize(Ms[r]->stream));
     }
     HIP_TRY(hipSetDevice(M->device));
-    int kst[4];
+    // an RCCL job: every rank learns whether any rank gave up a wait (err[7])
+    if (P == 1 && M->nranks > 1 && !M->in_group && g_comm.comm)
+        NCCL_TRY(ncclAllReduce(M->d_kst + kErrBase, M->d_kst + kErrBase + kErrAllRanks, 1, ncclInt32, ncclMax,
+                               g_comm.comm, M->stream));
+    int kst[kErrBase + kErrWords];
     HIP_TRY(hipMemcpyAsync(kst, M->d_kst, sizeof kst, hipMemcpyDeviceToHost, M->stream));
     // (the fused update keeps k in kst[0] / kst[2] by parity: the later one is the count)
     double scal[8];
     HIP_TRY(hipMemcpyAsync(scal, M->d_scal, sizeof scal, hipMemcpyDeviceToHost, M->stream));
     HIP_TRY(hipStreamSynchronize(M->stream));
     const auto t_end = std::chrono::steady_clock::now();
+    TRY(check_device_error(Ms, P, kst + kErrBase));
     const int niters = std::max(0, (av[0].fupd ? std::max(kst[0], kst[2]) : kst[0]) - 1);
     std::vector<double> hist(std::max(1, niters));
     if (niters > 0) HIP_TRY(hipMemcpy(hist.data(), M->d_hist, sizeof(double) * niters, hipMemcpyDeviceToHost));
@@ -1715,6 +1787,7 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     }
     *niters_out = niters;
     *normr_out = normr;
+    for (int r = 0; r < P; r++) Ms[r]->solve_dirty = 0;
     return 0;
 }
 
@@ -2065,6 +2138,39 @@ int hpccg_hip_comm_allreduce_host(double* vals, int n, int op)
     return 0;
 }
 
+int hpccg_hip_runtime_info(int ints_out[6], char* pci_bus_id, int pci_cap, char* rccl_path, char* hip_path,
+                           int path_cap)
+{
+    if (!ints_out) return set_err(HPCCG_HIP_EINVAL, "ints_out is NULL");
+    int dev = 0, v = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    ints_out[0] = ints_out[1] = 0;
+    if (g_comm.comm) {
+        NCCL_TRY(ncclCommCount(g_comm.comm, &ints_out[0]));
+        NCCL_TRY(ncclCommUserRank(g_comm.comm, &ints_out[1]));
+    }
+    NCCL_TRY(ncclGetVersion(&v));
+    ints_out[2] = v;
+    HIP_TRY(hipRuntimeGetVersion(&v));
+    ints_out[3] = v;
+    HIP_TRY(hipDriverGetVersion(&v));
+    ints_out[4] = v;
+    ints_out[5] = dev;
+    if (pci_bus_id && pci_cap > 0) HIP_TRY(hipDeviceGetPCIBusId(pci_bus_id, pci_cap, dev));
+    // the files the RCCL and HIP entry points of this library resolved to
+    auto where = [](const void* sym, char* out, int cap) {
+        Dl_info di;
+        if (!out || cap <= 0) return;
+        if (dladdr(sym, &di) && di.dli_fname)
+            std::snprintf(out, cap, "%s", di.dli_fname);
+        else
+            std::snprintf(out, cap, "?");
+    };
+    where(reinterpret_cast<const void*>(&ncclGetVersion), rccl_path, path_cap);
+    where(reinterpret_cast<const void*>(&hipRuntimeGetVersion), hip_path, path_cap);
+    return 0;
+}
+
 int hpccg_hip_device_name(char* buf, int cap, int* cus)
 {
     int dev = 0;
@@ -2381,6 +2487,12 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "force_comm")) {
         if (value < 0 || value > 2) return set_err(HPCCG_HIP_EINVAL, "force_comm is 0, 1 or 2");
         M->force_comm = (int)value;
+    } else if (!std::strcmp(key, "spin_budget_us")) {
+        if (value < 1 || value > 20000000LL) return set_err(HPCCG_HIP_EINVAL, "spin_budget_us must be 1..2e7");
+        M->spin_us = value;
+    } else if (!std::strcmp(key, "dbg_withhold")) {
+        if (value < 0 || value > M->nslices) return set_err(HPCCG_HIP_EINVAL, "dbg_withhold must be 0..nslices");
+        M->dbg_withhold = (int)value;
     } else if (!std::strcmp(key, "spmv_kernel")) {
         if (value != -1 && !spmv_kernel_ok((int)value))
             return set_err(HPCCG_HIP_EINVAL, "spmv_kernel must be -1 (auto), 0 (SELL-512), 1 (SELL-512-A direct) or "
@@ -2410,9 +2522,19 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "fuse_update")) *value = fuse_update_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "fused_update_slices")) *value = M->fused_update_slices;
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
-    else if (!std::strcmp(key, "graph_chunk")) *value = M->graph_iters;
+    else if (!std::strcmp(key, "graph_chunk")) {  // effective: see graph_chunk_of
+        long long c = std::max(1, M->graph_iters);
+        if (fuse_update_effective(M)) c += c & 1;
+        if (multi_of(M)) {
+            const long long ring = x_defer_effective(M) ? x_ring_effective(M) : (fuse_p_effective(M) ? 2 : 1);
+            c = (c + ring - 1) / ring * ring;
+        }
+        *value = c;
+    }
     else if (!std::strcmp(key, "graph_used")) *value = M->graph_used;
     else if (!std::strcmp(key, "force_comm")) *value = M->force_comm;
+    else if (!std::strcmp(key, "spin_budget_us")) *value = M->spin_us;
+    else if (!std::strcmp(key, "dbg_withhold")) *value = M->dbg_withhold;
     else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
     else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;
     else if (!std::strcmp(key, "stage16")) *value = M->stage16;

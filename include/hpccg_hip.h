@@ -58,6 +58,15 @@ int hpccg_hip_comm_size(int* nranks, int* rank);
 int hpccg_hip_comm_allreduce_host(double* vals, int n, int op);
 /* Device name and compute-unit count of the current device. */
 int hpccg_hip_device_name(char* buf, int cap, int* compute_units);
+/* Runtime identity of this process (diagnostics; replaces nothing in the
+ * reference, whose MPI path is compiled out: main.cpp:131-132):
+ * ints_out = {ranks of the RCCL communicator as RCCL counts them
+ * (ncclCommCount; 0 without one), this rank (ncclCommUserRank), ncclGetVersion,
+ * hipRuntimeGetVersion, hipDriverGetVersion, current device}; the device's PCI
+ * bus id; the shared objects the library's RCCL and HIP entry points resolved
+ * to (dladdr). Buffers may be NULL. */
+int hpccg_hip_runtime_info(int ints_out[6], char* pci_bus_id, int pci_cap, char* rccl_path, char* hip_path,
+                           int path_cap);
 
 /* ---- host-side input (the reference's generate_matrix.cpp:196-307) ------
  * Builds the reference HPC_Sparse_Matrix for rank `rank` of `size`
@@ -138,8 +147,18 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *   "use_graph"     replay CG iterations from hipGraphs (default 1; every rank
  *                   count, RCCL calls captured; falls back to eager launches if
  *                   the capture is refused); get "graph_used": the last solve did
- *   "graph_chunk"   iterations per graph (default 32; a multiple of the p ring
- *                   when a halo is exchanged)
+ *   "graph_chunk"   iterations per graph (default 32). Rounded up to an even
+ *                   count with the fused update (each captured launch bakes in
+ *                   the parity of its k) and to a multiple of the p ring when a
+ *                   halo is exchanged; get returns the effective count
+ *   "spin_budget_us" bound of every in-kernel wait (the dot slots, the fused
+ *                   update's p.Ap total), default 1000000. A wait that outlives
+ *                   it records itself on the device and ends the solve: the
+ *                   call returns HPCCG_HIP_EHIP naming the wait (block, group,
+ *                   iteration, dot), every rank of an RCCL job returns it, and
+ *                   the dot slots are reset before the next solve
+ *   "dbg_withhold"  debug (guard test): slice + 1 whose p.Ap partial is never
+ *                   published, so the solve must time out (0 = off)
  *   "event_timing"  1 = eager launches with hipEvents around every SpMV and
  *                   update (hpccg_hip_kernel_times)
  *   "fuse_p"        -1 auto / 0 off: p = r + beta p formed inside the SpMV
