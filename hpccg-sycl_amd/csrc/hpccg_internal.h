@@ -104,6 +104,13 @@ struct CgArgs {
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
+    // r-halo exchange (multi-rank z-slabs, fused p update): the halo moves r's
+    // boundary planes (with the r.r all-reduce) into r's ghost planes; the SpMV
+    // forms p_k = r + beta p_{k-1} at ghost rows itself, and its ghost blocks
+    // (index >= gbase) store p_k there for the next iteration's p_{k-1}
+    int rhalo;
+    int ghost_hi;                 // halo rows above (ghost_lo: below)
+    int gbase;                    // first ghost block of the SpMV launch (set at launch; INT_MAX: none)
 };
 
 // Bounded in-kernel waits: a wait that outlives the spin budget (s_memrealtime

@@ -804,7 +804,7 @@ __host__ __device__ constexpr int side_blocks(int nslices, int nring, int spu)
 template <int kSpu, int kB, bool kFU = false>
 __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
 {
-    if ((int)blockIdx.x < a.sgrid || (kFU && (int)blockIdx.x >= a.ubase)) return false;
+    if ((int)blockIdx.x < a.sgrid || (int)blockIdx.x >= a.gbase) return false;  // (gbase <= ubase)
     if (prologue) return true;
     const int k = iter_k<kFU>(a);
     if (k < 2 || !cg_run(a, k, false)) return true;
@@ -833,6 +833,34 @@ __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
         __builtin_nontemporal_store(d2v{xn.v[0], xn.v[1]}, reinterpret_cast<d2v*>(a.x + row));
     else
         st_rows(a.x, row, a.n, xn);
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// r-halo (a.rhalo): the ghost blocks of the SpMV launch (index >= a.gbase,
+// after the unit and side blocks) store p_k = r + beta p_{k-1} at the ghost
+// rows, k_p_update's expression on the received r planes and the p_{k-1}
+// ghosts the previous launch stored (k == 1: p_1 = r + 0 r). The neighbour
+// forms the same rows of its own p_k with the same expression and the same
+// all-reduced beta: the same bits the reference's halo would carry
+// (exchange_externals.cpp:87-126). Read as p_{k-1} by the next launch only.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
+{
+    if ((int)blockIdx.x < a.gbase) return false;
+    if (prologue) return true;
+    const int k = a.kst[0];
+    const double rr = a.g[kRR];
+    if (!cg_run(a, k, true, rr)) return true;
+    const double beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
+    const double* __restrict__ pold = (k == 1) ? a.r : cur_p(a, k - 1);
+    double* __restrict__ pk = cur_p(a, k);
+    const int nlo = a.ghost_lo, tot = a.ghost_lo + a.ghost_hi;
+    const int stride = (int)(gridDim.x - a.gbase) * (int)blockDim.x;
+    for (int i = ((int)blockIdx.x - a.gbase) * (int)blockDim.x + (int)threadIdx.x; i < tot; i += stride) {
+        const int row = i < nlo ? i - nlo : a.n + (i - nlo);
+        pk[row] = a.r[row] + beta * pold[row];
+    }
     return true;
 }
 
@@ -1008,6 +1036,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
         if (fused_update(a, prologue)) return;
     }
     if (side_flush<1, kW == 7 ? 8 : 4, kFU>(a, prologue)) return;
+    if (ghost_store(a, prologue)) return;
     IterState st;
     if (!spmv_begin<kFuse, kFU>(a, prologue, st)) return;
     if (s < 0) return;
@@ -1106,17 +1135,17 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 // slices 2P and 2P + 1 with 512 threads (waves 0-3 slice 2P, 4-7 slice
 // 2P + 1, two rows per thread). The pair's windows (one per offset cluster:
 // one per z-plane for the 27-pt stencil, holes included) are staged first,
-// with kFuse p_k = r + beta*p_{k-1} computed per staged own row (k_p_update's
-// expression; ghost rows of a multi-rank slab come from the halo, guard rows
-// are zeros). Slot j then reads xs[pair row + alds[s][j]]: one per-slice
+// with kFuse p_k = r + beta*p_{k-1} computed per staged row (k_p_update's
+// expression; at ghost rows of a multi-rank slab from r's received planes and
+// the p_{k-1} ghosts the ghost blocks stored; guard rows are zeros). Slot j then reads xs[pair row + alds[s][j]]: one per-slice
 // scalar per slot. kPre value slots are loaded before the iteration test.
 // Each half forms its slice's partial with block_sum<256>'s shape, so the dot
 // is bitwise the one-slice kernels'. 27-pt 200^3: a plane window covers 1024
 // rows for 1426 staged doubles (4.2 per row).
 // ---------------------------------------------------------------------------
 // The pair's windows into LDS (xs): fused, p_k = r + beta*p_{k-1} per staged
-// own row; ghost rows of a multi-rank slab come from the halo, guard rows are
-// zeros. stage16: row pairs (the windows' first row, length and LDS base are
+// row (ghost rows of a multi-rank slab: r's received planes and p_{k-1}'s
+// stored ghosts, ghost_store); guard rows are zeros. stage16: row pairs (the windows' first row, length and LDS base are
 // even, pair_windows) with 16-B loads and LDS stores.
 template <bool kFuse>
 __device__ __forceinline__ void stage_pair_windows(const CgArgs& a, const IterState& st, int P, const double* __restrict__ p,
@@ -1131,16 +1160,11 @@ __device__ __forceinline__ void stage_pair_windows(const CgArgs& a, const IterSt
             for (int i = 2 * threadIdx.x; i < len; i += 4 * kBlock) {
                 const int l = st0 + i;  // local rows l, l + 1 (< 0 / >= n: ghosts, guard or padding zeros)
                 d2v v;
-                if constexpr (kFuse) {
-                    if (l >= 0 && l + 1 < a.n) {  // both own rows (r has no ghost region)
-                        const d2v rv = *reinterpret_cast<const d2v*>(a.r + l);
-                        const d2v yv = *reinterpret_cast<const d2v*>(pold + l);
-                        v.x = rv.x + st.beta * yv.x;
-                        v.y = rv.y + st.beta * yv.y;
-                    } else {
-                        v.x = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
-                        v.y = ((unsigned)(l + 1) < (unsigned)a.n) ? a.r[l + 1] + st.beta * pold[l + 1] : p[l + 1];
-                    }
+                if constexpr (kFuse) {  // ghost rows too: r's received planes, p_{k-1}'s stored ghosts (rhalo)
+                    const d2v rv = *reinterpret_cast<const d2v*>(a.r + l);
+                    const d2v yv = *reinterpret_cast<const d2v*>(pold + l);
+                    v.x = rv.x + st.beta * yv.x;
+                    v.y = rv.y + st.beta * yv.y;
                 } else {
                     v = *reinterpret_cast<const d2v*>(p + l);
                 }
@@ -1150,7 +1174,7 @@ __device__ __forceinline__ void stage_pair_windows(const CgArgs& a, const IterSt
             for (int i = threadIdx.x; i < len; i += 2 * kBlock) {
                 const int l = st0 + i;  // local row (< 0 / >= n: ghosts, guard or padding zeros)
                 if constexpr (kFuse)
-                    xs[base + i] = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
+                    xs[base + i] = a.r[l] + st.beta * pold[l];
                 else
                     xs[base + i] = p[l];
             }
@@ -1180,7 +1204,6 @@ __device__ __forceinline__ void stage_pair_windows_batched(const CgArgs& a, cons
     const int tot = sld(win + 3 * (nw - 1) + 2) + sld(win + 3 * (nw - 1) + 1);
     for (int e0 = 2 * (int)threadIdx.x; e0 < tot; e0 += 4 * kBlock * kU) {
         d2v rv[kU], yv[kU];
-        unsigned direct = 0;  // bit u: rv[u] holds the staged values themselves
 #pragma unroll
         for (int u = 0; u < kU; u++) {
             const int e = e0 + 4 * kBlock * u;
@@ -1192,14 +1215,9 @@ __device__ __forceinline__ void stage_pair_windows_batched(const CgArgs& a, cons
                 const int l = prow0 + lo + (e - base);  // local rows l, l + 1
                 if (!kFuse) {
                     rv[u] = *reinterpret_cast<const d2v*>(p + l);
-                    direct |= 1u << u;
-                } else if (l >= 0 && l + 1 < a.n) {
+                } else {  // every row, ghosts and guard zeros included (rhalo)
                     rv[u] = *reinterpret_cast<const d2v*>(a.r + l);
                     yv[u] = *reinterpret_cast<const d2v*>(pold + l);
-                } else {  // ghosts, guard or padding zeros; an own row beside them
-                    rv[u].x = ((unsigned)l < (unsigned)a.n) ? a.r[l] + st.beta * pold[l] : p[l];
-                    rv[u].y = ((unsigned)(l + 1) < (unsigned)a.n) ? a.r[l + 1] + st.beta * pold[l + 1] : p[l + 1];
-                    direct |= 1u << u;
                 }
             }
         }
@@ -1208,7 +1226,7 @@ __device__ __forceinline__ void stage_pair_windows_batched(const CgArgs& a, cons
             const int e = e0 + 4 * kBlock * u;
             if (e < tot) {
                 d2v v = rv[u];
-                if (!(direct & (1u << u))) {
+                if constexpr (kFuse) {
                     v.x = rv[u].x + st.beta * yv[u].x;
                     v.y = rv[u].y + st.beta * yv[u].y;
                 }
@@ -1265,6 +1283,7 @@ __device__ __forceinline__ void pair_epilogue(const CgArgs& a, const IterState& 
 template <bool kNT, bool kFuse, int kPre>
 __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2(CgArgs a, bool prologue)
 {
+    if (ghost_store(a, prologue)) return;
     extern __shared__ __attribute__((aligned(16))) double xs[];
     const int P = unit_of(a);  // pair: all, or the interior / halo runs
     const int half = threadIdx.x / kBlock;
@@ -1343,6 +1362,7 @@ template <bool kFuse, int kW, int kR>
 __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2r(CgArgs a, bool prologue)
 {
     if (side_flush<2, 16>(a, prologue)) return;
+    if (ghost_store(a, prologue)) return;
     static_assert(kR >= 1 && kR <= kA2RingMax && kR <= kW, "ring depth");
     extern __shared__ __attribute__((aligned(16))) double xs[];
     const int P = unit_of(a);
@@ -1955,11 +1975,17 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     // fused update: a.grid update blocks after the side blocks, from a block
     // index that is a multiple of kNumXcd (their XCD-aware slice order)
     const bool fu = !prologue && a.fupd && kernel == kSpmvDirect && fuse;
+    // r-halo: ghost blocks after the side blocks store p_k at the ghost rows
+    // (about four rows per thread)
+    const int gtot = a.ghost_lo + a.ghost_hi;
+    const int gthreads = kernel == kSpmvPairs ? 2 * kBlock : kBlock;
+    const int nghost = (fuse && a.rhalo && gtot > 0) ? (gtot + 4 * gthreads - 1) / (4 * gthreads) : 0;
     CgArgs b = a;
-    b.ubase = fu ? (a.sgrid + nside + kNumXcd - 1) / kNumXcd * kNumXcd : 0;
+    b.ubase = fu ? (a.sgrid + nside + nghost + kNumXcd - 1) / kNumXcd * kNumXcd : 0;
+    b.gbase = nghost ? a.sgrid + nside : (fu ? b.ubase : INT_MAX);
     // update units: one slice per block, or two (a.fu2: four rows per thread)
     const int ugrid = a.fu2 ? (((a.nslices + 1) / 2 + kNumXcd - 1) / kNumXcd * kNumXcd) : a.grid;
-    const dim3 sg(fu ? b.ubase + ugrid : a.sgrid + nside);
+    const dim3 sg(fu ? b.ubase + ugrid : a.sgrid + nside + nghost);
 #define HPCCG_A(W, NT, PRE)                                                                                       \
     do {                                                                                                          \
         if (fu && a.atri && tri_groups(W) > 0 && PRE > 0)                                                       \
@@ -1982,9 +2008,9 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
 #define HPCCG_A2R(W, R)                                                                                           \
     do {                                                                                                          \
         if (fuse)                                                                                                 \
-            hipLaunchKernelGGL((k_spmv_a2r<true, W, R>), sg, dim3(2 * kBlock), smem, s, a, prologue); \
+            hipLaunchKernelGGL((k_spmv_a2r<true, W, R>), sg, dim3(2 * kBlock), smem, s, b, prologue); \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_spmv_a2r<false, W, R>), sg, dim3(2 * kBlock), smem, s, a, prologue); \
+            hipLaunchKernelGGL((k_spmv_a2r<false, W, R>), sg, dim3(2 * kBlock), smem, s, b, prologue); \
     } while (0)
             if (a.a_width == 7) {
                 switch (a.a2_ring) {
@@ -2006,9 +2032,9 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         }
         const size_t smem = (size_t)a.alds2_doubles * sizeof(double);
         if (fuse)
-            hipLaunchKernelGGL((k_spmv_a2<true, true, 3>), sg, dim3(2 * kBlock), smem, s, a, prologue);
+            hipLaunchKernelGGL((k_spmv_a2<true, true, 3>), sg, dim3(2 * kBlock), smem, s, b, prologue);
         else
-            hipLaunchKernelGGL((k_spmv_a2<true, false, 3>), sg, dim3(2 * kBlock), smem, s, a, prologue);
+            hipLaunchKernelGGL((k_spmv_a2<true, false, 3>), sg, dim3(2 * kBlock), smem, s, b, prologue);
         break;
     }
     case kSpmvDirect:
@@ -2032,9 +2058,9 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         break;
     default:
         if (a.nt)
-            hipLaunchKernelGGL((k_spmv_sell<true>), sg, dim3(kBlock), 0, s, a, prologue);
+            hipLaunchKernelGGL((k_spmv_sell<true>), sg, dim3(kBlock), 0, s, b, prologue);
         else
-            hipLaunchKernelGGL((k_spmv_sell<false>), sg, dim3(kBlock), 0, s, a, prologue);
+            hipLaunchKernelGGL((k_spmv_sell<false>), sg, dim3(kBlock), 0, s, b, prologue);
         break;
     }
 #undef HPCCG_A

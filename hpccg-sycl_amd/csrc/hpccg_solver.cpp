@@ -263,6 +263,7 @@ struct hpccg_hip_matrix {
     long long spin_us = kSpinTicksDefault / 100;  // bound of every in-kernel wait (option spin_budget_us)
     int dbg_withhold = 0;      // debug: slice + 1 whose p.Ap partial is withheld (guard test)
     int solve_dirty = 0;       // a solve started and did not finish cleanly: reset the dot slots first
+    int rhalo_group = 1;       // r-halo: the r.r all-reduce inside the planes' RCCL group (1) or before it (0)
     double* d_hist = nullptr;
     unsigned long long* d_stamps = nullptr;
     double* d_emul = nullptr;  // force_comm 2: self-exchange receive buffer
@@ -841,15 +842,34 @@ bool nt_store_effective(const hpccg_hip_matrix* M)
 }
 
 // p = r + beta p formed inside the SpMV: the pair kernel (ghost rows from the
-// halo) on any rank count; the direct kernel on one rank (it reads r and
-// p_{k-1} at ghost columns, which the halo does not carry); never the SELL-512
-// gather (it would double every gather: 561 -> 744 us at 200^3).
+// halo) on any rank count; the direct kernel on one rank, or on z-slab ranks
+// with the halo received into r's ghost planes (halo_into_r); never the
+// SELL-512 gather (it would double every gather: 561 -> 744 us at 200^3).
 bool fuse_p_effective(const hpccg_hip_matrix* M)
 {
     if (M->fuse_p == 0) return false;
     if (M->kernel == kSpmvPairs) return true;
-    if (M->kernel == kSpmvDirect) return M->nranks == 1;
+    if (M->kernel == kSpmvDirect) return M->nranks == 1 || !M->general;
     return false;
+}
+
+bool multi_of(const hpccg_hip_matrix* M);
+
+// The r-halo exchange (z-slab ranks, p update fused into the SpMV): instead of
+// p_k's boundary planes before the SpMV (k_p_boundary + a send/recv of its
+// own), r's boundary planes move right after the update, in the same RCCL
+// group as the r.r all-reduce, into r's ghost planes. The fused kernels form
+// p_k = r + beta p_{k-1} at every row they read, ghost rows included (the
+// p_{k-1} ghosts stored by the previous launch's ghost blocks), so the direct
+// kernel runs fused on any rank count and an iteration makes two RCCL calls
+// (p.Ap all-reduce; r.r all-reduce + r planes) and one launch less. The
+// neighbour forms the same p_k rows with the same expression and the same
+// all-reduced beta: the values the reference's exchange_externals delivers
+// (exchange_externals.cpp:87-126), bitwise.
+bool rhalo_of(const hpccg_hip_matrix* M)
+{
+    return multi_of(M) && !M->general && fuse_p_effective(M) &&
+           (M->kernel == kSpmvDirect || M->kernel == kSpmvPairs);
 }
 
 // Both dots folded into their producing kernels (slot completion, no
@@ -900,8 +920,9 @@ int alloc_workspace(hpccg_hip_matrix* M)
     const size_t ghi_pad = ((size_t)M->ghost_hi + 2 + kSliceRows - 1) / kSliceRows * kSliceRows;
     M->pstride = (long long)(kGuardRows + glo_pad + M->npad + ghi_pad + kGuardRows);
     TRY(alloc_ring(M, x_ring_effective(M)));
-    TRY(dev_alloc(M, &M->d_rbuf, M->npad + 2 * kGuardRows, true));
-    M->d_r = M->d_rbuf + kGuardRows;
+    // r as one p buffer: zeroed guard zones and ghost planes (halo_into_r)
+    TRY(dev_alloc(M, &M->d_rbuf, (size_t)M->pstride, true));
+    M->d_r = M->d_rbuf + kGuardRows + glo_pad;
     TRY(dev_alloc(M, &M->d_Ap, M->npad, true));
     TRY(dev_alloc(M, &M->d_x, M->npad, true));
     TRY(dev_alloc(M, &M->d_b, M->npad, true));
@@ -1023,6 +1044,9 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.hist = M->d_hist;
     a.kst = M->d_kst;
     a.dbg_withhold = M->dbg_withhold;
+    a.rhalo = rhalo_of(M) ? 1 : 0;
+    a.ghost_hi = M->ghost_hi;
+    a.gbase = INT_MAX;  // set per launch
     a.stamps = M->d_stamps;
     a.slice_base = M->d_slice_base;
     a.cols = M->d_cols;
@@ -1069,8 +1093,10 @@ CgArgs unit_range(const CgArgs& a, int s0, int n0, int s1, int n1)
 // Halo exchange of p (exchange_externals.cpp:51-131): the z-slab ghosts are
 // contiguous, so no pack: rank r sends its first send_lo rows down and its
 // last send_hi rows up, and receives straight into the ghost regions.
-int enqueue_halo(hpccg_hip_matrix* M, double* p, hipStream_t st)
+int enqueue_halo(hpccg_hip_matrix* M, double* p, hipStream_t st, double* dst = nullptr)
 {
+    // dst: where the ghost planes land (local row 0 of that buffer; p's own by default)
+    if (!dst) dst = p;
     if (g_comm.nranks == 1) {
         if (!emulated_multi(M)) return 0;
         // force_comm 2: one rank sends a slab plane's worth of its first rows
@@ -1085,11 +1111,11 @@ int enqueue_halo(hpccg_hip_matrix* M, double* p, hipStream_t st)
     const int r = g_comm.rank;
     NCCL_TRY(ncclGroupStart());
     if (r > 0) {
-        if (M->ghost_lo) NCCL_TRY(ncclRecv(p - M->ghost_lo, M->ghost_lo, ncclFloat64, r - 1, g_comm.comm, st));
+        if (M->ghost_lo) NCCL_TRY(ncclRecv(dst - M->ghost_lo, M->ghost_lo, ncclFloat64, r - 1, g_comm.comm, st));
         if (M->send_lo) NCCL_TRY(ncclSend(p, M->send_lo, ncclFloat64, r - 1, g_comm.comm, st));
     }
     if (r < g_comm.nranks - 1) {
-        if (M->ghost_hi) NCCL_TRY(ncclRecv(p + M->nrow, M->ghost_hi, ncclFloat64, r + 1, g_comm.comm, st));
+        if (M->ghost_hi) NCCL_TRY(ncclRecv(dst + M->nrow, M->ghost_hi, ncclFloat64, r + 1, g_comm.comm, st));
         if (M->send_hi) NCCL_TRY(ncclSend(p + M->nrow - M->send_hi, M->send_hi, ncclFloat64, r + 1, g_comm.comm, st));
     }
     NCCL_TRY(ncclGroupEnd());
@@ -1176,18 +1202,20 @@ int group_halo(const Ranks& R, int k_host, bool prologue)
         HIP_TRY(hipEventRecord(R.ev[r], R.M[r]->stream));
     }
     auto p_of = [&](int r) { return prologue ? R.a[r].p : ring_p(R.a[r], k_host); };
+    auto dst_of = p_of;
     for (int r = 0; r < R.P; r++) {
         hpccg_hip_matrix* M = R.M[r];
         TRY(use_device(R, r));
         if (r > 0 && M->ghost_lo) {
             const hpccg_hip_matrix* L = R.M[r - 1];
             HIP_TRY(hipStreamWaitEvent(M->stream, R.ev[r - 1], 0));
-            TRY(member_copy(M, p_of(r) - M->ghost_lo, L, p_of(r - 1) + L->nrow - M->ghost_lo, M->ghost_lo, M->stream));
+            TRY(member_copy(M, dst_of(r) - M->ghost_lo, L, p_of(r - 1) + L->nrow - M->ghost_lo, M->ghost_lo,
+                            M->stream));
         }
         if (r < R.P - 1 && M->ghost_hi) {
             const hpccg_hip_matrix* U = R.M[r + 1];
             HIP_TRY(hipStreamWaitEvent(M->stream, R.ev[r + 1], 0));
-            TRY(member_copy(M, p_of(r) + M->nrow, U, p_of(r + 1), M->ghost_hi, M->stream));
+            TRY(member_copy(M, dst_of(r) + M->nrow, U, p_of(r + 1), M->ghost_hi, M->stream));
         }
     }
     return 0;
@@ -1273,6 +1301,56 @@ int exch_allreduce(const Ranks& R, int which)
     return enqueue_allreduce(R.M[0], R.a[0], which);
 }
 
+// r-halo (rhalo_of): after the update, the r.r all-reduce and r's boundary
+// planes into the neighbours' r ghost planes. One RCCL group on a process's
+// communicator (force_comm 2: a plane-sized self send/recv of r, the shape of
+// the multi-rank iteration on one GPU); peer copies in an in-process group,
+// after the rank-ordered sum (whose stream waited for every member's update).
+int exch_rr_rhalo(const Ranks& R)
+{
+    if (R.P > 1) {
+        TRY(group_allreduce(R, kRR));
+        for (int r = 0; r < R.P; r++) {
+            hpccg_hip_matrix* M = R.M[r];
+            double* rr = R.a[r].r;
+            TRY(use_device(R, r));
+            if (r > 0 && M->ghost_lo)
+                TRY(member_copy(M, rr - M->ghost_lo, R.M[r - 1], R.a[r - 1].r + R.M[r - 1]->nrow - M->ghost_lo,
+                                M->ghost_lo, M->stream));
+            if (r < R.P - 1 && M->ghost_hi)
+                TRY(member_copy(M, rr + M->nrow, R.M[r + 1], R.a[r + 1].r, M->ghost_hi, M->stream));
+        }
+        return 0;
+    }
+    hpccg_hip_matrix* M = R.M[0];
+    const CgArgs& a = R.a[0];
+    if (!g_comm.comm) return 0;
+    // rhalo_group 1: the all-reduce and the planes in one RCCL group; 0: the
+    // all-reduce, then the planes' group
+    if (!M->rhalo_group) TRY(enqueue_allreduce(M, a, kRR));
+    NCCL_TRY(ncclGroupStart());
+    if (a.allreduce && M->rhalo_group)
+        NCCL_TRY(ncclAllReduce(a.loc + kRR, a.g + kRR, 1, ncclFloat64, ncclSum, g_comm.comm, M->stream));
+    if (g_comm.nranks == 1) {  // force_comm 2
+        const size_t cnt = emul_rows(M);
+        NCCL_TRY(ncclRecv(M->d_emul, cnt, ncclFloat64, 0, g_comm.comm, M->stream));
+        NCCL_TRY(ncclSend(a.r, cnt, ncclFloat64, 0, g_comm.comm, M->stream));
+    } else {
+        const int r = g_comm.rank;
+        if (r > 0) {
+            if (M->ghost_lo) NCCL_TRY(ncclRecv(a.r - M->ghost_lo, M->ghost_lo, ncclFloat64, r - 1, g_comm.comm, M->stream));
+            if (M->send_lo) NCCL_TRY(ncclSend(a.r, M->send_lo, ncclFloat64, r - 1, g_comm.comm, M->stream));
+        }
+        if (r < g_comm.nranks - 1) {
+            if (M->ghost_hi) NCCL_TRY(ncclRecv(a.r + M->nrow, M->ghost_hi, ncclFloat64, r + 1, g_comm.comm, M->stream));
+            if (M->send_hi)
+                NCCL_TRY(ncclSend(a.r + M->nrow - M->send_hi, M->send_hi, ncclFloat64, r + 1, g_comm.comm, M->stream));
+        }
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return 0;
+}
+
 // halo-dependent leading / trailing units of the kernel in use (-1: none known)
 void halo_units(const hpccg_hip_matrix* M, int* lo, int* hi)
 {
@@ -1309,7 +1387,7 @@ bool overlap_ok(const Ranks& R)
     // nor in the eager tail of a graph-replayed solve: there the first
     // overlapped iterations after the replays took ~60 ms each in an
     // in-process group (tools/probe/ovl_probe.py: 258 vs 75 ms per 100^3 solve)
-    if (g_capturing || R.M[0]->graph_used) return false;
+    if (g_capturing || R.M[0]->graph_used || R.a[0].rhalo) return false;  // (rhalo: no halo before the SpMV)
     for (int r = 0; r < R.P; r++) {
         const hpccg_hip_matrix* M = R.M[r];
         int lo, hi;
@@ -1334,20 +1412,21 @@ int enqueue_spmv_overlapped(const Ranks& R, int slot, int k_host)
         hpccg_hip_matrix* M = R.M[r];
         TRY(use_device(R, r));
         double* p = ring_p(R.a[r], k_host);
+        double* dst = p;  // where the ghost planes land
         if (R.P == 1) {
             HIP_TRY(hipStreamWaitEvent(M->stream2, M->ev_pb, 0));
-            TRY(enqueue_halo(M, p, M->stream2));
+            TRY(enqueue_halo(M, p, M->stream2, dst));
         } else {
             if (r > 0 && M->ghost_lo) {
                 const hpccg_hip_matrix* L = R.M[r - 1];
                 HIP_TRY(hipStreamWaitEvent(M->stream2, L->ev_pb, 0));
-                TRY(member_copy(M, p - M->ghost_lo, L, ring_p(R.a[r - 1], k_host) + L->nrow - M->ghost_lo,
+                TRY(member_copy(M, dst - M->ghost_lo, L, ring_p(R.a[r - 1], k_host) + L->nrow - M->ghost_lo,
                                 M->ghost_lo, M->stream2));
             }
             if (r < R.P - 1 && M->ghost_hi) {
                 const hpccg_hip_matrix* U = R.M[r + 1];
                 HIP_TRY(hipStreamWaitEvent(M->stream2, U->ev_pb, 0));
-                TRY(member_copy(M, p + M->nrow, U, ring_p(R.a[r + 1], k_host), M->ghost_hi, M->stream2));
+                TRY(member_copy(M, dst + M->nrow, U, ring_p(R.a[r + 1], k_host), M->ghost_hi, M->stream2));
             }
             // a member with no ghost still joins stream2 to its main stream
             if (!(r > 0 && M->ghost_lo) && !(r < R.P - 1 && M->ghost_hi))
@@ -1389,10 +1468,10 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
             TRY(use_device(R, r));
             if (!R.a[r].fuse_p)
                 launch_cg_p_update(R.a[r], R.M[r]->stream);
-            else if (multi && !R.M[r]->general)  // gather plan: k_pack computes the halo rows
+            else if (multi && !R.M[r]->general && !R.a[r].rhalo)  // gather plan: k_pack computes the halo rows
                 launch_cg_p_boundary(R.a[r], R.M[r]->send_lo, R.M[r]->send_hi, R.M[r]->stream);
         }
-        if (multi) TRY(exch_halo(R, k_host, false));
+        if (multi && !R.a[0].rhalo) TRY(exch_halo(R, k_host, false));  // (rhalo: r's planes came with r.r)
         for (int r = 0; r < R.P; r++) {
             hpccg_hip_matrix* M = R.M[r];
             CgArgs a = R.a[r];
@@ -1422,7 +1501,10 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 3], M->stream));
         if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, false, M->stream);
     }
-    TRY(exch_allreduce(R, kRR));
+    if (R.a[0].rhalo)
+        TRY(exch_rr_rhalo(R));
+    else
+        TRY(exch_allreduce(R, kRR));
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -1448,7 +1530,10 @@ int enqueue_prologue(const Ranks& R, bool events)
         if (events) HIP_TRY(hipEventRecord(M->ev[3], s));
         if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, true, s);  // rtrans, k = 1
     }
-    TRY(exch_allreduce(R, kRR));
+    if (R.a[0].rhalo)
+        TRY(exch_rr_rhalo(R));  // r_0's planes: iteration 1 forms p_1 = r_0 at the ghost rows
+    else
+        TRY(exch_allreduce(R, kRR));
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -1460,7 +1545,7 @@ int graph_chunk_of(const Ranks& R)
 {
     int chunk = std::max(1, R.M[0]->graph_iters);
     if (R.a[0].fupd) chunk += chunk & 1;  // the parity of k is baked into each captured launch
-    if (multi_of(R.M[0])) {
+    if (multi_of(R.M[0]) && !R.a[0].rhalo) {
         const int ring = R.a[0].nring;
         chunk = (chunk + ring - 1) / ring * ring;
     }
@@ -2490,6 +2575,13 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "spin_budget_us")) {
         if (value < 1 || value > 20000000LL) return set_err(HPCCG_HIP_EINVAL, "spin_budget_us must be 1..2e7");
         M->spin_us = value;
+    } else if (!std::strcmp(key, "rhalo_group")) {
+        // changes captured RCCL work that no kernel argument records: rebuild the graph
+        if (M->rhalo_group != (value ? 1 : 0) && M->graph_exec) {
+            (void)hipGraphExecDestroy(M->graph_exec);
+            M->graph_exec = nullptr;
+        }
+        M->rhalo_group = value ? 1 : 0;
     } else if (!std::strcmp(key, "dbg_withhold")) {
         if (value < 0 || value > M->nslices) return set_err(HPCCG_HIP_EINVAL, "dbg_withhold must be 0..nslices");
         M->dbg_withhold = (int)value;
@@ -2525,7 +2617,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "graph_chunk")) {  // effective: see graph_chunk_of
         long long c = std::max(1, M->graph_iters);
         if (fuse_update_effective(M)) c += c & 1;
-        if (multi_of(M)) {
+        if (multi_of(M) && !rhalo_of(M)) {
             const long long ring = x_defer_effective(M) ? x_ring_effective(M) : (fuse_p_effective(M) ? 2 : 1);
             c = (c + ring - 1) / ring * ring;
         }
@@ -2535,6 +2627,8 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "force_comm")) *value = M->force_comm;
     else if (!std::strcmp(key, "spin_budget_us")) *value = M->spin_us;
     else if (!std::strcmp(key, "dbg_withhold")) *value = M->dbg_withhold;
+    else if (!std::strcmp(key, "rhalo_group")) *value = M->rhalo_group;
+    else if (!std::strcmp(key, "rhalo")) *value = rhalo_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
     else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;
     else if (!std::strcmp(key, "stage16")) *value = M->stage16;

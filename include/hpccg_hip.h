@@ -159,10 +159,16 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   the dot slots are reset before the next solve
  *   "dbg_withhold"  debug (guard test): slice + 1 whose p.Ap partial is never
  *                   published, so the solve must time out (0 = off)
+ *   "rhalo_group"   multi-rank r-halo exchange (get "rhalo": in use; z-slab
+ *                   ranks with the p update fused): r's boundary planes move
+ *                   after the update into r's ghost planes and the SpMV forms
+ *                   p_k at ghost rows itself. 1 (default): the r.r all-reduce
+ *                   and the planes in one RCCL group; 0: the all-reduce first
  *   "event_timing"  1 = eager launches with hipEvents around every SpMV and
  *                   update (hpccg_hip_kernel_times)
  *   "fuse_p"        -1 auto / 0 off: p = r + beta p formed inside the SpMV
- *                   (pair kernel: any rank count; direct kernel: one rank)
+ *                   (pair and direct kernels; on several ranks with the z-slab
+ *                   plan, through the r-halo exchange below)
  *   "fold"          dots completed inside the producing kernel (self-validating
  *                   slots; tickets on unit-subset launches): 0 neither
  *                   (k_finalize), 1 both (auto), 2 p.Ap only, 3 r.r only

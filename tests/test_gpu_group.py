@@ -56,7 +56,8 @@ def test_group_matches_global_reference(hp, gpu, golden, name):
 def test_group_kernel_variants_bitwise(hp, gpu):
     """Multi-rank SpMV kernels (SELL-512 gather, SELL-512-A direct, SELL-512-A
     pair windows whose windows include the ghost planes), the p update fused
-    into the pair kernel (halo rows by k_p_boundary first), the halo
+    into the pair and direct kernels (halo rows by k_p_boundary first; the
+    direct kernel's halo lands in r's ghost planes), the halo
     overlapped with the interior units, the dot completion modes, the deferred
     x update and graph replay give the same bits."""
     hp.set_keep_sell(True)
@@ -76,8 +77,9 @@ def test_group_kernel_variants_bitwise(hp, gpu):
             M.set_option("use_graph", graph)
         if kernel > 0:  # graph replays run the halo in line (captured fork/join: DESIGN 6)
             assert Ms[1].get_option("overlap") == (ovl if not graph else 0)
-        # p = r + beta p inside the SpMV: the pair kernel only on multiple ranks
-        assert Ms[1].get_option("fuse_p") == (1 if (fuse and kernel == 2) else 0)
+        # p = r + beta p inside the SpMV on multiple ranks: the pair kernel, and the
+        # direct kernel with the halo received into r's ghost planes (z-slab plan)
+        assert Ms[1].get_option("fuse_p") == (1 if (fuse and kernel in (1, 2)) else 0)
         niters, normr, xs, _ = _solve_group(hp, Ms, max_iter=90)
         if graph:
             assert Ms[0].get_option("graph_used") == 1
