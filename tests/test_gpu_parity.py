@@ -15,6 +15,7 @@ work happens, never a value: the tests below require bitwise equal solves.
 """
 import itertools
 import math
+import os
 
 import numpy as np
 import pytest
@@ -419,23 +420,47 @@ def test_csr_entry_and_ragged_rows(hp, gpu):
 # and size-independent properties
 # ---------------------------------------------------------------------------
 def _oracle_trace(dims, s7, iters):
-    """The OpenMP oracle's first `iters` iterations on the same matrix."""
+    """The first `iters` iterations on the same matrix: the C restatement's
+    full trace (OpenMP), and -- where oracle/_ref is built -- the unmodified
+    reference HPCCG() (its OpenMP build, main.cpp's flags) at sampled
+    iterations k, by max_iter = k + 1 runs (the normr it returns is the one
+    computed in iteration k, HPCCG.cpp:358-373). Returns (trace, {k: normr}
+    or None)."""
     A = oracle.generate(*dims, use_7pt=s7)
-    ref = oracle.hpccg(A, max_iter=iters + 1, nthreads=max(1, min(16, oracle.max_threads())))
+    tr = oracle.hpccg(A, max_iter=iters + 1, nthreads=max(1, min(16, oracle.max_threads())))["trace"]
+    pts = None
+    if os.path.exists(oracle.REF_OMP_SO):
+        ks = sorted({k for k in (0, 1, 2, 3, 5, 8, 13, 21, 34, iters // 2, iters - 1) if 0 <= k < iters})
+        M = oracle.ref_from_csr(A, omp=True)
+        pts = {}
+        saved, null = os.dup(1), os.open(os.devnull, os.O_WRONLY)
+        os.dup2(null, 1)  # the reference prints its residual lines on fd 1
+        try:
+            for k in ks:
+                pts[k] = oracle.ref_hpccg(M, A.b, max_iter=k + 1)["normr"]
+        finally:
+            import ctypes
+            ctypes.CDLL(None).fflush(None)
+            os.dup2(saved, 1)
+            os.close(null)
+            os.close(saved)
+            M.close()
     del A
-    return ref["trace"]
+    return tr, pts
 
 
 @pytest.mark.parametrize("dims,s7,trace_iters", [((100, 100, 100), False, 90),
                                                   ((200, 200, 200), False, 60),
                                                   ((256, 256, 256), True, 60),
                                                   ((320, 320, 320), False, 0)])
-def test_full_size(hp, gpu, dims, s7, trace_iters):
+def test_full_size(hp, gpu, dims, s7, trace_iters, record_property):
     """BASELINE sizes (and 320^3: 32.8 M rows, 0.88 G nonzeros) on the default
-    kernel: the first iterations' rtrans against the OpenMP oracle on the same
-    matrix (1e-8), KAT-1 (A*1 == b bitwise), KAT-2 (rtrans_0 exact), KAT-4 (nnz
-    formula), the full 499-iteration solve's final residual and x, and the
-    device footprint (SELL-512 freed once the A image exists)."""
+    kernel: the first iterations' rtrans against the oracle on the same matrix
+    (1e-8) -- the unmodified reference build (oracle/_ref) at sampled
+    iterations where it is present, and the C restatement's full trace --,
+    KAT-1 (A*1 == b bitwise), KAT-2 (rtrans_0 exact), KAT-4 (nnz formula), the
+    full 499-iteration solve's final residual and x, and the device footprint
+    (SELL-512 freed once the A image exists)."""
     import torch
     M = hp.Matrix.generate(*dims, use_7pt=s7)
     info = M.info()
@@ -469,12 +494,22 @@ def test_full_size(hp, gpu, dims, s7, trace_iters):
     assert nr / tr[0] <= 1e-15
     assert (x - 1.0).abs().max().item() <= 1e-12
     if trace_iters:
-        ref = np.asarray(_oracle_trace(dims, s7, trace_iters))
+        ref, pts = _oracle_trace(dims, s7, trace_iters)
+        ref = np.asarray(ref)
         # every leading point above the 1e-20 cutoff (7-pt 256^3 passes it by k = 10)
         above = int(np.argmax(ref ** 2 < 1e-20 * ref[0] ** 2)) if np.any(ref ** 2 < 1e-20 * ref[0] ** 2) \
             else len(ref)
         assert above >= 10
         assert check_trace(tr, ref, RTRANS_RTOL_1GPU) == min(above, len(tr))
+        used = "C restatement (oracle/hpccg_oracle.c)"
+        if pts is not None:  # the reference build itself, where it is built (always here and on the GPU box)
+            used = f"reference build oracle/_ref (OpenMP) at k = {sorted(pts)} + C restatement"
+            for k, nr_ref in pts.items():
+                rr, rr_ref = tr[k] ** 2, nr_ref ** 2
+                if rr_ref >= 1e-20 * tr[0] ** 2:
+                    assert abs(rr - rr_ref) <= RTRANS_RTOL_1GPU * rr_ref, (k, tr[k], nr_ref)
+        record_property("oracle", used)
+        print(f"test_full_size{dims}: oracle = {used}")
 
 
 @pytest.mark.parametrize("dims,s7", [((1, 1, 1), False), ((2, 1, 1), False), ((3, 2, 1), False),
