@@ -111,7 +111,17 @@ struct CgArgs {
     int rhalo;
     int ghost_hi;                 // halo rows above (ghost_lo: below)
     int gbase;                    // first ghost block of the SpMV launch (set at launch; INT_MAX: none)
+    // peer-memory all-reduce of the two CG scalars (option peer_allreduce): the
+    // lane that completes a local dot stores it into slot [which][k & 1][prank]
+    // of every rank's mailbox (peers: device table of the ranks' mailboxes,
+    // IPC-mapped across processes), waits for all pranks slots of its own
+    // (mbox) and sums them in rank order -- no RCCL call, no launch
+    int peer_ar;
+    int prank, pranks;
+    double* mbox;
+    double* const* peers;
 };
+constexpr int kMboxSlots = 2 * 2 * 16;  // [dot][k & 1][rank], up to kMaxGroupRanks ranks
 
 // Bounded in-kernel waits: a wait that outlives the spin budget (s_memrealtime
 // ticks, 100 MHz) records itself in the device error record and ends the
@@ -137,6 +147,7 @@ enum DevError : int {
     kErrGroupWait = 1,  // a group's waiter: slice partials missing
     kErrTopWait = 2,    // the top waiter: group sums missing
     kErrReadyWait = 3,  // a fused update block: the launch's p.Ap total missing
+    kErrPeerWait = 4,   // peer all-reduce: another rank's contribution missing
 };
 constexpr long long kSpinTicksDefault = 100000000;  // 1 s
 

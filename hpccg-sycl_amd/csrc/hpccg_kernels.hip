@@ -433,6 +433,41 @@ __device__ __forceinline__ double top_sum_wave(Ld ld, int ng, int lane)
     return s;
 }
 
+// Peer-memory all-reduce of one CG scalar (MPI_Allreduce in ddot.cpp:79-80),
+// one lane: this rank's local sum into slot [which][k & 1][prank] of every
+// rank's mailbox (system-scope stores: the mailboxes of other GPUs are
+// IPC-mapped), then -- bounded -- until all pranks slots of its own mailbox
+// are full, and the sum in rank order from 0.0 (k_group_sum's order: bitwise
+// the in-process group's all-reduce). Its slots are emptied for iteration
+// k + 2, the next user of this parity; a rank writes them again only after it
+// has this rank's contributions to iteration k + 1, stored after the reset.
+// Returns NaN when the wait gave up (the solve is void then).
+__device__ __forceinline__ double peer_allreduce(const CgArgs& a, double s, int which, int k)
+{
+    const int base = (which * 2 + (k & 1)) * (kMboxSlots / 4);
+    for (int q = 0; q < a.pranks; q++)
+        __hip_atomic_store(a.peers[q] + base + a.prank, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    double* const mb = a.mbox + base;
+    unsigned t0 = 0, polls = 0;
+    for (;;) {
+        bool full = true;
+        for (int q = 0; q < a.pranks; q++)
+            full = full && slot_full(__hip_atomic_load(mb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        if (full) break;
+        if ((++polls & 15) == 0 && wait_expired(a, t0)) {
+            abort_solve(a, kErrPeerWait, which * 2 + (k & 1), k, which);
+            return __longlong_as_double(0x7FF8000000000000ll);
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    double tot = 0.0;
+    for (int q = 0; q < a.pranks; q++) tot += __hip_atomic_load(mb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int q = 0; q < a.pranks; q++)
+        __hip_atomic_store(mb + q, slot_empty(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return tot;
+}
+
 // The local total of a dot is known: publish it (k = the iteration it belongs
 // to). r.r closes iteration k: the next iteration is k + 1.
 // stamp_fin: the folded completion stamps the DDOT class here (k_finalize
@@ -440,7 +475,13 @@ __device__ __forceinline__ double top_sum_wave(Ld ld, int ng, int lane)
 __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which, int k, bool stamp_fin = true)
 {
     a.loc[which] = s;
-    if (!a.allreduce) a.g[which] = s;
+    if (a.peer_ar) {  // the global sum, in this kernel (the all-reduce class starts here)
+        stamp(a, k, which == kRR ? kStampArRR : kStampArPAP);
+        s = peer_allreduce(a, s, which, k);
+        a.g[which] = s;
+    } else if (!a.allreduce) {
+        a.g[which] = s;
+    }
     if (which == kRR) a.kst[a.fupd && ((k + 1) & 1) ? 2 : 0] = k + 1;
     if (a.fupd) {  // one copy per XCD group of update blocks, 128 B apart (no single hot line)
         for (int j = 0; j < kNumXcd; j++)
@@ -849,7 +890,7 @@ __device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
 {
     if ((int)blockIdx.x < a.gbase) return false;
     if (prologue) return true;
-    const int k = a.kst[0];
+    const int k = a.fupd ? iter_k<true>(a) : iter_k<false>(a);
     const double rr = a.g[kRR];
     if (!cg_run(a, k, true, rr)) return true;
     const double beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];

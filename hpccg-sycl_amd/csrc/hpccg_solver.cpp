@@ -264,6 +264,12 @@ struct hpccg_hip_matrix {
     int dbg_withhold = 0;      // debug: slice + 1 whose p.Ap partial is withheld (guard test)
     int solve_dirty = 0;       // a solve started and did not finish cleanly: reset the dot slots first
     int rhalo_group = 1;       // r-halo: the r.r all-reduce inside the planes' RCCL group (1) or before it (0)
+    // peer-memory all-reduce of the CG scalars (option peer_allreduce)
+    int peer_ar = 0;
+    double* d_mbox = nullptr;          // this rank's mailbox (kMboxSlots, uncached / fine-grained)
+    double** d_peers = nullptr;        // device table: every rank's mailbox, as this rank addresses it
+    int peers_for = 0;                 // ranks the table was built for (0: none)
+    std::vector<void*> ipc_opened;     // peers' mailboxes mapped from other processes
     double* d_hist = nullptr;
     unsigned long long* d_stamps = nullptr;
     double* d_emul = nullptr;  // force_comm 2: self-exchange receive buffer
@@ -323,6 +329,9 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_send_idx,   M->d_send_buf,  M->d_emul};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    for (void* p : M->ipc_opened) (void)hipIpcCloseMemHandle(p);
+    if (M->d_mbox) (void)hipFree(M->d_mbox);
+    if (M->d_peers) (void)hipFree(M->d_peers);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : {M->ev_pb, M->ev_halo})
         if (e) (void)hipEventDestroy(e);
@@ -872,6 +881,13 @@ bool rhalo_of(const hpccg_hip_matrix* M)
            (M->kernel == kSpmvDirect || M->kernel == kSpmvPairs);
 }
 
+// The peer-memory all-reduce (option peer_allreduce; RCCL stays the default):
+// on several ranks, or the 1-rank force_comm emulation. In an in-process group
+// the members' kernels wait for each other inside the GPU, so they must run
+// side by side: eager launches on their own streams, at most two members
+// (GPU_MAX_HW_QUEUES = 4 queues hold two members' two streams each).
+bool peer_ar_of(const hpccg_hip_matrix* M) { return M->peer_ar && multi_of(M) && (!M->in_group || M->nranks <= 2); }
+
 // Both dots folded into their producing kernels (slot completion, no
 // k_finalize launch): same-process A/B against p.Ap folded + r.r through
 // k_finalize, 100^3 19249 vs 17814 CG it/s, 200^3 2619 vs 2543, 7-pt 256^3
@@ -997,8 +1013,11 @@ int x_defer_effective(const hpccg_hip_matrix* M)
 bool fuse_update_effective(const hpccg_hip_matrix* M)
 {
     const bool want = M->fuse_update != 0;
-    return want && M->nranks == 1 && !M->in_group && !M->force_comm && M->kernel == kSpmvDirect &&
-           fuse_p_effective(M) && fold_effective(M) == 1 && x_defer_effective(M) == 2;
+    // several ranks: only with the in-kernel peer all-reduce (the update needs
+    // the global p.Ap inside the launch), and not in an in-process group
+    const bool ranks_ok = (M->nranks == 1 && !M->force_comm) || (peer_ar_of(M) && !M->in_group);
+    return want && ranks_ok && M->kernel == kSpmvDirect && fuse_p_effective(M) && fold_effective(M) == 1 &&
+           x_defer_effective(M) == 2;
 }
 
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
@@ -1047,6 +1066,14 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.rhalo = rhalo_of(M) ? 1 : 0;
     a.ghost_hi = M->ghost_hi;
     a.gbase = INT_MAX;  // set per launch
+    a.peer_ar = peer_ar_of(M) && M->d_peers ? 1 : 0;
+    if (a.peer_ar) {  // the scalars are summed inside the kernels: no RCCL all-reduce, no group sum
+        a.allreduce = 0;
+        a.prank = M->nranks > 1 ? M->rank : 0;
+        a.pranks = M->nranks;
+        a.mbox = M->d_mbox;
+        a.peers = M->d_peers;
+    }
     a.stamps = M->d_stamps;
     a.slice_base = M->d_slice_base;
     a.cols = M->d_cols;
@@ -1309,7 +1336,19 @@ int exch_allreduce(const Ranks& R, int which)
 int exch_rr_rhalo(const Ranks& R)
 {
     if (R.P > 1) {
-        TRY(group_allreduce(R, kRR));
+        if (R.a[0].allreduce) {
+            TRY(group_allreduce(R, kRR));
+        } else {  // peer all-reduce (in the kernels): only the copies' order on the members' streams
+            for (int r = 0; r < R.P; r++) {
+                TRY(use_device(R, r));
+                HIP_TRY(hipEventRecord(R.ev[r], R.M[r]->stream));
+            }
+            for (int r = 0; r < R.P; r++) {
+                TRY(use_device(R, r));
+                if (r > 0) HIP_TRY(hipStreamWaitEvent(R.M[r]->stream, R.ev[r - 1], 0));
+                if (r < R.P - 1) HIP_TRY(hipStreamWaitEvent(R.M[r]->stream, R.ev[r + 1], 0));
+            }
+        }
         for (int r = 0; r < R.P; r++) {
             hpccg_hip_matrix* M = R.M[r];
             double* rr = R.a[r].r;
@@ -1483,11 +1522,12 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
             if (!fold_of(a, kPAP)) launch_cg_finalize(a, kPAP, false, M->stream);
         }
     }
-    if (R.a[0].fupd) {  // one rank: the update ran inside the SpMV launch
+    if (R.a[0].fupd) {  // the update ran inside the SpMV launch (one rank, or the peer all-reduce)
         if (slot >= 0) {
             HIP_TRY(hipEventRecord(R.M[0]->ev[4 * slot + 2], R.M[0]->stream));
             HIP_TRY(hipEventRecord(R.M[0]->ev[4 * slot + 3], R.M[0]->stream));
         }
+        if (R.a[0].rhalo) TRY(exch_rr_rhalo(R));  // r's planes (the scalars were summed in the launch)
         HIP_TRY(hipGetLastError());
         return 0;
     }
@@ -1661,6 +1701,92 @@ int clear_state(hpccg_hip_matrix* M)
     return 0;
 }
 
+// A mailbox for the peer all-reduce: uncached device memory where the runtime
+// gives it (every load and store goes to memory: other GPUs write it over
+// xGMI), else fine-grained, else plain; every slot empty.
+int alloc_mbox(hpccg_hip_matrix* M, bool plain = false)
+{
+    const size_t bytes = sizeof(double) * kMboxSlots;
+    void* p = nullptr;
+    if (plain || hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+        if (plain || hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+            (void)hipGetLastError();
+            HIP_TRY(hipMalloc(&p, bytes));
+        }
+    }
+    M->d_mbox = static_cast<double*>(p);
+    const std::vector<unsigned long long> empty(kMboxSlots, kSlotEmpty);
+    HIP_TRY(hipMemcpy(M->d_mbox, empty.data(), bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+// The peer all-reduce's mailboxes and each rank's table of them (once per
+// rank count): an in-process group's members address each other's directly;
+// the ranks of an RCCL job exchange IPC handles of their mailboxes (one
+// all-gather over RCCL) and map them (hipIpcOpenMemHandle); the 1-rank
+// emulation addresses its own.
+int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
+{
+    hpccg_hip_matrix* M = Ms[0];
+    if (!peer_ar_of(M)) return 0;
+    const int nr = M->nranks;
+    if (nr > kMaxGroupRanks) return set_err(HPCCG_HIP_EINVAL, "peer_allreduce: at most %d ranks", kMaxGroupRanks);
+    bool ready = true;
+    for (int r = 0; r < P; r++) ready = ready && Ms[r]->peers_for == nr && Ms[r]->d_peers;
+    if (ready) return 0;
+    std::vector<std::vector<double*>> tables(P, std::vector<double*>(kMaxGroupRanks, nullptr));
+    if (P > 1 || nr == 1) {
+        for (int r = 0; r < P; r++) {
+            HIP_TRY(hipSetDevice(Ms[r]->device));
+            if (!Ms[r]->d_mbox) TRY(alloc_mbox(Ms[r]));
+        }
+        for (int r = 0; r < P; r++)
+            for (int q = 0; q < P; q++) tables[r][q] = Ms[q]->d_mbox;
+    } else {  // one process per GPU: IPC handles through RCCL
+        if (!g_comm.comm) return set_err(HPCCG_HIP_EINVAL, "peer_allreduce: no communicator");
+        if (!M->d_mbox) TRY(alloc_mbox(M));
+        hipIpcMemHandle_t h;
+        if (hipIpcGetMemHandle(&h, M->d_mbox) != hipSuccess) {  // not exportable: a plain allocation
+            (void)hipGetLastError();
+            (void)hipFree(M->d_mbox);
+            TRY(alloc_mbox(M, true));
+            HIP_TRY(hipIpcGetMemHandle(&h, M->d_mbox));
+        }
+        const size_t hb = sizeof(h);
+        unsigned char* d = nullptr;
+        HIP_TRY(hipMalloc(&d, hb * (nr + 1)));
+        HIP_TRY(hipMemcpy(d + hb * nr, &h, hb, hipMemcpyHostToDevice));
+        NCCL_TRY(ncclAllGather(d + hb * nr, d, hb, ncclUint8, g_comm.comm, M->stream));
+        HIP_TRY(hipStreamSynchronize(M->stream));
+        std::vector<unsigned char> all(hb * nr);
+        HIP_TRY(hipMemcpy(all.data(), d, hb * nr, hipMemcpyDeviceToHost));
+        (void)hipFree(d);
+        for (int q = 0; q < nr; q++) {
+            if (q == M->rank) {
+                tables[0][q] = M->d_mbox;
+                continue;
+            }
+            hipIpcMemHandle_t hq;
+            std::memcpy(&hq, all.data() + hb * q, hb);
+            void* ptr = nullptr;
+            HIP_TRY(hipIpcOpenMemHandle(&ptr, hq, hipIpcMemLazyEnablePeerAccess));
+            M->ipc_opened.push_back(ptr);
+            tables[0][q] = static_cast<double*>(ptr);
+        }
+    }
+    for (int r = 0; r < P; r++) {
+        hpccg_hip_matrix* Mr = Ms[r];
+        HIP_TRY(hipSetDevice(Mr->device));
+        if (!Mr->d_peers) HIP_TRY(hipMalloc(&Mr->d_peers, sizeof(double*) * kMaxGroupRanks));
+        HIP_TRY(hipMemcpy(Mr->d_peers, tables[r].data(), sizeof(double*) * kMaxGroupRanks, hipMemcpyHostToDevice));
+        Mr->peers_for = nr;
+    }
+    HIP_TRY(hipSetDevice(M->device));
+    return 0;
+}
+
 // After a failed solve: every dot slot empty again, tickets re-armed, the
 // error record cleared, so the next solve starts from the allocation state.
 int reset_dot_state(hpccg_hip_matrix* M)
@@ -1670,6 +1796,8 @@ int reset_dot_state(hpccg_hip_matrix* M)
     const std::vector<unsigned long long> empty(M->npartial, kSlotEmpty);
     HIP_TRY(hipMemcpyAsync(M->d_partial, empty.data(), M->npartial * sizeof(double), hipMemcpyHostToDevice, M->stream));
     HIP_TRY(hipMemsetAsync(M->d_tickets, 0, sizeof(unsigned int) * M->ntickets, M->stream));
+    if (M->d_mbox)
+        HIP_TRY(hipMemcpyAsync(M->d_mbox, empty.data(), sizeof(double) * kMboxSlots, hipMemcpyHostToDevice, M->stream));
     TRY(clear_state(M));
     HIP_TRY(hipStreamSynchronize(M->stream));
     return 0;
@@ -1739,6 +1867,7 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
         }
     }
     HIP_TRY(hipSetDevice(M->device));
+    TRY(ensure_peers(Ms, P));
     const auto t_begin = std::chrono::steady_clock::now();
     for (int r = 0; r < P; r++) {
         HIP_TRY(hipSetDevice(Ms[r]->device));
@@ -1770,7 +1899,9 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     int done = 0;
     M->graph_used = 0;
     const int chunk = graph_chunk_of(R);
-    if (!events && M->use_graph && !M->graph_failed && one_device && iters >= chunk) {
+    // (an in-process group with the peer all-reduce: its members' kernels wait
+    // for each other, so they are never serialised into one graph)
+    if (!events && M->use_graph && !M->graph_failed && one_device && iters >= chunk && !(P > 1 && av[0].peer_ar)) {
         // kernel arguments are baked into the graph: rebuild only when they change
         bool same = M->graph_exec && (int)M->graph_args.size() == P && M->graph_kernel == M->kernel &&
                     M->graph_chunk == chunk;
@@ -2575,6 +2706,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "spin_budget_us")) {
         if (value < 1 || value > 20000000LL) return set_err(HPCCG_HIP_EINVAL, "spin_budget_us must be 1..2e7");
         M->spin_us = value;
+    } else if (!std::strcmp(key, "peer_allreduce")) {
+        M->peer_ar = value ? 1 : 0;
     } else if (!std::strcmp(key, "rhalo_group")) {
         // changes captured RCCL work that no kernel argument records: rebuild the graph
         if (M->rhalo_group != (value ? 1 : 0) && M->graph_exec) {
@@ -2628,6 +2761,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "spin_budget_us")) *value = M->spin_us;
     else if (!std::strcmp(key, "dbg_withhold")) *value = M->dbg_withhold;
     else if (!std::strcmp(key, "rhalo_group")) *value = M->rhalo_group;
+    else if (!std::strcmp(key, "peer_allreduce")) *value = peer_ar_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "rhalo")) *value = rhalo_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
     else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;

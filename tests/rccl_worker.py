@@ -40,6 +40,15 @@ def main():
     check_final(it, nr, tr, rr["niters"], unhex(rr["normr"]), ref_tr, 500)
     assert (x - 1.0).abs().max().item() <= 1e-12
     assert times[4] > 0.0 and times[5] > 0.0
+    # the peer-memory all-reduce (IPC-mapped mailboxes, summed in the kernels,
+    # the update fused into the SpMV launch): two ranks, so the rank-order sum
+    # is RCCL's sum bit for bit -- the whole solve must be
+    got = (it, nr, tr.tobytes(), x.cpu().numpy().tobytes())
+    M.set_option("peer_allreduce", 1)
+    x.zero_()
+    _, it2, nr2, _ = hp.HPCCG(M, b, x, max_iter=500, device=True)
+    assert M.get_option("peer_allreduce") == 1 and M.get_option("fuse_update") == (1 if M.get_option("spmv_kernel") == 1 else 0)
+    assert (it2, nr2, M.last_trace().tobytes(), x.cpu().numpy().tobytes()) == got
     print(f"RCCL-WORKER-OK rank {rank} graph_used={M.get_option('graph_used')}", flush=True)
     M.close()
     hp.comm_destroy()
