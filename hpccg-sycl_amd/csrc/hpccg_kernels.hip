@@ -886,11 +886,14 @@ __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
 // all-reduced beta: the same bits the reference's halo would carry
 // (exchange_externals.cpp:87-126). Read as p_{k-1} by the next launch only.
 // ---------------------------------------------------------------------------
+// kFU: the launch's instantiation (a.fupd is set only with the direct kernel;
+// a run-time choice here cost the 7-pt fused instantiation 26 VGPRs)
+template <bool kFU>
 __device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
 {
     if ((int)blockIdx.x < a.gbase) return false;
     if (prologue) return true;
-    const int k = a.fupd ? iter_k<true>(a) : iter_k<false>(a);
+    const int k = iter_k<kFU>(a);
     const double rr = a.g[kRR];
     if (!cg_run(a, k, true, rr)) return true;
     const double beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
@@ -1077,7 +1080,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
         if (fused_update(a, prologue)) return;
     }
     if (side_flush<1, kW == 7 ? 8 : 4, kFU>(a, prologue)) return;
-    if (ghost_store(a, prologue)) return;
+    if (ghost_store<kFU>(a, prologue)) return;
     IterState st;
     if (!spmv_begin<kFuse, kFU>(a, prologue, st)) return;
     if (s < 0) return;
@@ -1324,7 +1327,7 @@ __device__ __forceinline__ void pair_epilogue(const CgArgs& a, const IterState& 
 template <bool kNT, bool kFuse, int kPre>
 __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2(CgArgs a, bool prologue)
 {
-    if (ghost_store(a, prologue)) return;
+    if (ghost_store<false>(a, prologue)) return;
     extern __shared__ __attribute__((aligned(16))) double xs[];
     const int P = unit_of(a);  // pair: all, or the interior / halo runs
     const int half = threadIdx.x / kBlock;
@@ -1403,7 +1406,7 @@ template <bool kFuse, int kW, int kR>
 __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2r(CgArgs a, bool prologue)
 {
     if (side_flush<2, 16>(a, prologue)) return;
-    if (ghost_store(a, prologue)) return;
+    if (ghost_store<false>(a, prologue)) return;
     static_assert(kR >= 1 && kR <= kA2RingMax && kR <= kW, "ring depth");
     extern __shared__ __attribute__((aligned(16))) double xs[];
     const int P = unit_of(a);
