@@ -57,7 +57,8 @@ import time
 # thread to its first place). The box's share is OMP_NUM_THREADS (16 there);
 # spread over cores, so the threads reach more memory channels than 16
 # neighbouring cores would (the reference is memory-bound on the host too).
-AFFINITY_CPUS = len(os.sched_getaffinity(0))
+AFFINITY_MASK = sorted(os.sched_getaffinity(0))
+AFFINITY_CPUS = len(AFFINITY_MASK)
 os.environ.setdefault("OMP_NUM_THREADS", str(AFFINITY_CPUS))
 os.environ.setdefault("OMP_PROC_BIND", "spread")
 os.environ.setdefault("OMP_PLACES", "cores")
@@ -107,9 +108,11 @@ def host_cpu():
 
 
 def physical_cores():
-    """Physical cores (distinct package/core ids) among this process's CPUs."""
+    """Physical cores (distinct package/core ids) among this process's CPUs,
+    from the mask read at start-up (libgomp later binds the main thread to
+    one place, so the mask at call time can be a single CPU)."""
     cores = set()
-    for c in os.sched_getaffinity(0):
+    for c in AFFINITY_MASK:
         t = f"/sys/devices/system/cpu/cpu{c}/topology"
         try:
             with open(f"{t}/physical_package_id") as f1, open(f"{t}/core_id") as f2:

@@ -172,7 +172,19 @@ def main():
     if bench:
         out["bench_avg_launch_us"] = bench["roofline"]["avg_launch_us"]
         out["bench_value"] = bench["value"]
-        shutil.copy(bench_log, os.path.join(outdir, "bench_line.json"))
+        shutil.copy(bench_log, os.path.join(outdir, "bench_line.json"))  # as printed
+        # the same line with roofline.traffic from THIS run's PMC passes (bench.py
+        # reads the committed profiles/pmc_*.json, which predate this run)
+        ann = json.loads(json.dumps(bench))
+        rl = ann["roofline"]
+        t = spmv_read + spmv_write
+        rl["traffic"] = t
+        rl["traffic_source"] = (f"profiles/{tag}/summary.json: rocprofv3 FETCH_SIZE (x{fetch_factor:.4f}, calibrated on "
+                                f"k_stream_a) + WRITE_SIZE passes of this evidence run (separate processes)")
+        rl["traffic_gbs"] = round(t / (rl["avg_launch_us"] * 1e3), 1)
+        rl["traffic_frac"] = round(rl["traffic_gbs"] / rl["peak"], 4)
+        with open(os.path.join(outdir, "bench_line_with_traffic.json"), "w") as f:
+            json.dump(ann, f)
     with open(os.path.join(ROOT, "profiles", f"pmc_spmv_{stencil}pt_{n}.json"), "w") as f:
         json.dump(out, f, indent=1)
     with open(os.path.join(outdir, "summary.json"), "w") as f:
