@@ -99,6 +99,7 @@ def lib() -> C.CDLL:
         "hpccg_hip_kernel_times_iter": (ip, [vp, PD, ip]),
         "hpccg_hip_diag_spmv": (ip, [vp, ip, ip, PD]),
         "hpccg_hip_diag_slot_plan": (ip, [ip, ip, ip, ip, PI, ip, PI]),
+        "hpccg_hip_diag_timeline": (ip, [vp, C.POINTER(C.c_uint64), ip]),
         "hpccg_hip_sparsemv": (ip, [vp, vp, vp]),
         "hpccg_hip_ddot": (ip, [ip, vp, vp, PD]),
         "hpccg_hip_waxpby": (ip, [ip, dp, vp, dp, vp, vp]),
@@ -321,6 +322,17 @@ class Matrix:
         us = C.c_double(0.0)
         _check(lib().hpccg_hip_diag_spmv(self.h, kernel, reps, C.byref(us)), "diag_spmv")
         return us.value
+
+    def diag_timeline(self) -> np.ndarray:
+        """Block timeline of the last ring-pair SpMV launch that ran an
+        iteration (option dbg_timeline 1): one row of 8 words per unit --
+        block | HW_ID << 32, five s_memrealtime stamps (entry, state, staged,
+        slots done, epilogue done; 100 MHz), XCC id, iteration k."""
+        cap = (int(self.info()["nrow"]) + 511) // 512  # >= the units of any SpMV launch
+        out = np.zeros(cap * 8, np.uint64)
+        n = lib().hpccg_hip_diag_timeline(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), cap)
+        _check(n if n < 0 else 0, "diag_timeline")
+        return out[:8 * n].reshape(n, 8)
 
     def last_trace(self, cap: int = 100000) -> np.ndarray:
         out = np.zeros(cap, np.float64)

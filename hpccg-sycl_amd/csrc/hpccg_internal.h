@@ -104,6 +104,9 @@ struct CgArgs {
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
+    int pgrid;                    // persistent ring pair kernel (k_spmv_a2p): its unit blocks; 0 off
+    unsigned long long* dbg_tl;   // diagnostics (option dbg_timeline): per unit 8 words of block clock stamps
+                                  // (kTlWords below); null off. Only the timeline instantiation writes it.
     // r-halo exchange (multi-rank z-slabs, fused p update): the halo moves r's
     // boundary planes (with the r.r all-reduce) into r's ghost planes; the SpMV
     // forms p_k = r + beta p_{k-1} at ghost rows itself, and its ghost blocks
@@ -121,6 +124,11 @@ struct CgArgs {
     double* mbox;
     double* const* peers;
 };
+// Block timeline (dbg_timeline), per unit of the ring pair kernel: [0] block
+// index | HW_ID << 32, [1] entry, [2] iteration state read, [3] windows staged
+// (after the barrier), [4] slot loop done, [5] epilogue + dot hand-off done
+// (s_memrealtime, 100 MHz), [6] XCC id, [7] iteration k.
+constexpr int kTlWords = 8;
 constexpr int kMboxSlots = 2 * 2 * 16;  // [dot][k & 1][rank], up to kMaxGroupRanks ranks
 
 // Bounded in-kernel waits: a wait that outlives the spin budget (s_memrealtime
@@ -189,6 +197,11 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s);
 constexpr int kA2RingDefault = 3;
 size_t a2_lds_bytes(int lds_doubles, int ring);
 int a2_ring_prepare();
+// The persistent form of the ring pair kernel (width 27, ring 3): its block
+// count on the current device (0: not available), and the largest pair
+// windows it stages through registers (5 rounds of 1024 doubles).
+constexpr int kA2pStageMax = 5 * 1024;
+int a2p_grid(int lds_doubles, int ring);
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s);
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);

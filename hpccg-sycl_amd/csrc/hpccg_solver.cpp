@@ -225,6 +225,7 @@ struct hpccg_hip_matrix {
     int stage16 = 1;      // pair kernel: 16-B staging of row pairs
     int nt_store = -1;    // CG vector stores non-temporal (-1 auto: nt_store_effective)
     int a2_ring = kA2RingDefault;  // pair kernel: LDS-DMA value ring depth per wave (0: register loads; uniform widths 27 and 7)
+    int a2_persist = 0;   // pair kernel: the persistent form (k_spmv_a2p) where it applies
     int tri = 1;          // direct kernel, width 7: x triple from adjacent lanes where the slice allows
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
@@ -262,6 +263,8 @@ struct hpccg_hip_matrix {
     int* d_kst = nullptr;      // [0, kErrBase) iteration state, then the device error record (kErrWords)
     long long spin_us = kSpinTicksDefault / 100;  // bound of every in-kernel wait (option spin_budget_us)
     int dbg_withhold = 0;      // debug: slice + 1 whose p.Ap partial is withheld (guard test)
+    unsigned long long* d_tl = nullptr;  // diagnostics (dbg_timeline): per unit kTlWords block stamps
+    int tl_units = 0;
     int solve_dirty = 0;       // a solve started and did not finish cleanly: reset the dot slots first
     int rhalo_group = 1;       // r-halo: the r.r all-reduce inside the planes' RCCL group (1) or before it (0)
     // peer-memory all-reduce of the CG scalars (option peer_allreduce)
@@ -326,7 +329,7 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_adiag2,     M->d_atri,      M->d_pbuf,    M->d_ahist,    M->d_rbuf,
                     M->d_Ap,         M->d_x,      M->d_b,         M->d_tickets,  M->d_scal,
                     M->d_kst,        M->d_hist,   M->d_stamps,    M->d_gen_b,   M->d_gen_x0,   M->d_gen_xexact,
-                    M->d_send_idx,   M->d_send_buf,  M->d_emul};
+                    M->d_send_idx,   M->d_send_buf,  M->d_emul,  M->d_tl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (void* p : M->ipc_opened) (void)hipIpcCloseMemHandle(p);
@@ -839,6 +842,24 @@ int a2_ring_effective(const hpccg_hip_matrix* M)
     return prepared == 0 ? M->a2_ring : 0;
 }
 
+// The persistent ring pair kernel: its unit blocks (a multiple of 8, at most
+// the launch's), 0 where it does not apply (ring depth 3 at width 27, the
+// pair windows within its register staging, the fused p update).
+bool fuse_p_effective(const hpccg_hip_matrix* M);
+bool peer_ar_of(const hpccg_hip_matrix* M);
+int grid_of(int units);
+int a2_persist_grid(const hpccg_hip_matrix* M)
+{
+    if (!M->a2_persist || a2_ring_effective(M) != 3 || M->a_width != 27 || !fuse_p_effective(M)) return 0;
+    // an in-process group with the peer all-reduce runs its members' kernels
+    // side by side on one GPU: no persistent grid claiming every CU there
+    if (M->in_group && peer_ar_of(M)) return 0;
+    const int units = (M->nslices + 1) / 2;
+    int g = a2p_grid(M->alds2_doubles, 3);
+    if (g > 0 && M->a2_persist > 1) g = std::min(g, M->a2_persist / kNumXcd * kNumXcd);  // tests: fewer blocks
+    return g > 0 ? std::min(g, grid_of(units)) : 0;
+}
+
 // Non-temporal stores of the CG vectors where the direct kernel streams an
 // image beyond the Infinity Cache: its x reads at the +-1-plane offsets live
 // on L2 reuse, which dirty Ap / p_k / r lines would crowd out. Same-process
@@ -1063,6 +1084,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.hist = M->d_hist;
     a.kst = M->d_kst;
     a.dbg_withhold = M->dbg_withhold;
+    a.dbg_tl = M->d_tl;
     a.rhalo = rhalo_of(M) ? 1 : 0;
     a.ghost_hi = M->ghost_hi;
     a.gbase = INT_MAX;  // set per launch
@@ -1090,6 +1112,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.awn2 = M->d_awn2;
     a.alds2_doubles = std::max(1, M->alds2_doubles);
     a.a2_ring = a2_ring_effective(M);
+    a.pgrid = a2_persist_grid(M);
     a.slots = 1;
     a.nt_store = nt_store_effective(M) ? 1 : 0;
     if (std::getenv("HPCCG_DEBUG_ADDR"))
@@ -2715,6 +2738,21 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
             M->graph_exec = nullptr;
         }
         M->rhalo_group = value ? 1 : 0;
+    } else if (!std::strcmp(key, "a2_persist")) {
+        if (value != 0 && value != 1 && (value < kNumXcd || value % kNumXcd))
+            return set_err(HPCCG_HIP_EINVAL, "a2_persist must be 0, 1 or a block count (a multiple of 8)");
+        M->a2_persist = (int)value;
+    } else if (!std::strcmp(key, "dbg_timeline")) {
+        if (value != 0 && value != 1) return set_err(HPCCG_HIP_EINVAL, "dbg_timeline must be 0 or 1");
+        HIP_TRY(hipSetDevice(M->device));
+        if (M->d_tl) {
+            dev_free(M, &M->d_tl, (size_t)M->tl_units * kTlWords);
+            M->tl_units = 0;
+        }
+        if (value) {
+            M->tl_units = M->nslices;  // >= the units of any SpMV launch (slices or pairs)
+            TRY(dev_alloc(M, &M->d_tl, (size_t)M->tl_units * kTlWords, true));
+        }  // the graph cache compares the kernel arguments: a changed dbg_tl re-captures
     } else if (!std::strcmp(key, "dbg_withhold")) {
         if (value < 0 || value > M->nslices) return set_err(HPCCG_HIP_EINVAL, "dbg_withhold must be 0..nslices");
         M->dbg_withhold = (int)value;
@@ -2760,6 +2798,9 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "force_comm")) *value = M->force_comm;
     else if (!std::strcmp(key, "spin_budget_us")) *value = M->spin_us;
     else if (!std::strcmp(key, "dbg_withhold")) *value = M->dbg_withhold;
+    else if (!std::strcmp(key, "dbg_timeline")) *value = M->d_tl ? 1 : 0;
+    else if (!std::strcmp(key, "a2_persist")) *value = a2_persist_grid(M) > 0 ? 1 : 0;
+    else if (!std::strcmp(key, "a2_persist_grid")) *value = a2_persist_grid(M);
     else if (!std::strcmp(key, "rhalo_group")) *value = M->rhalo_group;
     else if (!std::strcmp(key, "peer_allreduce")) *value = peer_ar_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "rhalo")) *value = rhalo_of(M) ? 1 : 0;
@@ -2855,6 +2896,17 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_u
     (void)hipEventDestroy(e1);
     *avg_us = 1e3 * ms / reps;
     return 0;
+}
+
+int hpccg_hip_diag_timeline(const hpccg_hip_matrix* M, unsigned long long* out, int cap)
+{
+    if (!M || !out) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    if (!M->d_tl) return set_err(HPCCG_HIP_EINVAL, "dbg_timeline is off");
+    const int n = std::min(cap, M->tl_units);
+    HIP_TRY(hipSetDevice(M->device));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    HIP_TRY(hipMemcpy(out, M->d_tl, (size_t)n * kTlWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return n;
 }
 
 int hpccg_hip_diag_slot_plan(int units, int grid, int spu, int rev, int* last_unit, int cap, int* top_group)

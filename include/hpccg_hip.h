@@ -157,6 +157,13 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   call returns HPCCG_HIP_EHIP naming the wait (block, group,
  *                   iteration, dot), every rank of an RCCL job returns it, and
  *                   the dot slots are reset before the next solve
+ *   "a2_persist"    ring pair kernel (width 27, ring 3, fused p): 1 = the
+ *                   persistent form (as many blocks as the CUs hold, each
+ *                   walking its XCD's pairs with the next pair's staging and
+ *                   ring slots overlapped), 0 = one block per pair; a multiple
+ *                   of 8 caps its blocks (tests). Same bits either way.
+ *   "dbg_timeline"  diagnostics: 1 = the ring pair kernel (width 27, ring 3)
+ *                   records a per-block timeline (hpccg_hip_diag_timeline)
  *   "dbg_withhold"  debug (guard test): slice + 1 whose p.Ap partial is never
  *                   published, so the solve must time out (0 = off)
  *   "rhalo_group"   multi-rank r-halo exchange (get "rhalo": in use; z-slab
@@ -224,6 +231,13 @@ int hpccg_hip_kernel_times_iter(const hpccg_hip_matrix* M, double* out, int cap)
  * resident p; kernel 9 streams the SELL-512-A values alone (8 B x slots read,
  * 8 B x n written: the rocprofv3 FETCH_SIZE calibration). */
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_us);
+/* Diagnostic (option dbg_timeline 1): per unit of the last SpMV launch that ran
+ * an iteration with the ring pair kernel at width 27, ring depth 3, kTlWords
+ * = 8 words: block index | HW_ID << 32, s_memrealtime stamps (100 MHz) at
+ * entry, iteration state read, windows staged, slot loop done, epilogue done,
+ * XCC id, iteration k. Up to cap units (cap x 8 words); returns the count.
+ * Replaces nothing in the reference (its TICK/TOCK classes are per kernel). */
+int hpccg_hip_diag_timeline(const hpccg_hip_matrix* M, unsigned long long* out, int cap);
 /* Diagnostic (host only, no GPU): the folded dot completion's plan for a
  * launch of `units` units (spu = 1 slice or 2 slices each) on `grid` blocks
  * dealt over the 8 XCDs (rev: the update's reversed order): for each group of

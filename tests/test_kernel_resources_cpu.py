@@ -21,7 +21,7 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 # demangled-name fragment -> max VGPRs (the occupancy step each default runs at)
 BUDGETS = {
     # 200^3 default: the ring pair kernel (LDS-bound at 2 blocks of 8 waves per CU)
-    "k_spmv_a2r<true, 27, 3>": 80,
+    "k_spmv_a2r<true, 27, 3, false>": 80,
     # 100^3 default: direct kernel, fused p, 4 early slots, fused update (6 waves)
     "k_spmv_a<27, false, true, 4, false, true>": 80,
     "k_spmv_a<27, false, true, 4, true, true>": 80,
