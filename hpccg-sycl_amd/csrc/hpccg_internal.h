@@ -105,6 +105,7 @@ struct CgArgs {
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
     int pgrid;                    // persistent ring pair kernel (k_spmv_a2p): its unit blocks; 0 off
+    int a2p_var;                  // k_spmv_a2p pipelining variant (A/B)
     unsigned long long* dbg_tl;   // diagnostics (option dbg_timeline): per unit 8 words of block clock stamps
                                   // (kTlWords below); null off. Only the timeline instantiation writes it.
     // r-halo exchange (multi-rank z-slabs, fused p update): the halo moves r's

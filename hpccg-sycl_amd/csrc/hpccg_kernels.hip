@@ -1540,13 +1540,20 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2r(CgArgs a, bool prologue
 // dot shape: the bits of k_spmv_a2r. Trailing blocks (index >= pgrid) run
 // the side-flush and ghost-store work of virtual blocks sgrid + (index - pgrid).
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr int a2p_stage_slot(int w, int r) { return w / 3 < w - r - 1 ? w / 3 : w - r - 1; }
+// The staging loads go after the last refill: vmcnt retires in issue order,
+// so every later wait on a ring slot would wait for them too (issued at slot
+// w / 3 they stalled the loop three slots later: 361 vs 337 us at 200^3).
+__host__ __device__ constexpr int a2p_stage_slot(int w, int r) { return w - r - 1; }
 
-template <int kW, int kR, int kU = 5>
+// kVar (A/B of the pipelining, option a2p_var): 0 as described; 1 the next
+// pair's ring slots issued after the dot hand-off, the epilogue barrier
+// draining (__syncthreads); 2 as 1, and the windows staged after the dot
+// hand-off too (k_spmv_a2r's order, persistent only).
+template <int kW, int kR, int kU = 5, int kVar = 0>
 __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2p(CgArgs a, bool prologue)
 {
     static_assert(kR >= 1 && kR <= kA2RingMax && kR + 1 < kW, "ring depth");
-    constexpr int kJS = a2p_stage_slot(kW, kR);  // staging loads issued after slot kJS's refill
+    constexpr int kJS = kVar == 2 ? kW : a2p_stage_slot(kW, kR);  // staging loads issued after slot kJS's refill
     constexpr int kStageOps = 2 * kU;            // r and p_{k-1}: one 16-B load each per round
     static_assert(kR - 1 + kStageOps <= 15, "vm_wait range");
     const int G = a.pgrid;
@@ -1635,15 +1642,18 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2p(CgArgs a, bool prologue
         }
     };
     auto stage_write = [&]() {  // p_k = r + beta p_{k-1} (k_p_update's expression)
+        d2v v[kU];  // every staged register consumed on every path: no load into them stays
+                    // pending (a later write to the register would wait for it, vmcnt(0))
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            v[u].x = sr[u].x + st.beta * sy[u].x;
+            v[u].y = sr[u].y + st.beta * sy[u].y;
+            asm volatile("" : "+v"(v[u].x), "+v"(v[u].y));  // here, on every path (not sunk into the branch)
+        }
 #pragma unroll
         for (int u = 0; u < kU; u++) {
             const int e = 2 * (int)threadIdx.x + 4 * kBlock * u;
-            if (e < stot) {
-                d2v v;
-                v.x = sr[u].x + st.beta * sy[u].x;
-                v.y = sr[u].y + st.beta * sy[u].y;
-                *reinterpret_cast<d2v*>(xs + e) = v;
-            }
+            if (e < stot) *reinterpret_cast<d2v*>(xs + e) = v[u];
         }
     };
     stage_load(P);
@@ -1694,7 +1704,7 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2p(CgArgs a, bool prologue
                 d = spmv_rows_out<true>(a, st, false, s * kSliceRows + lrow, sum);
             }
         }
-        if (P2 >= 0) {
+        if (kVar == 0 && P2 >= 0) {
             vp = vptr(P2);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -1702,8 +1712,12 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2p(CgArgs a, bool prologue
         }
         const double wv = wave_sum(d);
         if (lane == 0) wsum[threadIdx.x / kWave] = wv;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS only: the ring keeps streaming
-        __builtin_amdgcn_s_barrier();
+        if constexpr (kVar == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS only: the ring keeps streaming
+            __builtin_amdgcn_s_barrier();
+        } else {
+            __syncthreads();
+        }
         if (threadIdx.x < kWave) {
             constexpr int kWh = kBlock / kWave;
             double bs = 0.0;
@@ -1714,6 +1728,12 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2p(CgArgs a, bool prologue
             complete_dot_lanes(a, spmv_units(a, 2), P, 2 * P, min(2, a.nslices - 2 * P), bs, kPAP, st.k);
         }
         if (P2 < 0) break;
+        if constexpr (kVar != 0) {
+            vp = vptr(P2);
+#pragma unroll
+            for (int j = 0; j < kR; j++) ring_issue(vp, j);
+            if constexpr (kVar == 2) stage_load(P2);
+        }
         stage_write();  // the windows were read (epilogue) before the barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -2240,6 +2260,10 @@ int a2_ring_prepare()
                                 lim);
     if (e == hipSuccess)  // the persistent form
         e = hipFuncSetAttribute((const void*)k_spmv_a2p<27, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_spmv_a2p<27, 3, 5, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k_spmv_a2p<27, 3, 5, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     return e == hipSuccess ? 0 : -1;
 }
 
@@ -2306,8 +2330,13 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
             const size_t smem = a2_lds_bytes(a.alds2_doubles, a.a2_ring);
             if (fuse && a.pgrid > 0 && a.a_width == 27 && a.a2_ring == 3 && !a.dbg_tl && a.s0 == 0 && a.sn1 == 0 &&
                 a.sn0 == (a.nslices + 1) / 2) {  // persistent form: pgrid unit blocks + the trailing ones
-                hipLaunchKernelGGL((k_spmv_a2p<27, 3>), dim3(a.pgrid + nside + nghost), dim3(2 * kBlock), smem, s, b,
-                                   prologue);
+                const dim3 pg(a.pgrid + nside + nghost);
+                if (a.a2p_var == 1)
+                    hipLaunchKernelGGL((k_spmv_a2p<27, 3, 5, 1>), pg, dim3(2 * kBlock), smem, s, b, prologue);
+                else if (a.a2p_var == 2)
+                    hipLaunchKernelGGL((k_spmv_a2p<27, 3, 5, 2>), pg, dim3(2 * kBlock), smem, s, b, prologue);
+                else
+                    hipLaunchKernelGGL((k_spmv_a2p<27, 3>), pg, dim3(2 * kBlock), smem, s, b, prologue);
                 break;
             }
             if (fuse && a.dbg_tl && a.a_width == 27 && a.a2_ring == 3) {  // diagnostics: block timeline

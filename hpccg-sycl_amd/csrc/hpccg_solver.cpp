@@ -226,6 +226,7 @@ struct hpccg_hip_matrix {
     int nt_store = -1;    // CG vector stores non-temporal (-1 auto: nt_store_effective)
     int a2_ring = kA2RingDefault;  // pair kernel: LDS-DMA value ring depth per wave (0: register loads; uniform widths 27 and 7)
     int a2_persist = 0;   // pair kernel: the persistent form (k_spmv_a2p) where it applies
+    int a2p_var = 0;      // its pipelining variant (A/B)
     int tri = 1;          // direct kernel, width 7: x triple from adjacent lanes where the slice allows
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
@@ -1113,6 +1114,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.alds2_doubles = std::max(1, M->alds2_doubles);
     a.a2_ring = a2_ring_effective(M);
     a.pgrid = a2_persist_grid(M);
+    a.a2p_var = M->a2p_var;
     a.slots = 1;
     a.nt_store = nt_store_effective(M) ? 1 : 0;
     if (std::getenv("HPCCG_DEBUG_ADDR"))
@@ -2738,6 +2740,9 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
             M->graph_exec = nullptr;
         }
         M->rhalo_group = value ? 1 : 0;
+    } else if (!std::strcmp(key, "a2p_var")) {
+        if (value < 0 || value > 2) return set_err(HPCCG_HIP_EINVAL, "a2p_var must be 0..2");
+        M->a2p_var = (int)value;
     } else if (!std::strcmp(key, "a2_persist")) {
         if (value != 0 && value != 1 && (value < kNumXcd || value % kNumXcd))
             return set_err(HPCCG_HIP_EINVAL, "a2_persist must be 0, 1 or a block count (a multiple of 8)");
@@ -2801,6 +2806,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "dbg_timeline")) *value = M->d_tl ? 1 : 0;
     else if (!std::strcmp(key, "a2_persist")) *value = a2_persist_grid(M) > 0 ? 1 : 0;
     else if (!std::strcmp(key, "a2_persist_grid")) *value = a2_persist_grid(M);
+    else if (!std::strcmp(key, "a2p_var")) *value = M->a2p_var;
     else if (!std::strcmp(key, "rhalo_group")) *value = M->rhalo_group;
     else if (!std::strcmp(key, "peer_allreduce")) *value = peer_ar_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "rhalo")) *value = rhalo_of(M) ? 1 : 0;
