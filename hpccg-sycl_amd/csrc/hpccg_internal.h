@@ -104,8 +104,6 @@ struct CgArgs {
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
-    int pgrid;                    // persistent ring pair kernel (k_spmv_a2p): its unit blocks; 0 off
-    int a2p_var;                  // k_spmv_a2p pipelining variant (A/B)
     unsigned long long* dbg_tl;   // diagnostics (option dbg_timeline): per unit 8 words of block clock stamps
                                   // (kTlWords below); null off. Only the timeline instantiation writes it.
     // r-halo exchange (multi-rank z-slabs, fused p update): the halo moves r's
@@ -198,11 +196,6 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s);
 constexpr int kA2RingDefault = 3;
 size_t a2_lds_bytes(int lds_doubles, int ring);
 int a2_ring_prepare();
-// The persistent form of the ring pair kernel (width 27, ring 3): its block
-// count on the current device (0: not available), and the largest pair
-// windows it stages through registers (5 rounds of 1024 doubles).
-constexpr int kA2pStageMax = 5 * 1024;
-int a2p_grid(int lds_doubles, int ring);
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s);
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);

@@ -842,23 +842,15 @@ __host__ __device__ constexpr int side_blocks(int nslices, int nring, int spu)
     return ((nslices + nring - 2) / (nring - 1) + spu - 1) / spu;
 }
 
-// kVirt: vb is the block's index in the launch's block order (the persistent
-// pair kernel's trailing blocks stand for the blocks after its units); else
-// blockIdx.x. (Written out twice: the same expression through a parameter
-// raised the direct kernel's unfused instantiations from 67 to 75 VGPRs.)
-template <int kSpu, int kB, bool kFU = false, bool kVirt = false>
-__device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue, int vb = 0)
+template <int kSpu, int kB, bool kFU = false>
+__device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
 {
-    if constexpr (kVirt) {
-        if (vb < a.sgrid || vb >= a.gbase) return false;
-    } else {
-        if ((int)blockIdx.x < a.sgrid || (int)blockIdx.x >= a.gbase) return false;  // (gbase <= ubase)
-    }
+    if ((int)blockIdx.x < a.sgrid || (int)blockIdx.x >= a.gbase) return false;  // (gbase <= ubase)
     if (prologue) return true;
     const int k = iter_k<kFU>(a);
     if (k < 2 || !cg_run(a, k, false)) return true;
     const int q = a.nring - 1;
-    const int s = k % q + q * (kSpu * ((kVirt ? vb : (int)blockIdx.x) - a.sgrid) + (int)threadIdx.x / kBlock);
+    const int s = k % q + q * (kSpu * ((int)blockIdx.x - a.sgrid) + (int)threadIdx.x / kBlock);
     if (s >= a.nslices) return true;
     const int row = s * kSliceRows + (threadIdx.x % kBlock) * kRpt;
     // streamed once: non-temporal, so they do not displace the SpMV's window rows from L2
@@ -896,13 +888,10 @@ __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue, int v
 // ---------------------------------------------------------------------------
 // kFU: the launch's instantiation (a.fupd is set only with the direct kernel;
 // a run-time choice here cost the 7-pt fused instantiation 26 VGPRs)
-// bidx / vgrid: the block's index and the grid in the launch's block order
-// (as side_flush).
 template <bool kFU>
-__device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue, int bidx = (int)blockIdx.x,
-                                            int vgrid = (int)gridDim.x)
+__device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
 {
-    if (bidx < a.gbase) return false;
+    if ((int)blockIdx.x < a.gbase) return false;
     if (prologue) return true;
     const int k = iter_k<kFU>(a);
     const double rr = a.g[kRR];
@@ -911,8 +900,8 @@ __device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue, int 
     const double* __restrict__ pold = (k == 1) ? a.r : cur_p(a, k - 1);
     double* __restrict__ pk = cur_p(a, k);
     const int nlo = a.ghost_lo, tot = a.ghost_lo + a.ghost_hi;
-    const int stride = (vgrid - a.gbase) * (int)blockDim.x;
-    for (int i = (bidx - a.gbase) * (int)blockDim.x + (int)threadIdx.x; i < tot; i += stride) {
+    const int stride = (int)(gridDim.x - a.gbase) * (int)blockDim.x;
+    for (int i = ((int)blockIdx.x - a.gbase) * (int)blockDim.x + (int)threadIdx.x; i < tot; i += stride) {
         const int row = i < nlo ? i - nlo : a.n + (i - nlo);
         pk[row] = a.r[row] + beta * pold[row];
     }
@@ -1405,7 +1394,6 @@ __device__ __forceinline__ void vm_wait(int n)  // n: a constant after unrolling
 #define HPCCG_VMW(i) \
     case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
         HPCCG_VMW(0) HPCCG_VMW(1) HPCCG_VMW(2) HPCCG_VMW(3) HPCCG_VMW(4) HPCCG_VMW(5) HPCCG_VMW(6) HPCCG_VMW(7)
-        HPCCG_VMW(8) HPCCG_VMW(9) HPCCG_VMW(10) HPCCG_VMW(11) HPCCG_VMW(12) HPCCG_VMW(13) HPCCG_VMW(14) HPCCG_VMW(15)
 #undef HPCCG_VMW
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1516,229 +1504,6 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2r(CgArgs a, bool prologue
             o[6] = xcc;
             o[7] = (unsigned long long)st.k;
         }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent ring pair kernel (a.pgrid > 0: in-loop launches with the fused p
-// update over every unit, uniform width kW, ring depth kR). a.pgrid blocks
-// (as many as the CUs hold at once, a multiple of kNumXcd) walk the launch's
-// virtual blocks vb = blockIdx.x + i * pgrid: each block keeps its XCD
-// (vb % 8 == blockIdx.x % 8) and each XCD's blocks sweep its eighth of the
-// pairs in order, as the one-block-per-pair launch (k_spmv_a2r) does. Unit u
-// runs at virtual block unit_block(u), so the slot completion's waiter choice
-// (the largest block index) is unchanged: a waiter waits only for units of
-// smaller vb, which are done or running on co-resident blocks (the unit of
-// smallest vb not yet done is always running, and waits for nothing).
-// What k_spmv_a2r does serially per block is pipelined across units (block
-// timeline at 200^3, tools/timeline.py: window staging 20 % and the
-// epilogue 11 % of a block's 19.8 us, and a 1.2 us dispatch gap between
-// blocks): the next pair's window rows are loaded into registers during the
-// slot loop (after slot kJS), its first kR ring slots are issued right after
-// the loop, ahead of the epilogue, and its windows are written as soon as
-// the epilogue has read the current ones. Same products, same order, same
-// dot shape: the bits of k_spmv_a2r. Trailing blocks (index >= pgrid) run
-// the side-flush and ghost-store work of virtual blocks sgrid + (index - pgrid).
-// ---------------------------------------------------------------------------
-// The staging loads go after the last refill: vmcnt retires in issue order,
-// so every later wait on a ring slot would wait for them too (issued at slot
-// w / 3 they stalled the loop three slots later: 361 vs 337 us at 200^3).
-__host__ __device__ constexpr int a2p_stage_slot(int w, int r) { return w - r - 1; }
-
-// kVar (A/B of the pipelining, option a2p_var): 0 as described; 1 the next
-// pair's ring slots issued after the dot hand-off, the epilogue barrier
-// draining (__syncthreads); 2 as 1, and the windows staged after the dot
-// hand-off too (k_spmv_a2r's order, persistent only).
-template <int kW, int kR, int kU = 5, int kVar = 0>
-__global__ __launch_bounds__(2 * kBlock) void k_spmv_a2p(CgArgs a, bool prologue)
-{
-    static_assert(kR >= 1 && kR <= kA2RingMax && kR + 1 < kW, "ring depth");
-    constexpr int kJS = kVar == 2 ? kW : a2p_stage_slot(kW, kR);  // staging loads issued after slot kJS's refill
-    constexpr int kStageOps = 2 * kU;            // r and p_{k-1}: one 16-B load each per round
-    static_assert(kR - 1 + kStageOps <= 15, "vm_wait range");
-    const int G = a.pgrid;
-    if ((int)blockIdx.x >= G) {  // side-flush / ghost-store blocks
-        const int vb = a.sgrid + ((int)blockIdx.x - G);
-        if (side_flush<2, 16, false, true>(a, prologue, vb)) return;
-        ghost_store<false>(a, prologue, vb, a.sgrid + ((int)gridDim.x - G));
-        return;
-    }
-    extern __shared__ __attribute__((aligned(16))) double xs[];
-    __shared__ double wsum[2 * kBlock / kWave];
-    const int half = threadIdx.x / kBlock;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int lrow = (threadIdx.x % kBlock) * kRpt;  // row within the slice
-    const int prow = half * kSliceRows + lrow;       // row within the pair
-    double* __restrict__ ring = xs + ((a.alds2_doubles + 1) & ~1) + (threadIdx.x / kWave) * (kR * 2 * kWave);
-    const int per = a.sgrid / kNumXcd;
-    const int units = (a.nslices + 1) / 2;
-    auto unit_of_v = [&](int v) -> int {  // the launch covers every unit (host-checked)
-        if (v >= a.sgrid) return -1;
-        const int i = (v % kNumXcd) * per + v / kNumXcd;
-        return i < units ? i : -1;
-    };
-    // values of this wave's half of pair P_ (an odd last pair's second half
-    // streams its partner's values, never used)
-    auto vptr = [&](int P_) -> const double* {
-        const int s_ = 2 * P_ + half;
-        return a.aval + (size_t)(s_ < a.nslices ? s_ : s_ - 1) * kW * kSliceRows + lrow;
-    };
-    auto ring_issue = [&](const double* vp_, int j) {
-        __builtin_amdgcn_global_load_lds((const void*)(vp_ + (size_t)j * kSliceRows),
-                                         (lds_void*)(ring + (j % kR) * 2 * kWave), 16, 0, 2 /* nt */);
-    };
-    int vb = blockIdx.x;
-    int P = unit_of_v(vb);
-    if (P < 0) return;
-    const double* vp = vptr(P);
-#pragma unroll
-    for (int j = 0; j < kR; j++) ring_issue(vp, j);
-    // iteration state through the scalar cache (k_spmv_a2r's)
-    IterState st;
-    st.k = sld(a.kst);
-    st.rr = sld(a.g + kRR);
-    const double h1 = sld(a.hist + max(st.k - 2, 0));  // r_{k-2}.r_{k-2} (k >= 2)
-    const bool run = st.k < a.max_iter && sqrt(st.k == 1 ? st.rr : h1) > a.tol;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        publish_iter(a, st.k, run);
-        if (st.k == 1 || run) a.hist[st.k - 1] = st.rr;
-        if (run)
-            stamp(a, st.k, kStampSpmv);
-        else
-            mark_end(a);
-    }
-    if (!run) {
-        vm_wait(0);  // no DMA may land after the block's LDS is released
-        return;
-    }
-    st.beta = (st.k == 1) ? 0.0 : st.rr / h1;
-    const double* __restrict__ pold = (st.k == 1) ? a.r : cur_p(a, st.k - 1);
-    // window rows of pair P_ into registers: kU rounds of row pairs e = 2 t +
-    // 1024 u over the pair's LDS range [0, tot); every lane loads (clamped), so
-    // every wave issues exactly kStageOps loads (the slot loop counts them)
-    d2v sr[kU], sy[kU];
-    int stot = 0;
-    auto stage_load = [&](int P_) {
-        const int nw = sld(a.awn2 + P_);
-        const int* __restrict__ win = a.awin2 + (size_t)P_ * kAWin * 3;
-        int wlo[kAWin], wbase[kAWin];
-#pragma unroll
-        for (int w = 0; w < kAWin; w++) {
-            wlo[w] = w < nw ? sld(win + 3 * w) : 0;
-            wbase[w] = w < nw ? sld(win + 3 * w + 2) : INT_MAX;
-        }
-        stot = sld(win + 3 * (nw - 1) + 2) + sld(win + 3 * (nw - 1) + 1);
-        const int prow0 = 2 * P_ * kSliceRows;
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int e = min(2 * (int)threadIdx.x + 4 * kBlock * u, stot - 2);
-            int lo = wlo[0], base = wbase[0];
-#pragma unroll
-            for (int w = 1; w < kAWin; w++)
-                if (e >= wbase[w]) lo = wlo[w], base = wbase[w];
-            const int l = prow0 + lo + (e - base);  // local rows l, l + 1 (ghosts, guard zeros included)
-            sr[u] = *reinterpret_cast<const d2v*>(a.r + l);
-            sy[u] = *reinterpret_cast<const d2v*>(pold + l);
-        }
-    };
-    auto stage_write = [&]() {  // p_k = r + beta p_{k-1} (k_p_update's expression)
-        d2v v[kU];  // every staged register consumed on every path: no load into them stays
-                    // pending (a later write to the register would wait for it, vmcnt(0))
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            v[u].x = sr[u].x + st.beta * sy[u].x;
-            v[u].y = sr[u].y + st.beta * sy[u].y;
-            asm volatile("" : "+v"(v[u].x), "+v"(v[u].y));  // here, on every path (not sunk into the branch)
-        }
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int e = 2 * (int)threadIdx.x + 4 * kBlock * u;
-            if (e < stot) *reinterpret_cast<d2v*>(xs + e) = v[u];
-        }
-    };
-    stage_load(P);
-    stage_write();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    typedef const __attribute__((address_space(4))) int* cint_p;  // constant space: s_load
-    for (;;) {
-        const int vb2 = vb + G;
-        const int P2 = unit_of_v(vb2);
-        const int s = 2 * P + half;
-        const bool have = s < a.nslices;
-        const int su = __builtin_amdgcn_readfirstlane(have ? s : s - 1);
-        const cint_p cl = (cint_p)(a.alds2 + (size_t)su * kAMax);
-        int clv[kW];
-#pragma unroll
-        for (int j = 0; j < kW; j++) clv[j] = cl[j];
-        const int pd = a.adiag2 ? sld(a.adiag2 + su) : -1;  // LDS position of offset 0 (scalar: no vmcnt)
-        double sum[kRpt] = {0.0, 0.0};
-#pragma unroll
-        for (int j = 0; j < kW; j++) {
-            // slot j has landed: the ring DMAs issued after it, and the staging
-            // loads when they were issued after it
-            vm_wait((j + kR < kW ? j + kR : kW) - j - 1 + ((j > kJS && j <= kJS + kR) ? kStageOps : 0));
-            const d2v v = *reinterpret_cast<const d2v*>(ring + (j % kR) * 2 * kWave + 2 * lane);
-            const int c = prow + clv[j];
-            sum[0] = sum[0] + v.x * xs[c];
-            sum[1] = sum[1] + v.y * xs[c + 1];
-            asm volatile("" : "+v"(sum[0]), "+v"(sum[1]));  // keep the products here
-            if (j + kR < kW) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry read before its refill lands
-                ring_issue(vp, j + kR);
-            }
-            if (j == kJS) {
-                asm volatile("" ::: "memory");  // after the refill, in this order
-                stage_load(P2 >= 0 ? P2 : P);   // the last unit loads its own rows again (unused)
-                asm volatile("" ::: "memory");
-            }
-        }
-        // epilogue stores first (Ap, p_k from the window), then the next
-        // pair's first ring slots: a wait on slot 0 then counts only them
-        double d = 0.0;
-        if (have) {
-            if (pd >= 0 && a.lds_ep) {
-                const Rows pk{{xs[prow + pd], xs[prow + pd + 1]}};
-                d = spmv_rows_out<true>(a, st, false, s * kSliceRows + lrow, sum, &pk);
-            } else {
-                d = spmv_rows_out<true>(a, st, false, s * kSliceRows + lrow, sum);
-            }
-        }
-        if (kVar == 0 && P2 >= 0) {
-            vp = vptr(P2);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int j = 0; j < kR; j++) ring_issue(vp, j);
-        }
-        const double wv = wave_sum(d);
-        if (lane == 0) wsum[threadIdx.x / kWave] = wv;
-        if constexpr (kVar == 0) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS only: the ring keeps streaming
-            __builtin_amdgcn_s_barrier();
-        } else {
-            __syncthreads();
-        }
-        if (threadIdx.x < kWave) {
-            constexpr int kWh = kBlock / kWave;
-            double bs = 0.0;
-            if (lane < 2) {
-#pragma unroll
-                for (int i = 0; i < kWh; i++) bs += wsum[lane * kWh + i];
-            }
-            complete_dot_lanes(a, spmv_units(a, 2), P, 2 * P, min(2, a.nslices - 2 * P), bs, kPAP, st.k);
-        }
-        if (P2 < 0) break;
-        if constexpr (kVar != 0) {
-            vp = vptr(P2);
-#pragma unroll
-            for (int j = 0; j < kR; j++) ring_issue(vp, j);
-            if constexpr (kVar == 2) stage_load(P2);
-        }
-        stage_write();  // the windows were read (epilogue) before the barrier
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        P = P2;
-        vb = vb2;
     }
 }
 
@@ -2258,29 +2023,9 @@ int a2_ring_prepare()
     if (e == hipSuccess)  // the timeline diagnostic's instantiation
         e = hipFuncSetAttribute((const void*)k_spmv_a2r<true, 27, 3, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 lim);
-    if (e == hipSuccess)  // the persistent form
-        e = hipFuncSetAttribute((const void*)k_spmv_a2p<27, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_spmv_a2p<27, 3, 5, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)k_spmv_a2p<27, 3, 5, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     return e == hipSuccess ? 0 : -1;
 }
 
-// Blocks of the persistent ring pair kernel: as many as the device holds at
-// once (occupancy x CUs), a multiple of kNumXcd; 0 when it cannot run.
-int a2p_grid(int lds_doubles, int ring)
-{
-    if (ring != 3 || lds_doubles > kA2pStageMax) return 0;
-    int dev = 0, cus = 0, occ = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_spmv_a2p<27, 3>, 2 * kBlock,
-                                                     a2_lds_bytes(lds_doubles, ring)) != hipSuccess)
-        return 0;
-    return occ * cus / kNumXcd * kNumXcd;
-}
 
 // The SpMV of one CG iteration (or of the prologue). Template choice:
 //   kSpmvSell   k_spmv_sell, non-temporal above the Infinity Cache (a.nt)
@@ -2328,17 +2073,6 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     case kSpmvPairs: {
         if (a.a2_ring > 0) {
             const size_t smem = a2_lds_bytes(a.alds2_doubles, a.a2_ring);
-            if (fuse && a.pgrid > 0 && a.a_width == 27 && a.a2_ring == 3 && !a.dbg_tl && a.s0 == 0 && a.sn1 == 0 &&
-                a.sn0 == (a.nslices + 1) / 2) {  // persistent form: pgrid unit blocks + the trailing ones
-                const dim3 pg(a.pgrid + nside + nghost);
-                if (a.a2p_var == 1)
-                    hipLaunchKernelGGL((k_spmv_a2p<27, 3, 5, 1>), pg, dim3(2 * kBlock), smem, s, b, prologue);
-                else if (a.a2p_var == 2)
-                    hipLaunchKernelGGL((k_spmv_a2p<27, 3, 5, 2>), pg, dim3(2 * kBlock), smem, s, b, prologue);
-                else
-                    hipLaunchKernelGGL((k_spmv_a2p<27, 3>), pg, dim3(2 * kBlock), smem, s, b, prologue);
-                break;
-            }
             if (fuse && a.dbg_tl && a.a_width == 27 && a.a2_ring == 3) {  // diagnostics: block timeline
                 hipLaunchKernelGGL((k_spmv_a2r<true, 27, 3, true>), sg, dim3(2 * kBlock), smem, s, b, prologue);
                 break;

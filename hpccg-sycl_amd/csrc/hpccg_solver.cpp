@@ -225,8 +225,6 @@ struct hpccg_hip_matrix {
     int stage16 = 1;      // pair kernel: 16-B staging of row pairs
     int nt_store = -1;    // CG vector stores non-temporal (-1 auto: nt_store_effective)
     int a2_ring = kA2RingDefault;  // pair kernel: LDS-DMA value ring depth per wave (0: register loads; uniform widths 27 and 7)
-    int a2_persist = 0;   // pair kernel: the persistent form (k_spmv_a2p) where it applies
-    int a2p_var = 0;      // its pipelining variant (A/B)
     int tri = 1;          // direct kernel, width 7: x triple from adjacent lanes where the slice allows
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
@@ -843,24 +841,6 @@ int a2_ring_effective(const hpccg_hip_matrix* M)
     return prepared == 0 ? M->a2_ring : 0;
 }
 
-// The persistent ring pair kernel: its unit blocks (a multiple of 8, at most
-// the launch's), 0 where it does not apply (ring depth 3 at width 27, the
-// pair windows within its register staging, the fused p update).
-bool fuse_p_effective(const hpccg_hip_matrix* M);
-bool peer_ar_of(const hpccg_hip_matrix* M);
-int grid_of(int units);
-int a2_persist_grid(const hpccg_hip_matrix* M)
-{
-    if (!M->a2_persist || a2_ring_effective(M) != 3 || M->a_width != 27 || !fuse_p_effective(M)) return 0;
-    // an in-process group with the peer all-reduce runs its members' kernels
-    // side by side on one GPU: no persistent grid claiming every CU there
-    if (M->in_group && peer_ar_of(M)) return 0;
-    const int units = (M->nslices + 1) / 2;
-    int g = a2p_grid(M->alds2_doubles, 3);
-    if (g > 0 && M->a2_persist > 1) g = std::min(g, M->a2_persist / kNumXcd * kNumXcd);  // tests: fewer blocks
-    return g > 0 ? std::min(g, grid_of(units)) : 0;
-}
-
 // Non-temporal stores of the CG vectors where the direct kernel streams an
 // image beyond the Infinity Cache: its x reads at the +-1-plane offsets live
 // on L2 reuse, which dirty Ap / p_k / r lines would crowd out. Same-process
@@ -1113,8 +1093,6 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.awn2 = M->d_awn2;
     a.alds2_doubles = std::max(1, M->alds2_doubles);
     a.a2_ring = a2_ring_effective(M);
-    a.pgrid = a2_persist_grid(M);
-    a.a2p_var = M->a2p_var;
     a.slots = 1;
     a.nt_store = nt_store_effective(M) ? 1 : 0;
     if (std::getenv("HPCCG_DEBUG_ADDR"))
@@ -2740,13 +2718,6 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
             M->graph_exec = nullptr;
         }
         M->rhalo_group = value ? 1 : 0;
-    } else if (!std::strcmp(key, "a2p_var")) {
-        if (value < 0 || value > 2) return set_err(HPCCG_HIP_EINVAL, "a2p_var must be 0..2");
-        M->a2p_var = (int)value;
-    } else if (!std::strcmp(key, "a2_persist")) {
-        if (value != 0 && value != 1 && (value < kNumXcd || value % kNumXcd))
-            return set_err(HPCCG_HIP_EINVAL, "a2_persist must be 0, 1 or a block count (a multiple of 8)");
-        M->a2_persist = (int)value;
     } else if (!std::strcmp(key, "dbg_timeline")) {
         if (value != 0 && value != 1) return set_err(HPCCG_HIP_EINVAL, "dbg_timeline must be 0 or 1");
         HIP_TRY(hipSetDevice(M->device));
@@ -2804,9 +2775,6 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "spin_budget_us")) *value = M->spin_us;
     else if (!std::strcmp(key, "dbg_withhold")) *value = M->dbg_withhold;
     else if (!std::strcmp(key, "dbg_timeline")) *value = M->d_tl ? 1 : 0;
-    else if (!std::strcmp(key, "a2_persist")) *value = a2_persist_grid(M) > 0 ? 1 : 0;
-    else if (!std::strcmp(key, "a2_persist_grid")) *value = a2_persist_grid(M);
-    else if (!std::strcmp(key, "a2p_var")) *value = M->a2p_var;
     else if (!std::strcmp(key, "rhalo_group")) *value = M->rhalo_group;
     else if (!std::strcmp(key, "peer_allreduce")) *value = peer_ar_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "rhalo")) *value = rhalo_of(M) ? 1 : 0;

@@ -157,11 +157,6 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   call returns HPCCG_HIP_EHIP naming the wait (block, group,
  *                   iteration, dot), every rank of an RCCL job returns it, and
  *                   the dot slots are reset before the next solve
- *   "a2_persist"    ring pair kernel (width 27, ring 3, fused p): 1 = the
- *                   persistent form (as many blocks as the CUs hold, each
- *                   walking its XCD's pairs with the next pair's staging and
- *                   ring slots overlapped), 0 = one block per pair; a multiple
- *                   of 8 caps its blocks (tests). Same bits either way.
  *   "dbg_timeline"  diagnostics: 1 = the ring pair kernel (width 27, ring 3)
  *                   records a per-block timeline (hpccg_hip_diag_timeline)
  *   "dbg_withhold"  debug (guard test): slice + 1 whose p.Ap partial is never

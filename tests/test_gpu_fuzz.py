@@ -49,7 +49,6 @@ def _cases():
         max_iter = int(rng.integers(1, 91))
         early = bool(rng.integers(3) == 0)
         opts = {k: int(rng.choice(v)) for k, v in OPTIONS.items()}
-        opts["a2_persist"] = (0, 1, 8, 16)[i % 4]  # outside the rng stream: the earlier cases stay as they were
         out.append((i, (nx, ny, nz), s7, max_iter, early, opts))
     return out
 

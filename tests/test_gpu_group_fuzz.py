@@ -41,7 +41,6 @@ def _cases():
         nz = int(rng.integers(1, 9))
         max_iter = int(rng.integers(1, 61))
         opts = {k: int(rng.choice(v)) for k, v in OPTIONS.items()}
-        opts["a2_persist"] = (0, 1, 8, 16)[i % 4]  # outside the rng stream: the earlier cases stay as they were
         out.append((i, P, (nx, ny, nz), s7, max_iter, opts))
     return out
 

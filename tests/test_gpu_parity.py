@@ -130,21 +130,6 @@ def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
         M.set_option("use_graph", graph)
         assert M.get_option("x_defer") == 2
         out[("side", fuse, xring, graph)] = solve_bits(hp, M, prob.b, 120)
-    # the persistent form of the ring kernel (width 27): capped block counts
-    # make every block walk several pairs (8: one block per XCD), with the
-    # side blocks after them; graph replay and eager
-    if not s7:
-        for persist, graph, xring in ((1, 1, 32), (8, 0, 32), (16, 1, 5), (24, 1, 32), (8, 1, 2)):
-            M.set_option("fuse_p", -1)
-            M.set_option("a2_ring", -1)
-            M.set_option("x_defer", 2)
-            M.set_option("x_ring", xring)
-            M.set_option("use_graph", graph)
-            M.set_option("a2_persist", persist)
-            assert M.get_option("a2_persist") == 1
-            out[("persist", persist, graph, xring)] = solve_bits(hp, M, prob.b, 120)
-        M.set_option("a2_persist", 0)
-        M.set_option("x_ring", -1)
     M.set_option("a2_ring", 0)
     assert M.get_option("x_defer") == 1  # register-load pair kernel: batched in the update
     M.set_option("a2_ring", -1)
