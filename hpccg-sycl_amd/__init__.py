@@ -324,11 +324,11 @@ class Matrix:
         return us.value
 
     def diag_timeline(self) -> np.ndarray:
-        """Block timeline of the last ring-pair SpMV launch that ran an
-        iteration (option dbg_timeline 1): one row of 8 words per unit --
-        block | HW_ID << 32, five s_memrealtime stamps (entry, state, staged,
-        slots done, epilogue done; 100 MHz), XCC id, iteration k."""
-        cap = (int(self.info()["nrow"]) + 511) // 512  # >= the units of any SpMV launch
+        """Block timeline (option dbg_timeline 1) of the last SpMV launch
+        that ran an iteration, 8 words per row (include/hpccg_hip.h): the ring
+        pair kernel one row per pair, the direct kernel's fused-update
+        defaults one row per block of the launch."""
+        cap = 3 * ((int(self.info()["nrow"]) + 511) // 512) + 1024  # the buffer: every block of any launch
         out = np.zeros(cap * 8, np.uint64)
         n = lib().hpccg_hip_diag_timeline(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), cap)
         _check(n if n < 0 else 0, "diag_timeline")

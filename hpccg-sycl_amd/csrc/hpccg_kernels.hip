@@ -921,7 +921,7 @@ __device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
 // published, read with agent-scope loads. r is prefetched before the wait.
 // Saves the update's launch and ramp; bitwise the unfused iteration.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue)
+__device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue, unsigned long long* tw = nullptr)
 {
     if ((int)blockIdx.x < a.ubase) return false;
     if (prologue) return true;
@@ -960,6 +960,7 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue)
     }
     __syncthreads();
     if (gave_up) return true;
+    if (tw && threadIdx.x == 0) *tw = now_ticks();  // diagnostics (the timeline instantiation)
     const double alpha = rr / pap_s;
     if (bl == 0 && threadIdx.x == 0) {
         a.ahist[k] = alpha;
@@ -1059,7 +1060,33 @@ __host__ __device__ constexpr int tri_groups(int w) { return w == 7 ? 5 : 0; }
 __host__ __device__ constexpr int tri_first(int w, int g) { return g <= 2 ? g : g + 2; }
 __host__ __device__ constexpr int tri_size(int w, int g) { return g == 2 ? 3 : 1; }
 
-template <int kW, bool kNT, bool kFuse, int kPre, bool kTri = false, bool kFU = false>
+// Block timeline of the direct kernel (dbg_timeline, the kTL instantiations
+// of the 100^3 and 7-pt defaults): per block of the launch, kTlWords words --
+// block | HW_ID << 32, entry, state read (unit) / p.Ap ready (update block),
+// slot loop done (unit), end, role (0 unit, 1 side, 2 ghost, 3 update), XCC.
+// Each stamp is stored when it is taken, by every lane to the same word (one
+// store, no branch) through an asm store the compiler does not treat as a
+// memory operation: the diagnostic then holds no register across the kernel
+// and moves no load (a plain store, or a branch around it, cost occupancy
+// steps: 77 -> 255 VGPRs). No-op launches leave rows half written: read it
+// after an eager solve.
+__device__ __forceinline__ void tl_stamp(const CgArgs& a, int word)
+{
+    const unsigned long long t = now_ticks();
+    asm volatile("global_store_dwordx2 %0, %1, off" : : "v"(a.dbg_tl + (size_t)blockIdx.x * kTlWords + word), "v"(t));
+}
+__device__ __forceinline__ void tl_end(const CgArgs& a, int role)
+{
+    if (threadIdx.x != 0) return;
+    unsigned long long* o = a.dbg_tl + (size_t)blockIdx.x * kTlWords;
+    o[4] = now_ticks();
+    o[0] = (unsigned long long)blockIdx.x |
+           ((unsigned long long)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)) << 32);  // HW_ID
+    o[5] = (unsigned long long)role;
+    o[6] = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11));  // XCC_ID
+}
+
+template <int kW, bool kNT, bool kFuse, int kPre, bool kTri = false, bool kFU = false, bool kTL = false>
 __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 {
     static_assert(kPre == 0 || (kW > 0 && kPre <= kW), "early loads need the uniform width");
@@ -1076,14 +1103,27 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
             for (int j = 0; j < kW; j++) offp[j] = a.aoff[(size_t)s * kAMax + j];
         }
     }
-    if constexpr (kFU) {
+    if constexpr (kTL) tl_stamp(a, 1);  // entry (after the early loads: before them it cost 24 VGPRs)
+    if constexpr (kFU && kTL) {
+        if (fused_update(a, prologue, a.dbg_tl + (size_t)blockIdx.x * kTlWords + 2)) {
+            tl_end(a, 3);
+            return;
+        }
+    } else if constexpr (kFU) {
         if (fused_update(a, prologue)) return;
     }
-    if (side_flush<1, kW == 7 ? 8 : 4, kFU>(a, prologue)) return;
-    if (ghost_store<kFU>(a, prologue)) return;
+    if (side_flush<1, kW == 7 ? 8 : 4, kFU>(a, prologue)) {
+        if constexpr (kTL) tl_end(a, 1);
+        return;
+    }
+    if (ghost_store<kFU>(a, prologue)) {
+        if constexpr (kTL) tl_end(a, 2);
+        return;
+    }
     IterState st;
     if (!spmv_begin<kFuse, kFU>(a, prologue, st)) return;
     if (s < 0) return;
+    if constexpr (kTL) tl_stamp(a, 2);
     const int wdt = kW > 0 ? kW : (int)(a.abase[s + 1] - a.abase[s]);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
     const double* __restrict__ xr = cur_p(a, st.k) + row;  // x of column row + off at xr[off]
@@ -1138,10 +1178,12 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
                     triple(val(j0), val(j0 + 1), val(j0 + 2), offp[j0 + 1]);
                 }
             }
+            if constexpr (kTL) tl_stamp(a, 3);
             const double d = spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
             if (prologue) return;
             const double bs = block_sum<kBlock>(d);
             complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
+            if constexpr (kTL) tl_end(a, 0);
             return;
         }
     }
@@ -1168,10 +1210,12 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 #pragma unroll
         for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xv.v[i];
     }
+    if constexpr (kTL) tl_stamp(a, 3);
     const double d = spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
     if (prologue) return;
     const double bs = block_sum<kBlock>(d);
     complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
+    if constexpr (kTL) tl_end(a, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -2054,6 +2098,16 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     // update units: one slice per block, or two (a.fu2: four rows per thread)
     const int ugrid = a.fu2 ? (((a.nslices + 1) / 2 + kNumXcd - 1) / kNumXcd * kNumXcd) : a.grid;
     const dim3 sg(fu ? b.ubase + ugrid : a.sgrid + nside + nghost);
+    // diagnostics: the block-timeline instantiations of the two fused-update defaults
+    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 7 && a.nt && a.atri &&
+        (a.apre < 0 || a.apre == 7)) {
+        hipLaunchKernelGGL((k_spmv_a<7, true, true, 7, true, true, true>), sg, dim3(kBlock), 0, s, b, prologue);
+        return;
+    }
+    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 27 && !a.nt && a.apre != 0) {
+        hipLaunchKernelGGL((k_spmv_a<27, false, true, 4, false, true, true>), sg, dim3(kBlock), 0, s, b, prologue);
+        return;
+    }
 #define HPCCG_A(W, NT, PRE)                                                                                       \
     do {                                                                                                          \
         if (fu && a.atri && tri_groups(W) > 0 && PRE > 0)                                                       \

@@ -2726,7 +2726,7 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
             M->tl_units = 0;
         }
         if (value) {
-            M->tl_units = M->nslices;  // >= the units of any SpMV launch (slices or pairs)
+            M->tl_units = 3 * M->nslices + 1024;  // >= the blocks of any SpMV launch (units, side, ghost, update)
             TRY(dev_alloc(M, &M->d_tl, (size_t)M->tl_units * kTlWords, true));
         }  // the graph cache compares the kernel arguments: a changed dbg_tl re-captures
     } else if (!std::strcmp(key, "dbg_withhold")) {

@@ -226,12 +226,16 @@ int hpccg_hip_kernel_times_iter(const hpccg_hip_matrix* M, double* out, int cap)
  * resident p; kernel 9 streams the SELL-512-A values alone (8 B x slots read,
  * 8 B x n written: the rocprofv3 FETCH_SIZE calibration). */
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_us);
-/* Diagnostic (option dbg_timeline 1): per unit of the last SpMV launch that ran
- * an iteration with the ring pair kernel at width 27, ring depth 3, kTlWords
- * = 8 words: block index | HW_ID << 32, s_memrealtime stamps (100 MHz) at
+/* Diagnostic (option dbg_timeline 1): block timeline of the last SpMV launch
+ * that ran an iteration, 8 words per row, s_memrealtime stamps (100 MHz).
+ * Ring pair kernel (width 27, ring 3), one row per pair: block | HW_ID << 32,
  * entry, iteration state read, windows staged, slot loop done, epilogue done,
- * XCC id, iteration k. Up to cap units (cap x 8 words); returns the count.
- * Replaces nothing in the reference (its TICK/TOCK classes are per kernel). */
+ * XCC id, iteration k. Direct kernel with the fused update (the 100^3 and 7-pt
+ * defaults), one row per block of the launch: block | HW_ID << 32, entry,
+ * state read (unit block) or p.Ap ready (update block), slot loop done, end,
+ * role (0 unit, 1 side flush, 2 ghost store, 3 update), XCC id, 0. Up to cap
+ * rows (cap x 8 words); returns the row count. Replaces nothing in the
+ * reference (its TICK/TOCK classes are per kernel). */
 int hpccg_hip_diag_timeline(const hpccg_hip_matrix* M, unsigned long long* out, int cap);
 /* Diagnostic (host only, no GPU): the folded dot completion's plan for a
  * launch of `units` units (spu = 1 slice or 2 slices each) on `grid` blocks

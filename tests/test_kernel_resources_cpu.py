@@ -23,13 +23,13 @@ BUDGETS = {
     # 200^3 default: the ring pair kernel (LDS-bound at 2 blocks of 8 waves per CU)
     "k_spmv_a2r<true, 27, 3, false>": 80,
     # 100^3 default: direct kernel, fused p, 4 early slots, fused update (6 waves)
-    "k_spmv_a<27, false, true, 4, false, true>": 80,
-    "k_spmv_a<27, false, true, 4, true, true>": 80,
+    "k_spmv_a<27, false, true, 4, false, true, false>": 80,
+    "k_spmv_a<27, false, true, 4, true, true, false>": 80,
     # 7-pt 256^3 default: nt, fused p, 7 early slots, x triple, fused update (6 waves)
-    "k_spmv_a<7, true, true, 7, true, true>": 80,
+    "k_spmv_a<7, true, true, 7, true, true, false>": 80,
     # unfused direct kernel (several ranks over RCCL): 7 waves
-    "k_spmv_a<27, false, true, 4, false, false>": 72,
-    "k_spmv_a<7, true, true, 7, true, false>": 80,
+    "k_spmv_a<27, false, true, 4, false, false, false>": 72,
+    "k_spmv_a<7, true, true, 7, true, false, false>": 80,
     "k_update<false>": 64,
 }
 
