@@ -1748,12 +1748,25 @@ __device__ __forceinline__ void x_accumulate(const CgArgs& a, int row, int j0, i
 //           deferral the x update runs every nring iterations over the ring
 //           of p buffers, the same roundings in the same order.
 // ---------------------------------------------------------------------------
+// In the loop, Ap and r are loaded together with the iteration state, which
+// comes through the scalar cache (published by this iteration's SpMV launch):
+// the loop test no longer holds the loads back (a no-op launch after the end
+// loads them for nothing).
 template <bool kPrologue>
 __global__ __launch_bounds__(kBlock) void k_update(CgArgs a)
 {
     int k = 0;
+    const int s = a.rev ? xcd_slice_rev(a.grid) : xcd_slice(a.grid);
+    const int row = s * kSliceRows + threadIdx.x * kRpt;
+    Rows apv, rv;
     if constexpr (!kPrologue) {
-        const bool run = iter_of(a, k);
+        k = sld(a.kst + 4);  // publish_iter's {k, run}
+        const bool run = sld(a.kst + 5) != 0;
+        if (s < a.nslices) {
+            apv = ld(a.Ap + row);
+            rv = ld(a.r + row);
+        }
+        asm volatile("" ::: "memory");  // the loads stay ahead of the test
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             if (run)
                 stamp(a, k, kStampUpdate);
@@ -1762,22 +1775,19 @@ __global__ __launch_bounds__(kBlock) void k_update(CgArgs a)
         }
         if (!run) return;
     }
-    const int s = a.rev ? xcd_slice_rev(a.grid) : xcd_slice(a.grid);
     if (s >= a.nslices) return;
     double alpha = 0.0;
     if constexpr (!kPrologue) {
-        alpha = a.g[kRR] / a.g[kPAP];
+        alpha = sld(a.g + kRR) / sld(a.g + kPAP);
         if (blockIdx.x == 0 && threadIdx.x == 0) a.ahist[k] = alpha;
     }
-    const int row = s * kSliceRows + threadIdx.x * kRpt;
-    const Rows apv = ld(a.Ap + row);
     Rows rn;
     if constexpr (kPrologue) {
+        apv = ld(a.Ap + row);
         const Rows bv = ld(a.b + row);
 #pragma unroll
         for (int i = 0; i < kRpt; i++) rn.v[i] = bv.v[i] + (-1.0) * apv.v[i];
     } else {
-        const Rows rv = ld(a.r + row);
 #pragma unroll
         for (int i = 0; i < kRpt; i++) rn.v[i] = rv.v[i] + (-alpha) * apv.v[i];
         if (!a.xdefer) {
