@@ -83,7 +83,9 @@ def test_sparsemv_bitwise_vs_reference(hp, gpu, golden, keep_sell, kernel):
 
 
 @pytest.mark.parametrize("dims,s7", [((24, 20, 18), False), ((13, 7, 5), False), ((40, 40, 40), False),
-                                     ((32, 16, 40), True), ((17, 9, 11), True)])
+                                     ((32, 16, 40), True), ((17, 9, 11), True),
+                                     # pair windows past one staging round of the ring kernel (3 x 1866 > 5120)
+                                     ((420, 8, 24), False)])
 def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
     """SELL-512 gather, SELL-512-A direct and SELL-512-A pair windows, with the
     p update separate or formed inside the SpMV, give bitwise the same solve
