@@ -1191,8 +1191,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
             };
             auto val = [&](int j) -> Rows { return j < kPre ? vpre[j] : ld_m<kNT>(vp + (size_t)j * kSliceRows); };
             const int lane = threadIdx.x & (kWave - 1);
+            Rows ctr{{0.0, 0.0}};  // the triple's centre pair: x at the rows themselves when its offset is 0
             auto triple = [&](const Rows& v0, const Rows& v1, const Rows& v2, int o) {
                 const Rows c = xpair(o);
+                ctr = c;
                 double left = wave_shr1(c.v[1]);
                 double right = wave_shl1(c.v[0]);
                 if (lane == 0) left = x1(o - 1);
@@ -1217,7 +1219,11 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
                 }
             }
             if constexpr (kTL) tl_stamp(a, 3);
-            const double d = spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
+            // the rows' p_k is the triple's centre (offset 0: the same expression,
+            // so the same bits): no second read of r and p_{k-1} for the epilogue
+            constexpr int kCtr = tri_first(kW, 2) + 1;
+            const double d = offp[kCtr] == 0 ? spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum, &ctr)
+                                             : spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
             if (prologue) return;
             const double bs = block_sum<kBlock>(d);
             complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
