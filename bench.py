@@ -104,6 +104,16 @@ def host_cpu():
                 info[k] = v
     except Exception as e:  # reported, not fatal
         info["lscpu_error"] = repr(e)
+    # the process's CPU bandwidth quota (cgroup v2 cpu.max "quota period"): on a
+    # shared box it, not the affinity mask, bounds how many threads run at once
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        info["cgroup_cpu_max"] = f"{q} {per}"
+        if q != "max":
+            info["cgroup_cpu_quota_cores"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     return info
 
 
