@@ -277,6 +277,10 @@ struct hpccg_hip_matrix {
     double* d_emul = nullptr;  // force_comm 2: self-exchange receive buffer
     int hist_cap = 0;
     long long stamp_cap = 0;
+    // pinned readback of a solve's results (state, scalars, r.r history, timer
+    // stamps): one batch of async copies and one wait per solve
+    char* h_rb = nullptr;
+    size_t h_rb_bytes = 0;
     double *d_gen_b = nullptr, *d_gen_x0 = nullptr, *d_gen_xexact = nullptr;
     long long bytes = 0;       // device bytes held
     // hipGraph of graph_chunk iterations (kernel arguments are baked in)
@@ -332,6 +336,7 @@ int free_matrix(hpccg_hip_matrix* M)
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (void* p : M->ipc_opened) (void)hipIpcCloseMemHandle(p);
+    if (M->h_rb) (void)hipHostFree(M->h_rb);
     if (M->d_mbox) (void)hipFree(M->d_mbox);
     if (M->d_peers) (void)hipFree(M->d_peers);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -974,6 +979,12 @@ bool emulated_multi(const hpccg_hip_matrix* M)
 size_t emul_rows(const hpccg_hip_matrix* M) { return std::min<size_t>(M->nrow, 40000); }  // a 200^2 plane
 bool multi_of(const hpccg_hip_matrix* M) { return M->nranks > 1 || emulated_multi(M); }
 
+// Pinned readback layout: kst + error record (64 B), the scalars (64 B), then
+// hist (hist_cap doubles), then the stamps (stamp_cap words).
+constexpr size_t kRbScal = 64;
+constexpr size_t kRbHist = 128;
+static_assert(sizeof(int) * (kErrBase + kErrWords) <= kRbScal, "readback layout");
+
 int ensure_hist(hpccg_hip_matrix* M, int max_iter)
 {
     if (emulated_multi(M) && !M->d_emul) TRY(dev_alloc(M, &M->d_emul, emul_rows(M), true));
@@ -991,7 +1002,29 @@ int ensure_hist(hpccg_hip_matrix* M, int max_iter)
         TRY(dev_alloc(M, &M->d_stamps, (size_t)scap));
         M->stamp_cap = scap;
     }
+    const size_t rb = kRbHist + sizeof(double) * (size_t)M->hist_cap + sizeof(unsigned long long) * (size_t)M->stamp_cap;
+    if (rb > M->h_rb_bytes) {
+        if (M->h_rb) HIP_TRY(hipHostFree(M->h_rb));
+        M->h_rb = nullptr;
+        M->h_rb_bytes = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&M->h_rb), rb, hipHostMallocDefault));
+        M->h_rb_bytes = rb;
+    }
     return 0;
+}
+
+// Wait for a stream by polling it: a blocking wait on a solve-long stream
+// sleeps, and its wake-up cost 120-820 us per synchronous readback at the end
+// of a 200^3 solve (rocprof kernel trace, profiles/r03_200); polling returns
+// within microseconds.
+int wait_stream(hipStream_t st)
+{
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) return 0;
+        if (e != hipErrorNotReady) return set_err(HPCCG_HIP_EHIP, "hipStreamQuery: %s", hipGetErrorString(e));
+        __builtin_ia32_pause();
+    }
 }
 
 int grid_of(int units) { return std::max(kNumXcd, (units + kNumXcd - 1) / kNumXcd * kNumXcd); }
@@ -1951,17 +1984,26 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     if (P == 1 && M->nranks > 1 && !M->in_group && g_comm.comm)
         NCCL_TRY(ncclAllReduce(M->d_kst + kErrBase, M->d_kst + kErrBase + kErrAllRanks, 1, ncclInt32, ncclMax,
                                g_comm.comm, M->stream));
-    int kst[kErrBase + kErrWords];
-    HIP_TRY(hipMemcpyAsync(kst, M->d_kst, sizeof kst, hipMemcpyDeviceToHost, M->stream));
-    // (the fused update keeps k in kst[0] / kst[2] by parity: the later one is the count)
-    double scal[8];
-    HIP_TRY(hipMemcpyAsync(scal, M->d_scal, sizeof scal, hipMemcpyDeviceToHost, M->stream));
-    HIP_TRY(hipStreamSynchronize(M->stream));
+    // one batch of async copies into the pinned readback buffer, one wait:
+    // the state, the scalars, the r.r history and (times) the stamps
+    int* const kst = reinterpret_cast<int*>(M->h_rb);
+    double* const scal = reinterpret_cast<double*>(M->h_rb + kRbScal);
+    double* const hist = reinterpret_cast<double*>(M->h_rb + kRbHist);
+    unsigned long long* const stamps =
+        reinterpret_cast<unsigned long long*>(M->h_rb + kRbHist + sizeof(double) * (size_t)M->hist_cap);
+    const size_t nstamps = (size_t)(max_iter + 2) * kNumStampSlots;
+    HIP_TRY(hipMemcpyAsync(kst, M->d_kst, sizeof(int) * (kErrBase + kErrWords), hipMemcpyDeviceToHost, M->stream));
+    HIP_TRY(hipMemcpyAsync(scal, M->d_scal, sizeof(double) * 8, hipMemcpyDeviceToHost, M->stream));
+    if (max_iter > 0)
+        HIP_TRY(hipMemcpyAsync(hist, M->d_hist, sizeof(double) * max_iter, hipMemcpyDeviceToHost, M->stream));
+    if (times)
+        HIP_TRY(hipMemcpyAsync(stamps, M->d_stamps, sizeof(unsigned long long) * nstamps, hipMemcpyDeviceToHost,
+                               M->stream));
+    TRY(wait_stream(M->stream));
     const auto t_end = std::chrono::steady_clock::now();
     TRY(check_device_error(Ms, P, kst + kErrBase));
+    // (the fused update keeps k in kst[0] / kst[2] by parity: the later one is the count)
     const int niters = std::max(0, (av[0].fupd ? std::max(kst[0], kst[2]) : kst[0]) - 1);
-    std::vector<double> hist(std::max(1, niters));
-    if (niters > 0) HIP_TRY(hipMemcpy(hist.data(), M->d_hist, sizeof(double) * niters, hipMemcpyDeviceToHost));
     // normr after iteration k is sqrt(r_{k-1}.r_{k-1}) (HPCCG.cpp:371)
     M->trace.assign(niters + 1, 0.0);
     M->trace[0] = std::sqrt(niters > 0 ? hist[0] : scal[kRR]);
@@ -1999,8 +2041,7 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
                 std::cout << "Iteration = " << k << "   Residual = " << M->trace[k] << std::endl;
     }
     if (times) {
-        std::vector<unsigned long long> st((size_t)(max_iter + 2) * kNumStampSlots);
-        HIP_TRY(hipMemcpy(st.data(), M->d_stamps, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost));
+        const std::vector<unsigned long long> st(stamps, stamps + nstamps);
         stamps_to_times(st, max_iter, times);
         times[0] = std::chrono::duration<double>(t_end - t_begin).count();
     }
@@ -2817,8 +2858,7 @@ int hpccg_hip_solve_device(hpccg_hip_matrix* M, const double* b_dev, double* x_d
     }
     TRY(solve_impl(M, b, x, max_iter, tolerance, niters, normr, times, print));
     HIP_TRY(hipMemcpyAsync(x_dev, x, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
-    HIP_TRY(hipStreamSynchronize(M->stream));
-    return 0;
+    return wait_stream(M->stream);
 }
 
 int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tolerance, int* niters,
