@@ -950,8 +950,9 @@ __device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
 // kNumXcd copies 128 B apart, block b polls copy b mod kNumXcd, so no single
 // line takes every poll). Every unit block is dispatched before them and none
 // waits on them, so the wait ends. Ap comes from this launch's unit blocks on
-// any XCD: stored write-through, drained before their partials are
-// published, read with agent-scope loads. r is prefetched before the wait.
+// any XCD: stored write-through, drained (an explicit vmcnt(0) in every wave
+// before the block sum) before their partials are published, read with
+// agent-scope loads. r is prefetched before the wait.
 // Saves the update's launch and ramp; bitwise the unfused iteration.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue, unsigned long long* tw = nullptr)
@@ -1225,6 +1226,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
             const double d = offp[kCtr] == 0 ? spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum, &ctr)
                                              : spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
             if (prologue) return;
+            if constexpr (kFU) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Ap landed before the partial
             const double bs = block_sum<kBlock>(d);
             complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
             if constexpr (kTL) tl_end(a, 0);
@@ -1257,6 +1259,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
     if constexpr (kTL) tl_stamp(a, 3);
     const double d = spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
     if (prologue) return;
+    // fused update: this wave's write-through Ap has landed before the block's
+    // partial can be published (the update blocks read it once the p.Ap total
+    // is out); explicit, not left to how __syncthreads() lowers
+    if constexpr (kFU) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const double bs = block_sum<kBlock>(d);
     complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
     if constexpr (kTL) tl_end(a, 0);
