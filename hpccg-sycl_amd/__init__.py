@@ -100,6 +100,10 @@ def lib() -> C.CDLL:
         "hpccg_hip_diag_spmv": (ip, [vp, ip, ip, PD]),
         "hpccg_hip_diag_slot_plan": (ip, [ip, ip, ip, ip, PI, ip, PI]),
         "hpccg_hip_diag_timeline": (ip, [vp, C.POINTER(C.c_uint64), ip]),
+        "hpccg_hip_diag_realloc": (ip, [vp, ip]),
+        "hpccg_hip_probe_placement": (ip, [vp, ip]),
+        "hpccg_hip_diag_placement": (ip, [vp, PD, ip]),
+        "hpccg_hip_set_placement_probe": (ip, [ip]),
         "hpccg_hip_sparsemv": (ip, [vp, vp, vp]),
         "hpccg_hip_ddot": (ip, [ip, vp, vp, PD]),
         "hpccg_hip_waxpby": (ip, [ip, dp, vp, dp, vp, vp]),
@@ -243,6 +247,12 @@ def set_keep_sell(keep: bool) -> None:
     _check(lib().hpccg_hip_set_keep_sell(int(keep)), "set_keep_sell")
 
 
+def set_placement_probe(tries: int) -> None:
+    """Placement probe of matrices created afterwards: -1 auto (6 candidates
+    when the values exceed 512 MB), 0 off, 1..16 candidates."""
+    _check(lib().hpccg_hip_set_placement_probe(int(tries)), "set_placement_probe")
+
+
 SPMV_SELL, SPMV_DIRECT, SPMV_PAIRS = 0, 1, 2
 SPMV_KERNEL_NAMES = {0: "SELL-512 (int32 columns, x gathered)",
                      1: "SELL-512-A (offset-aligned slots, x read at the slice's offsets)",
@@ -335,6 +345,28 @@ class Matrix:
         n = lib().hpccg_hip_diag_timeline(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), cap)
         _check(n if n < 0 else 0, "diag_timeline")
         return out[:8 * n].reshape(n, 8)
+
+    def diag_realloc(self, which: int) -> None:
+        """Move a device buffer to new memory (0 values, 1 p ring, 2 r, 3 Ap,
+        4 x; diagnostics: physical placement)."""
+        _check(lib().hpccg_hip_diag_realloc(self.h, which), "diag_realloc")
+
+    def probe_placement(self, tries: int = 6) -> np.ndarray:
+        """Time CG iterations on the current placement, then on up to `tries`
+        contiguous placements of the values (keep the fastest), then of the p
+        ring (likewise); results unchanged. Returns placement()."""
+        _check(lib().hpccg_hip_probe_placement(self.h, int(tries)), "probe_placement")
+        return self.placement()
+
+    def placement(self) -> np.ndarray:
+        """us per CG iteration of each candidate of the last placement probe
+        ([0] the placement before it, then the values candidates, then the
+        ring candidates; empty if none ran). Option placement_pick: values
+        index | ring index << 8."""
+        out = np.zeros(33, np.float64)
+        n = lib().hpccg_hip_diag_placement(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), 33)
+        _check(n if n < 0 else 0, "diag_placement")
+        return out[:n]
 
     def last_trace(self, cap: int = 100000) -> np.ndarray:
         out = np.zeros(cap, np.float64)

@@ -114,6 +114,10 @@ struct GroupCtx {
 thread_local GroupCtx g_group_ctx;
 int g_halo_mode = 0;  // 0 auto (slab when it serves every rank), 1 slab only, 2 gather
 int g_keep_sell = 0;  // keep the SELL-512 image beside SELL-512-A (kernel A/B, diagnostics)
+int g_place_tries = -1;  // placement probe at creation: -1 auto, 0 off, n candidates
+constexpr int kPlaceAuto = 6;        // candidates of the automatic probe
+constexpr int kPlaceReps = 6;        // timed SpMV launches per candidate
+constexpr double kPlaceMinBytes = 512e6;  // auto: only images that stream from HBM
 int comm_nranks() { return g_group_ctx.active ? g_group_ctx.nranks : g_comm.nranks; }
 int comm_rank() { return g_group_ctx.active ? g_group_ctx.rank : g_comm.rank; }
 
@@ -281,6 +285,9 @@ struct hpccg_hip_matrix {
     // stamps): one batch of async copies and one wait per solve
     char* h_rb = nullptr;
     size_t h_rb_bytes = 0;
+    std::vector<void*> graveyard;  // diagnostics: buffers moved by hpccg_hip_diag_realloc, held until destroy
+    std::vector<double> place_us;  // placement probe: SpMV us per candidate (0 = the creation placement)
+    int place_pick = 0;            // the candidate kept
     double *d_gen_b = nullptr, *d_gen_x0 = nullptr, *d_gen_xexact = nullptr;
     long long bytes = 0;       // device bytes held
     // hipGraph of graph_chunk iterations (kernel arguments are baked in)
@@ -302,11 +309,25 @@ struct hpccg_hip_matrix {
 
 namespace {
 
+// Large device buffers (experiment, HPCCG_CONTIG=1): physically contiguous
+// allocations (hipDeviceMallocContiguous), falling back to hipMalloc.
+hipError_t big_malloc(void** p, size_t b)
+{
+    static const bool contig = [] {
+        const char* e = std::getenv("HPCCG_CONTIG");
+        return e && e[0] == '1';
+    }();
+    if (contig && b >= (16u << 20) && hipExtMallocWithFlags(p, b, hipDeviceMallocContiguous) == hipSuccess)
+        return hipSuccess;
+    (void)hipGetLastError();
+    return hipMalloc(p, b);
+}
+
 template <class T>
 int dev_alloc(hpccg_hip_matrix* M, T** p, size_t count, bool zero = false)
 {
     const size_t b = sizeof(T) * std::max<size_t>(1, count);
-    HIP_TRY(hipMalloc(p, b));
+    HIP_TRY(big_malloc(reinterpret_cast<void**>(p), b));
     if (zero) HIP_TRY(hipMemset(*p, 0, b));
     M->bytes += (long long)b;
     return 0;
@@ -337,6 +358,7 @@ int free_matrix(hpccg_hip_matrix* M)
         if (p) (void)hipFree(p);
     for (void* p : M->ipc_opened) (void)hipIpcCloseMemHandle(p);
     if (M->h_rb) (void)hipHostFree(M->h_rb);
+    for (void* p : M->graveyard) (void)hipFree(p);
     if (M->d_mbox) (void)hipFree(M->d_mbox);
     if (M->d_peers) (void)hipFree(M->d_peers);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -922,7 +944,7 @@ int alloc_ring(hpccg_hip_matrix* M, int nbuf)
     const size_t glo_pad = ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows;
     const size_t ptotal = (size_t)M->pstride * nbuf;
     double* buf = nullptr;
-    HIP_TRY(hipMalloc(&buf, sizeof(double) * ptotal));
+    HIP_TRY(big_malloc(reinterpret_cast<void**>(&buf), sizeof(double) * ptotal));
     if (hipMemset(buf, 0, sizeof(double) * ptotal) != hipSuccess) {
         (void)hipFree(buf);
         return set_err(HPCCG_HIP_EHIP, "hipMemset of the p ring failed");
@@ -2068,7 +2090,10 @@ int finish_matrix(hpccg_hip_matrix* M)
     TRY(build_a_image(M));
     if (M->has_a && !g_keep_sell) drop_sell(M);
     M->kernel = choose_kernel(M);
-    return alloc_workspace(M);
+    TRY(alloc_workspace(M));
+    if (g_place_tries == 0 || M->in_group || !M->has_a) return 0;
+    const int tries = g_place_tries > 0 ? g_place_tries : ((double)M->a_slots * 8.0 >= kPlaceMinBytes ? kPlaceAuto : 0);
+    return tries ? hpccg_hip_probe_placement(M, tries) : 0;
 }
 
 template <class RowLen, class RowAt>
@@ -2660,6 +2685,13 @@ int hpccg_hip_set_keep_sell(int keep)
     return 0;
 }
 
+int hpccg_hip_set_placement_probe(int tries)
+{
+    if (tries < -1 || tries > 16) return set_err(HPCCG_HIP_EINVAL, "placement probe: -1 (auto), 0 (off) or 1..16");
+    g_place_tries = tries;
+    return 0;
+}
+
 int hpccg_hip_matrix_destroy(hpccg_hip_matrix* M) { return free_matrix(M); }
 
 int hpccg_hip_matrix_info(const hpccg_hip_matrix* M, long long info[8])
@@ -2837,6 +2869,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_pairs ? M->alds2_doubles : 0;
     else if (!std::strcmp(key, "nt")) *value = image_big(M) ? 1 : 0;
     else if (!std::strcmp(key, "device_bytes")) *value = M->bytes;
+    else if (!std::strcmp(key, "placement_pick")) *value = M->place_pick;
     else return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
     return 0;
 }
@@ -2910,6 +2943,158 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_u
     (void)hipEventDestroy(e1);
     *avg_us = 1e3 * ms / reps;
     return 0;
+}
+
+// Physical placement probe: the CG iteration rate of a large
+// image depends on where in HBM its values and the p ring were placed (306-350
+// us per 200^3 SpMV on one box, same code, same virtual layout). Time a few
+// CG iterations on the creation placement and on `tries` physically
+// contiguous candidates (each allocated while the earlier ones are held, so
+// each lands elsewhere), keep the fastest, free the rest. Values are copied,
+// the ring is zeroed as alloc_ring leaves it; nothing else moves and no
+// result changes.
+constexpr int kPlaceIters = 10;  // CG iterations per candidate (eager, event-timed)
+
+// Median SpMV + update time (us) of iterations 2.. of a short eager solve on
+// scratch b, x. A rank of an RCCL job or a group member is timed as one rank
+// (no halo, no all-reduce: the probe must not make collective calls that the
+// other ranks' probes might not match; the ghost rows it leaves unwritten are
+// the ring's zeros).
+int probe_time(hpccg_hip_matrix* M, const double* b, double* x, double* us)
+{
+    const int nr = M->nranks, ev = M->event_timing, gr = M->use_graph;
+    M->nranks = 1;
+    M->event_timing = 1;
+    M->use_graph = 0;
+    int it = 0;
+    double normr = 0.0;
+    int rc = 0;
+    if (hipMemsetAsync(x, 0, sizeof(double) * std::max(1, M->nrow), M->stream) != hipSuccess)
+        rc = set_err(HPCCG_HIP_EHIP, "placement probe: hipMemsetAsync failed");
+    if (!rc) rc = solve_ranks(&M, 1, &b, &x, kPlaceIters, 0.0, &it, &normr, nullptr, 0);
+    M->nranks = nr;
+    M->event_timing = ev;
+    M->use_graph = gr;
+    if (rc) return rc;
+    std::vector<double> v;
+    for (int i = 2; i <= it; i++) v.push_back(M->kiter[2 * i] + M->kiter[2 * i + 1]);
+    if (v.empty()) return set_err(HPCCG_HIP_EINVAL, "placement probe: the solve ran %d iterations", it);
+    std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+    *us = 1e3 * v[v.size() / 2];
+    return 0;
+}
+
+int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
+{
+    if (!M) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    if (tries < 0 || tries > 16) return set_err(HPCCG_HIP_EINVAL, "tries must be 0..16");
+    M->place_us.clear();
+    M->place_pick = 0;
+    if (!tries || !M->has_a || !M->d_aval || !M->d_pbuf) return 0;
+    HIP_TRY(hipSetDevice(M->device));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    const size_t n = (size_t)std::max(1, M->nrow);
+    double* scratch = nullptr;  // b | x of the timed solves
+    HIP_TRY(hipMalloc(&scratch, 2 * sizeof(double) * n));
+    auto done = [&](int rc) {
+        (void)hipStreamSynchronize(M->stream);
+        (void)hipFree(scratch);
+        (void)hipGetLastError();  // a refused candidate allocation only ends a phase
+        M->trace.clear();         // the probe's solves are not the caller's
+        M->last_niters = 0;
+        M->kiter.clear();
+        for (double& t : M->ktimes) t = 0.0;
+        return rc;
+    };
+    // b: every 32-bit word 0x3ff00000 (each double ~1.0000002; only the rate matters)
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(scratch), 0x3ff00000u, 2 * n, M->stream) != hipSuccess)
+        return done(set_err(HPCCG_HIP_EHIP, "placement probe: hipMemsetD32Async failed"));
+    double us = 0.0;
+    int rc = probe_time(M, scratch, scratch + n, &us);
+    if (rc) return done(rc);
+    M->place_us.push_back(us);
+    double best_us = us;
+    // phase 0 places the values (copied), phase 1 the p ring (zeroed, as
+    // alloc_ring leaves it), each against the other's kept placement
+    const ptrdiff_t poff = M->d_p - M->d_pbuf;
+    for (int phase = 0; phase < 2; phase++) {
+        double** slot = phase == 0 ? &M->d_aval : &M->d_pbuf;
+        const size_t bytes = phase == 0 ? sizeof(double) * (size_t)std::max<long long>(1, M->a_slots)
+                                        : sizeof(double) * (size_t)M->pstride * M->ring_alloc;
+        auto set = [&](double* q) {
+            *slot = q;
+            if (phase == 1) M->d_p = q + poff;
+        };
+        std::vector<double*> cand{*slot};
+        size_t best = 0;
+        for (int t = 0; t < tries && !rc; t++) {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < bytes + (size_t(8) << 30)) break;  // headroom
+            double* q = nullptr;
+            if (hipExtMallocWithFlags(reinterpret_cast<void**>(&q), bytes, hipDeviceMallocContiguous) != hipSuccess)
+                break;
+            cand.push_back(q);
+            const hipError_t e = phase == 0 ? hipMemcpyAsync(q, cand[0], bytes, hipMemcpyDeviceToDevice, M->stream)
+                                            : hipMemsetAsync(q, 0, bytes, M->stream);
+            if (e != hipSuccess) {
+                rc = set_err(HPCCG_HIP_EHIP, "placement probe: filling candidate %d failed", t + 1);
+                break;
+            }
+            set(q);
+            rc = probe_time(M, scratch, scratch + n, &us);
+            if (rc) break;
+            M->place_us.push_back(us);
+            if (us < best_us) {
+                best_us = us;
+                best = cand.size() - 1;
+            }
+        }
+        if (rc) best = 0;
+        (void)hipStreamSynchronize(M->stream);  // no launch reads the others any more
+        set(cand[best]);
+        for (size_t i = 0; i < cand.size(); i++)
+            if (i != best) (void)hipFree(cand[i]);
+        if (phase == 1 && hipMemsetAsync(cand[best], 0, bytes, M->stream) != hipSuccess && !rc)
+            rc = set_err(HPCCG_HIP_EHIP, "placement probe: hipMemsetAsync failed");  // the solves' values
+        M->place_pick |= (int)best << (8 * phase);
+        if (rc) break;
+    }
+    return done(rc);
+}
+
+int hpccg_hip_diag_placement(const hpccg_hip_matrix* M, double* us_out, int cap)
+{
+    if (!M || (!us_out && cap > 0)) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    const int n = (int)M->place_us.size();
+    for (int i = 0; i < std::min(n, cap); i++) us_out[i] = M->place_us[i];
+    return n;
+}
+
+int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which)
+{
+    if (!M) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(M->device));
+    HIP_TRY(hipStreamSynchronize(M->stream));
+    double** buf;
+    size_t n;
+    switch (which) {
+    case 0: buf = &M->d_aval; n = (size_t)std::max<long long>(1, M->a_slots); break;
+    case 1: buf = &M->d_pbuf; n = (size_t)M->pstride * M->ring_alloc; break;
+    case 2: buf = &M->d_rbuf; n = (size_t)M->pstride; break;
+    case 3: buf = &M->d_Ap; n = M->npad; break;
+    case 4: buf = &M->d_x; n = M->npad; break;
+    default: return set_err(HPCCG_HIP_EINVAL, "which must be 0..4");
+    }
+    if (!*buf) return set_err(HPCCG_HIP_EINVAL, "buffer %d not allocated", which);
+    double* nb = nullptr;
+    HIP_TRY(big_malloc(reinterpret_cast<void**>(&nb), sizeof(double) * n));
+    HIP_TRY(hipMemcpy(nb, *buf, sizeof(double) * n, hipMemcpyDeviceToDevice));
+    M->graveyard.push_back(*buf);  // held: the new buffer gets other physical memory
+    const ptrdiff_t poff = M->d_p - M->d_pbuf, roff = M->d_r - M->d_rbuf;
+    *buf = nb;
+    if (which == 1) M->d_p = M->d_pbuf + poff;
+    if (which == 2) M->d_r = M->d_rbuf + roff;
+    return 0;  // the graph cache compares kernel arguments: the next solve re-captures
 }
 
 int hpccg_hip_diag_timeline(const hpccg_hip_matrix* M, unsigned long long* out, int cap)

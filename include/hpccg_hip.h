@@ -117,6 +117,11 @@ int hpccg_hip_set_halo_mode(int mode);
  * (process-wide; default 0 frees it once the A image exists). Only for
  * kernel A/B comparisons ("spmv_kernel" 0 on a stencil matrix). */
 int hpccg_hip_set_keep_sell(int keep);
+/* Placement probe of matrices created afterwards (process-wide): -1 auto
+ * (default: 6 candidates when the SELL-512-A values exceed 512 MB, off
+ * otherwise and for in-process group members), 0 off, 1..16 candidates. See
+ * hpccg_hip_probe_placement. Replaces nothing in the reference. */
+int hpccg_hip_set_placement_probe(int tries);
 /* nrow, ncol (incl. ghosts), stored nnz, matrix slots (incl. padding),
  * ghost_lo, ghost_hi, SpMV kernel, uniform slot count (0 = per slice). */
 int hpccg_hip_matrix_info(const hpccg_hip_matrix* M, long long info_out[8]);
@@ -226,6 +231,27 @@ int hpccg_hip_kernel_times_iter(const hpccg_hip_matrix* M, double* out, int cap)
  * resident p; kernel 9 streams the SELL-512-A values alone (8 B x slots read,
  * 8 B x n written: the rocprofv3 FETCH_SIZE calibration). */
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_us);
+/* Diagnostic: move one device buffer to a new allocation (contents copied;
+ * the old one is held until the matrix is destroyed, so the new one lands on
+ * other physical memory): 0 the SELL-512-A values, 1 the p ring, 2 r, 3 Ap,
+ * 4 x. For measuring the effect of physical placement on the kernels' rate.
+ * Replaces nothing in the reference. */
+int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which);
+/* The CG iteration rate of a large matrix depends on the physical HBM
+ * placement of its values and p ring (306-350 us per 200^3 SpMV on one box).
+ * Times a few eager CG iterations (median SpMV + update, scratch b and x; a
+ * rank of an RCCL job is timed alone, no collective call) on the current
+ * placement, then on up to `tries` physically contiguous placements of the
+ * values (copied) and keeps the fastest, then likewise of the p ring
+ * (zeroed); frees the rest. A phase stops early, keeping its best so far, when
+ * free memory falls below the candidate size + 8 GiB. Results are unchanged
+ * (bitwise). Option "placement_pick" reads the kept candidates: values index
+ * | ring index << 8 (0 = the placement before the probe). */
+int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries);
+/* The last probe's times (us per iteration: [0] the placement before the
+ * probe, then the values candidates, then the ring candidates): returns their
+ * count, copies up to cap. */
+int hpccg_hip_diag_placement(const hpccg_hip_matrix* M, double* us_out, int cap);
 /* Diagnostic (option dbg_timeline 1): block timeline of the last SpMV launch
  * that ran an iteration, 8 words per row, s_memrealtime stamps (100 MHz).
  * Ring pair kernel (width 27, ring 3), one row per pair: block | HW_ID << 32,
