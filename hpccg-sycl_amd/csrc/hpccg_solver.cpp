@@ -323,12 +323,23 @@ hipError_t big_malloc(void** p, size_t b)
     return hipMalloc(p, b);
 }
 
+// Host-to-device copy ordered on stream s, where the kernels (or RCCL calls)
+// that read it run: a plain hipMemcpy is ordered on the null stream, which the
+// library's non-blocking streams do not wait for (with pageable sources it
+// can return before the data has landed). Waits, so the source may go away.
+int h2d(hipStream_t s, void* dst, const void* src, size_t bytes)
+{
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return 0;
+}
+
 template <class T>
 int dev_alloc(hpccg_hip_matrix* M, T** p, size_t count, bool zero = false)
 {
     const size_t b = sizeof(T) * std::max<size_t>(1, count);
     HIP_TRY(big_malloc(reinterpret_cast<void**>(p), b));
-    if (zero) HIP_TRY(hipMemset(*p, 0, b));
+    if (zero) HIP_TRY(hipMemsetAsync(*p, 0, b, M->stream));  // ordered before M's kernels and copies
     M->bytes += (long long)b;
     return 0;
 }
@@ -498,7 +509,7 @@ int rccl_requests(hpccg_hip_matrix* M, GatherPlan& g)
     for (int q = 0; q < P; q++) mine[q] = (int)g.req[q].size();
     int* d = nullptr;
     HIP_TRY(hipMalloc(&d, sizeof(int) * (size_t)P * (P + 1)));
-    HIP_TRY(hipMemcpy(d, mine.data(), sizeof(int) * P, hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, d, mine.data(), sizeof(int) * P));
     NCCL_TRY(ncclAllGather(d, d + P, P, ncclInt32, g_comm.comm, M->stream));
     std::vector<int> cnt((size_t)P * P);
     HIP_TRY(hipMemcpyAsync(cnt.data(), d + P, sizeof(int) * P * P, hipMemcpyDeviceToHost, M->stream));
@@ -515,7 +526,7 @@ int rccl_requests(hpccg_hip_matrix* M, GatherPlan& g)
     HIP_TRY(hipMalloc(&din, sizeof(int) * std::max(1LL, nin)));
     std::vector<int> flat;
     for (int q = 0; q < P; q++) flat.insert(flat.end(), g.req[q].begin(), g.req[q].end());
-    if (nout) HIP_TRY(hipMemcpy(dout, flat.data(), sizeof(int) * nout, hipMemcpyHostToDevice));
+    if (nout) TRY(h2d(M->stream, dout, flat.data(), sizeof(int) * nout));
     NCCL_TRY(ncclGroupStart());
     long long oo = 0, oi = 0;
     for (int q = 0; q < P; q++) {
@@ -558,7 +569,7 @@ int install_gather(hpccg_hip_matrix* M, const GatherPlan& g)
     TRY(dev_alloc(M, &M->d_send_idx, M->nsend));
     TRY(dev_alloc(M, &M->d_send_buf, M->nsend));
     if (M->nsend)
-        HIP_TRY(hipMemcpy(M->d_send_idx, g.send_idx.data(), sizeof(int) * M->nsend, hipMemcpyHostToDevice));
+        TRY(h2d(M->stream, M->d_send_idx, g.send_idx.data(), sizeof(int) * M->nsend));
     return 0;
 }
 
@@ -591,7 +602,7 @@ int exchange_plan(hpccg_hip_matrix* M, int* mode = nullptr, std::vector<int>* al
     int* d = nullptr;
     HIP_TRY(hipMalloc(&d, sizeof(int) * 4 * (g_comm.nranks + 1)));
     int mine[4] = {M->nrow, M->ghost_lo, M->ghost_hi, M->start_row};
-    HIP_TRY(hipMemcpy(d, mine, sizeof mine, hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, d, mine, sizeof mine));
     NCCL_TRY(ncclAllGather(d, d + 4, 4, ncclInt32, g_comm.comm, M->stream));
     std::vector<int> all(4 * g_comm.nranks);
     HIP_TRY(hipMemcpyAsync(all.data(), d + 4, sizeof(int) * 4 * g_comm.nranks, hipMemcpyDeviceToHost, M->stream));
@@ -739,7 +750,7 @@ int build_a_image(hpccg_hip_matrix* M)
     }
     M->a_slots = (long long)ab[S] * kSliceRows;
     TRY(dev_alloc(M, &M->d_abase, ab.size()));
-    HIP_TRY(hipMemcpy(M->d_abase, ab.data(), sizeof(unsigned int) * ab.size(), hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, M->d_abase, ab.data(), sizeof(unsigned int) * ab.size()));
     TRY(dev_alloc(M, &M->d_aval, (size_t)M->a_slots));
     HIP_TRY(hipMemsetAsync(M->d_aval, 0, sizeof(double) * std::max<long long>(1, M->a_slots), M->stream));
     launch_a_fill(M->d_slice_base, S, M->d_cols, M->d_vals, M->ghost_lo, M->d_aoff, d_acount, M->d_abase,
@@ -784,7 +795,7 @@ int build_a_image(hpccg_hip_matrix* M)
             tri[s] = sizes == want ? 1 : 0;
         }
         TRY(dev_alloc(M, &M->d_atri, tri.size()));
-        HIP_TRY(hipMemcpy(M->d_atri, tri.data(), tri.size(), hipMemcpyHostToDevice));
+        TRY(h2d(M->stream, M->d_atri, tri.data(), tri.size()));
     }
     // pair windows
     const int NP = (S + 1) / 2;
@@ -807,13 +818,13 @@ int build_a_image(hpccg_hip_matrix* M)
         for (int j = 0; j < cnt[s]; j++)
             if (off[(size_t)s * kAMax + j] == 0) diag[s] = lds[(size_t)s * kAMax + j];
     TRY(dev_alloc(M, &M->d_adiag2, diag.size()));
-    HIP_TRY(hipMemcpy(M->d_adiag2, diag.data(), sizeof(int) * diag.size(), hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, M->d_adiag2, diag.data(), sizeof(int) * diag.size()));
     TRY(dev_alloc(M, &M->d_alds2, lds.size()));
     TRY(dev_alloc(M, &M->d_awin2, win.size()));
     TRY(dev_alloc(M, &M->d_awn2, wn.size()));
-    HIP_TRY(hipMemcpy(M->d_alds2, lds.data(), sizeof(int) * lds.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(M->d_awin2, win.data(), sizeof(int) * win.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(M->d_awn2, wn.data(), sizeof(int) * wn.size(), hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, M->d_alds2, lds.data(), sizeof(int) * lds.size()));
+    TRY(h2d(M->stream, M->d_awin2, win.data(), sizeof(int) * win.size()));
+    TRY(h2d(M->stream, M->d_awn2, wn.data(), sizeof(int) * wn.size()));
     M->alds2_doubles = std::max(1, maxd);
     M->has_pairs = 1;
     return 0;
@@ -945,7 +956,7 @@ int alloc_ring(hpccg_hip_matrix* M, int nbuf)
     const size_t ptotal = (size_t)M->pstride * nbuf;
     double* buf = nullptr;
     HIP_TRY(big_malloc(reinterpret_cast<void**>(&buf), sizeof(double) * ptotal));
-    if (hipMemset(buf, 0, sizeof(double) * ptotal) != hipSuccess) {
+    if (hipMemsetAsync(buf, 0, sizeof(double) * ptotal, M->stream) != hipSuccess) {
         (void)hipFree(buf);
         return set_err(HPCCG_HIP_EHIP, "hipMemset of the p ring failed");
     }
@@ -983,11 +994,12 @@ int alloc_workspace(hpccg_hip_matrix* M)
         M->d_kst = reinterpret_cast<int*>(blk);
         M->d_partial = blk + kKstDoubles;
         const std::vector<unsigned long long> empty(np, kSlotEmpty);  // every dot slot starts empty
-        HIP_TRY(hipMemcpy(M->d_partial, empty.data(), np * sizeof(double), hipMemcpyHostToDevice));
+        TRY(h2d(M->stream, M->d_partial, empty.data(), np * sizeof(double)));
     }
     M->ntickets = 2 * (ngroups + 1);
     TRY(dev_alloc(M, &M->d_tickets, M->ntickets, true));
     TRY(dev_alloc(M, &M->d_scal, 8, true));
+    HIP_TRY(hipStreamSynchronize(M->stream));  // every fill landed: other streams and peers may read them
     return 0;
 }
 
@@ -1776,7 +1788,7 @@ int alloc_mbox(hpccg_hip_matrix* M, bool plain = false)
     }
     M->d_mbox = static_cast<double*>(p);
     const std::vector<unsigned long long> empty(kMboxSlots, kSlotEmpty);
-    HIP_TRY(hipMemcpy(M->d_mbox, empty.data(), bytes, hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, M->d_mbox, empty.data(), bytes));
     return 0;
 }
 
@@ -1815,7 +1827,7 @@ int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
         const size_t hb = sizeof(h);
         unsigned char* d = nullptr;
         HIP_TRY(hipMalloc(&d, hb * (nr + 1)));
-        HIP_TRY(hipMemcpy(d + hb * nr, &h, hb, hipMemcpyHostToDevice));
+        TRY(h2d(M->stream, d + hb * nr, &h, hb));
         NCCL_TRY(ncclAllGather(d + hb * nr, d, hb, ncclUint8, g_comm.comm, M->stream));
         HIP_TRY(hipStreamSynchronize(M->stream));
         std::vector<unsigned char> all(hb * nr);
@@ -1838,7 +1850,7 @@ int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
         hpccg_hip_matrix* Mr = Ms[r];
         HIP_TRY(hipSetDevice(Mr->device));
         if (!Mr->d_peers) HIP_TRY(hipMalloc(&Mr->d_peers, sizeof(double*) * kMaxGroupRanks));
-        HIP_TRY(hipMemcpy(Mr->d_peers, tables[r].data(), sizeof(double*) * kMaxGroupRanks, hipMemcpyHostToDevice));
+        TRY(h2d(Mr->stream, Mr->d_peers, tables[r].data(), sizeof(double*) * kMaxGroupRanks));
         Mr->peers_for = nr;
     }
     HIP_TRY(hipSetDevice(M->device));
@@ -2180,11 +2192,11 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
     }
     if (bad) return set_err(HPCCG_HIP_EPLAN, "column index outside the halo plan");
     TRY(dev_alloc(M, &M->d_slice_base, sb.size()));
-    HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size()));
     TRY(dev_alloc(M, &M->d_cols, hc.size()));
-    HIP_TRY(hipMemcpy(M->d_cols, hc.data(), sizeof(int) * hc.size(), hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, M->d_cols, hc.data(), sizeof(int) * hc.size()));
     TRY(dev_alloc(M, &M->d_vals, hv.size()));
-    HIP_TRY(hipMemcpy(M->d_vals, hv.data(), sizeof(double) * hv.size(), hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, M->d_vals, hv.data(), sizeof(double) * hv.size()));
     M->has_sell = 1;
     TRY(finish_matrix(M));
     *out = guard.release();
@@ -2413,7 +2425,7 @@ int hpccg_hip_comm_allreduce_host(double* vals, int n, int op)
     hipStream_t s = nullptr;
     HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     HIP_TRY(hipMalloc(&d, sizeof(double) * n));
-    HIP_TRY(hipMemcpy(d, vals, sizeof(double) * n, hipMemcpyHostToDevice));
+    TRY(h2d(s, d, vals, sizeof(double) * n));
     const ncclRedOp_t ops[3] = {ncclSum, ncclMin, ncclMax};
     NCCL_TRY(ncclAllReduce(d, d, n, ncclFloat64, ops[op], g_comm.comm, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -2555,7 +2567,7 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     M->nslots = acc * kSliceRows;
     M->width = M->uniform ? wmax : 0;
     TRY(dev_alloc(M, &M->d_slice_base, sb.size()));
-    HIP_TRY(hipMemcpy(M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size(), hipMemcpyHostToDevice));
+    TRY(h2d(M->stream, M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size()));
     TRY(dev_alloc(M, &M->d_cols, (size_t)M->nslots));
     TRY(dev_alloc(M, &M->d_vals, (size_t)M->nslots));
     M->has_sell = 1;
@@ -3088,7 +3100,8 @@ int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which)
     if (!*buf) return set_err(HPCCG_HIP_EINVAL, "buffer %d not allocated", which);
     double* nb = nullptr;
     HIP_TRY(big_malloc(reinterpret_cast<void**>(&nb), sizeof(double) * n));
-    HIP_TRY(hipMemcpy(nb, *buf, sizeof(double) * n, hipMemcpyDeviceToDevice));
+    HIP_TRY(hipMemcpyAsync(nb, *buf, sizeof(double) * n, hipMemcpyDeviceToDevice, M->stream));
+    HIP_TRY(hipStreamSynchronize(M->stream));
     M->graveyard.push_back(*buf);  // held: the new buffer gets other physical memory
     const ptrdiff_t poff = M->d_p - M->d_pbuf, roff = M->d_r - M->d_rbuf;
     *buf = nb;

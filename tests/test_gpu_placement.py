@@ -43,7 +43,7 @@ def test_probe_at_creation(hp, gpu):
     try:
         hp.set_placement_probe(2)
         M = hp.Matrix.from_hpc(prob)
-        assert M.placement().shape == (5,)
+        assert M.placement().shape == (5,), {k: M.get_option(k) for k in ("has_a", "spmv_kernel", "a_width")}
         assert solve_bits(hp, M, prob.b, 30) == base
         M.close()
         G = hp.Matrix.generate(32, 32, 32)
