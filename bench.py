@@ -275,6 +275,8 @@ def main():
     ap.add_argument("--overlap", type=int, default=-1, help="multi-rank: halo beside the interior SpMV")
     ap.add_argument("--a-pre", type=int, default=-1, help="direct kernel: value slots loaded before the test")
     ap.add_argument("--use-graph", type=int, default=-1, help="hipGraph replay (-1 default on)")
+    ap.add_argument("--placement", type=int, default=-1,
+                    help="placement probe candidates at creation (-1 auto: 6 for images > 512 MB; 0 off)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VAL",
                     help="any other solver option (hpccg_hip_set_option), e.g. --set nt_store=0")
     ap.add_argument("--timeout", type=float, default=1200.0,
@@ -326,8 +328,11 @@ def main():
     n = args.n
     use_7pt = args.stencil == 7
     t0 = time.time()
+    hp.set_placement_probe(args.placement)
     M = hp.Matrix.generate(n, n, n, use_7pt=use_7pt)
     info = M.info()
+    probe_us = M.placement()
+    pick = M.get_option("placement_pick")
     for opt, val in (("spmv_kernel", args.kernel), ("fuse_p", args.fuse_p), ("fold", args.fold),
                      ("graph_chunk", args.graph_chunk), ("x_defer", args.x_defer), ("x_ring", args.x_ring),
                      ("rev_update", args.rev_update), ("overlap", args.overlap), ("a_pre", args.a_pre),
@@ -459,6 +464,11 @@ def main():
                 "spmv_kernel": kernel, "matrix_format": FORMAT_NAMES[kfmt],
                 "device_bytes_per_gpu": M.get_option("device_bytes"),
                 "graph_replay": bool(graph_used),
+                "placement_probe": {
+                    "note": "setup, untimed: CG iterations timed on contiguous candidate placements of the "
+                            "values and the p ring, fastest kept (DESIGN.md 4); rank 0's",
+                    "us_per_iteration": [round(float(v), 2) for v in probe_us],
+                    "kept": {"values": pick & 255, "ring": pick >> 8}},
                 "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update",
                                                          "overlap", "graph_chunk", "nt", "a2_ring", "nt_store",
                                                          "fuse_update")},
