@@ -100,7 +100,7 @@ def lib() -> C.CDLL:
         "hpccg_hip_diag_spmv": (ip, [vp, ip, ip, PD]),
         "hpccg_hip_diag_slot_plan": (ip, [ip, ip, ip, ip, PI, ip, PI]),
         "hpccg_hip_diag_timeline": (ip, [vp, C.POINTER(C.c_uint64), ip]),
-        "hpccg_hip_diag_realloc": (ip, [vp, ip]),
+        "hpccg_hip_diag_realloc": (ip, [vp, ip, C.POINTER(C.c_uint64)]),
         "hpccg_hip_probe_placement": (ip, [vp, ip]),
         "hpccg_hip_diag_placement": (ip, [vp, PD, ip]),
         "hpccg_hip_set_placement_probe": (ip, [ip]),
@@ -346,10 +346,14 @@ class Matrix:
         _check(n if n < 0 else 0, "diag_timeline")
         return out[:8 * n].reshape(n, 8)
 
-    def diag_realloc(self, which: int) -> None:
+    def diag_realloc(self, which: int, mode: int = 0) -> int:
         """Move a device buffer to new memory (0 values, 1 p ring, 2 r, 3 Ap,
-        4 x; diagnostics: physical placement)."""
-        _check(lib().hpccg_hip_diag_realloc(self.h, which), "diag_realloc")
+        4 x) allocated by mode (0 hipMalloc, 1 contiguous, 2/3/4 VMM at 2 MB /
+        64 MB / 1 GB alignment); returns its virtual address (diagnostics:
+        physical placement)."""
+        va = C.c_uint64(0)
+        _check(lib().hpccg_hip_diag_realloc(self.h, which | (mode << 8), C.byref(va)), "diag_realloc")
+        return va.value
 
     def probe_placement(self, tries: int = 6) -> np.ndarray:
         """Time CG iterations on the current placement, then on up to `tries`

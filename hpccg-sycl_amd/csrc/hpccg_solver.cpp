@@ -286,6 +286,14 @@ struct hpccg_hip_matrix {
     char* h_rb = nullptr;
     size_t h_rb_bytes = 0;
     std::vector<void*> graveyard;  // diagnostics: buffers moved by hpccg_hip_diag_realloc, held until destroy
+    struct Vmm {
+        void* va;  // the mapping (aligned inside the reservation)
+        size_t bytes;
+        hipMemGenericAllocationHandle_t h;
+        void* res;  // the reservation
+        size_t res_bytes;
+    };
+    std::vector<Vmm> vmm;  // diagnostics: hpccg_hip_diag_realloc's VMM mappings (unmapped at destroy)
     std::vector<double> place_us;  // placement probe: SpMV us per candidate (0 = the creation placement)
     int place_pick = 0;            // the candidate kept
     double *d_gen_b = nullptr, *d_gen_x0 = nullptr, *d_gen_xexact = nullptr;
@@ -360,6 +368,9 @@ int free_matrix(hpccg_hip_matrix* M)
     (void)hipSetDevice(M->device);
     if (M->stream) (void)hipStreamSynchronize(M->stream);
     if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
+    for (const auto& v : M->vmm)  // diagnostics' VMM mappings: released below, not hipFree'd
+        for (double** q : {&M->d_aval, &M->d_pbuf, &M->d_rbuf, &M->d_Ap, &M->d_x})
+            if (*q == v.va) *q = nullptr;
     void* ptrs[] = {M->d_slice_base, M->d_cols,   M->d_vals,      M->d_aval,    M->d_aoff,     M->d_abase,
                     M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_adiag2,     M->d_atri,      M->d_pbuf,    M->d_ahist,    M->d_rbuf,
                     M->d_Ap,         M->d_x,      M->d_b,         M->d_tickets,  M->d_scal,
@@ -370,6 +381,11 @@ int free_matrix(hpccg_hip_matrix* M)
     for (void* p : M->ipc_opened) (void)hipIpcCloseMemHandle(p);
     if (M->h_rb) (void)hipHostFree(M->h_rb);
     for (void* p : M->graveyard) (void)hipFree(p);
+    for (const auto& v : M->vmm) {
+        (void)hipMemUnmap(v.va, v.bytes);
+        (void)hipMemRelease(v.h);
+        (void)hipMemAddressFree(v.res, v.res_bytes);
+    }
     if (M->d_mbox) (void)hipFree(M->d_mbox);
     if (M->d_peers) (void)hipFree(M->d_peers);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
@@ -3082,9 +3098,40 @@ int hpccg_hip_diag_placement(const hpccg_hip_matrix* M, double* us_out, int cap)
     return n;
 }
 
-int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which)
+// Diagnostics: a mapping through the VMM API at a chosen virtual alignment.
+int vmm_alloc(hpccg_hip_matrix* M, size_t bytes, size_t align, double** out)
+{
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = M->device;
+    size_t gran = 0;
+    HIP_TRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+    const size_t sz = (bytes + gran - 1) / gran * gran;
+    // reserve align more and map at an aligned address inside (the
+    // reservation's own alignment argument is not honoured above 2 MB here)
+    align = std::max(align, gran);
+    void* res = nullptr;
+    HIP_TRY(hipMemAddressReserve(&res, sz + align, gran, nullptr, 0));
+    const uintptr_t a0 = (reinterpret_cast<uintptr_t>(res) + align - 1) / align * align;
+    void* va = reinterpret_cast<void*>(a0);
+    hipMemGenericAllocationHandle_t h;
+    HIP_TRY(hipMemCreate(&h, sz, &prop, 0));
+    HIP_TRY(hipMemMap(va, sz, 0, h, 0));
+    hipMemAccessDesc ad = {};
+    ad.location = prop.location;
+    ad.flags = hipMemAccessFlagsProtReadWrite;
+    HIP_TRY(hipMemSetAccess(va, sz, &ad, 1));
+    M->vmm.push_back({va, sz, h, res, sz + align});
+    *out = static_cast<double*>(va);
+    return 0;
+}
+
+int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which, unsigned long long* va_out)
 {
     if (!M) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    const int mode = which >> 8;
+    which &= 255;
     HIP_TRY(hipSetDevice(M->device));
     HIP_TRY(hipStreamSynchronize(M->stream));
     double** buf;
@@ -3097,16 +3144,28 @@ int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which)
     case 4: buf = &M->d_x; n = M->npad; break;
     default: return set_err(HPCCG_HIP_EINVAL, "which must be 0..4");
     }
+    if (mode < 0 || mode > 4) return set_err(HPCCG_HIP_EINVAL, "mode must be 0..4");
     if (!*buf) return set_err(HPCCG_HIP_EINVAL, "buffer %d not allocated", which);
     double* nb = nullptr;
-    HIP_TRY(big_malloc(reinterpret_cast<void**>(&nb), sizeof(double) * n));
-    HIP_TRY(hipMemcpyAsync(nb, *buf, sizeof(double) * n, hipMemcpyDeviceToDevice, M->stream));
+    const size_t bytes = sizeof(double) * n;
+    if (mode == 0) {
+        HIP_TRY(big_malloc(reinterpret_cast<void**>(&nb), bytes));
+    } else if (mode == 1) {
+        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocContiguous));
+    } else {  // VMM at 2 MB, 64 MB or 1 GB virtual alignment
+        const size_t align = mode == 2 ? (size_t(1) << 21) : mode == 3 ? (size_t(1) << 26) : (size_t(1) << 30);
+        TRY(vmm_alloc(M, bytes, align, &nb));
+    }
+    HIP_TRY(hipMemcpyAsync(nb, *buf, bytes, hipMemcpyDeviceToDevice, M->stream));
     HIP_TRY(hipStreamSynchronize(M->stream));
-    M->graveyard.push_back(*buf);  // held: the new buffer gets other physical memory
+    bool mapped = false;  // a VMM mapping is released at destroy, not hipFree'd
+    for (const auto& v : M->vmm) mapped = mapped || v.va == *buf;
+    if (!mapped) M->graveyard.push_back(*buf);  // held: the new buffer gets other physical memory
     const ptrdiff_t poff = M->d_p - M->d_pbuf, roff = M->d_r - M->d_rbuf;
     *buf = nb;
     if (which == 1) M->d_p = M->d_pbuf + poff;
     if (which == 2) M->d_r = M->d_rbuf + roff;
+    if (va_out) *va_out = reinterpret_cast<unsigned long long>(nb);
     return 0;  // the graph cache compares kernel arguments: the next solve re-captures
 }
 

@@ -233,10 +233,14 @@ int hpccg_hip_kernel_times_iter(const hpccg_hip_matrix* M, double* out, int cap)
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_us);
 /* Diagnostic: move one device buffer to a new allocation (contents copied;
  * the old one is held until the matrix is destroyed, so the new one lands on
- * other physical memory): 0 the SELL-512-A values, 1 the p ring, 2 r, 3 Ap,
- * 4 x. For measuring the effect of physical placement on the kernels' rate.
- * Replaces nothing in the reference. */
-int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which);
+ * other physical memory): which & 255 = 0 the SELL-512-A values, 1 the p
+ * ring, 2 r, 3 Ap, 4 x; which >> 8 = the allocation: 0 hipMalloc, 1
+ * physically contiguous (hipDeviceMallocContiguous), 2/3/4 the VMM API
+ * (hipMemCreate + hipMemMap) at 2 MB / 64 MB / 1 GB virtual alignment. The
+ * new virtual address goes to *va_out (may be NULL). For measuring the effect
+ * of physical placement on the kernels' rate. Replaces nothing in the
+ * reference. */
+int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which, unsigned long long* va_out);
 /* The CG iteration rate of a large matrix depends on the physical HBM
  * placement of its values and p ring (306-350 us per 200^3 SpMV on one box).
  * Times a few eager CG iterations (median SpMV + update, scratch b and x; a

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--stencil", type=int, default=27)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--which", default="0,1,2,3")
+    ap.add_argument("--mode", type=int, default=0, help="0 hipMalloc, 1 contiguous, 2/3/4 VMM 2 MB/64 MB/1 GB")
     ap.add_argument("--max-iter", type=int, default=200)
     ap.add_argument("--probe", type=int, default=0, help="candidates of the creation probe (A/B mode)")
     args = ap.parse_args()
@@ -38,6 +39,7 @@ def main():
     hp.set_device(0)
     if args.probe:
         return probe_ab(hp, torch, args)
+    hp.set_placement_probe(0)  # the creation placement as hipMalloc leaves it
     M = hp.Matrix.generate(args.n, args.n, args.n, use_7pt=args.stencil == 7)
     b = M.vectors()[0]
     x = torch.zeros(args.n ** 3, dtype=torch.float64, device="cuda:0")
@@ -46,10 +48,10 @@ def main():
     print(json.dumps({"moved": None, "it_per_s": round(r0, 1), "spmv_us": round(s0, 2)}), flush=True)
     for w in [int(v) for v in args.which.split(",")]:
         for rnd in range(args.rounds):
-            M.diag_realloc(w)
+            va = M.diag_realloc(w, args.mode)
             r, sp = measure()
-            print(json.dumps({"moved": NAMES[w], "round": rnd, "it_per_s": round(r, 1), "spmv_us": round(sp, 2)}),
-                  flush=True)
+            print(json.dumps({"moved": NAMES[w], "mode": args.mode, "round": rnd, "va_mod_1g_mb": (va % (1 << 30)) >> 20,
+                              "it_per_s": round(r, 1), "spmv_us": round(sp, 2)}), flush=True)
     M.close()
 
 
