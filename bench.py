@@ -466,9 +466,9 @@ def main():
                 "graph_replay": bool(graph_used),
                 "placement_probe": {
                     "note": "setup, untimed: CG iterations timed on contiguous candidate placements of the "
-                            "values and the p ring, fastest kept (DESIGN.md 4); rank 0's",
+                            "values, the p ring, r and Ap, fastest kept (DESIGN.md 4); rank 0's",
                     "us_per_iteration": [round(float(v), 2) for v in probe_us],
-                    "kept": {"values": pick & 255, "ring": pick >> 8}},
+                    "kept": {b: (pick >> (8 * i)) & 255 for i, b in enumerate(("values", "ring", "r", "Ap"))}},
                 "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update",
                                                          "overlap", "graph_chunk", "nt", "a2_ring", "nt_store",
                                                          "fuse_update")},

@@ -358,17 +358,17 @@ class Matrix:
     def probe_placement(self, tries: int = 6) -> np.ndarray:
         """Time CG iterations on the current placement, then on up to `tries`
         contiguous placements of the values (keep the fastest), then of the p
-        ring (likewise); results unchanged. Returns placement()."""
+        ring, r and Ap (likewise); results unchanged. Returns placement()."""
         _check(lib().hpccg_hip_probe_placement(self.h, int(tries)), "probe_placement")
         return self.placement()
 
     def placement(self) -> np.ndarray:
         """us per CG iteration of each candidate of the last placement probe
-        ([0] the placement before it, then the values candidates, then the
-        ring candidates; empty if none ran). Option placement_pick: values
-        index | ring index << 8."""
-        out = np.zeros(33, np.float64)
-        n = lib().hpccg_hip_diag_placement(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), 33)
+        ([0] the placement before it, then the values, ring, r and Ap
+        candidates in turn; empty if none ran). Option placement_pick: one
+        byte per buffer, values | ring << 8 | r << 16 | Ap << 24."""
+        out = np.zeros(65, np.float64)
+        n = lib().hpccg_hip_diag_placement(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), 65)
         _check(n if n < 0 else 0, "diag_placement")
         return out[:n]
 

@@ -116,7 +116,7 @@ int g_halo_mode = 0;  // 0 auto (slab when it serves every rank), 1 slab only, 2
 int g_keep_sell = 0;  // keep the SELL-512 image beside SELL-512-A (kernel A/B, diagnostics)
 int g_place_tries = -1;  // placement probe at creation: -1 auto, 0 off, n candidates
 constexpr int kPlaceAuto = 6;        // candidates of the automatic probe
-constexpr int kPlaceReps = 6;        // timed SpMV launches per candidate
+constexpr int kPlacePhases = 4;      // values, p ring, r, Ap
 constexpr double kPlaceMinBytes = 512e6;  // auto: only images that stream from HBM
 int comm_nranks() { return g_group_ctx.active ? g_group_ctx.nranks : g_comm.nranks; }
 int comm_rank() { return g_group_ctx.active ? g_group_ctx.rank : g_comm.rank; }
@@ -215,6 +215,7 @@ struct hpccg_hip_matrix {
     int overlap = 0;  // eager launches only (see overlap_ok)
     hipStream_t stream = nullptr, stream2 = nullptr;
     hipEvent_t ev_pb = nullptr, ev_halo = nullptr;
+    hipEvent_t ev_flush = nullptr;  // flush_stream's marker (default flags: system-scope release)
     long long nnz = 0, nslots = 0;
     int nslices = 0, grid = 0, width = 0, uniform = 0;
     int kernel = 0;       // SpMV kernel in use (SpmvKernel)
@@ -240,6 +241,8 @@ struct hpccg_hip_matrix {
     double* d_vals = nullptr;
     // SELL-512-A
     int has_a = 0, a_width = 0;
+    int a_reject = 0;  // SELL-512-A not built (diagnostics): 2 its flag read late, 3 rejected although
+                       // the device's columns fit (a kernel fault), 4 rejected and they do not
     long long a_slots = 0;
     double* d_aval = nullptr;
     int* d_aoff = nullptr;
@@ -331,14 +334,23 @@ hipError_t big_malloc(void** p, size_t b)
     return hipMalloc(p, b);
 }
 
-// Host-to-device copy ordered on stream s, where the kernels (or RCCL calls)
-// that read it run: a plain hipMemcpy is ordered on the null stream, which the
-// library's non-blocking streams do not wait for (with pageable sources it
-// can return before the data has landed). Waits, so the source may go away.
-int h2d(hipStream_t s, void* dst, const void* src, size_t bytes)
+// Host-to-device copy ordered on stream s (no matrix: the kernel-level API's
+// scratch); waits, so the source may go away.
+int h2d_stream(hipStream_t s, void* dst, const void* src, size_t bytes)
 {
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));
+    return 0;
+}
+
+// Device-to-host copy into pageable memory after the work queued on stream s:
+// a synchronous copy once s has drained, so the data is in dst on return
+// (an async copy into pageable memory gives no such guarantee at the stream
+// sync).
+int d2h(hipStream_t s, void* dst, const void* src, size_t bytes)
+{
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -352,10 +364,39 @@ int dev_alloc(hpccg_hip_matrix* M, T** p, size_t count, bool zero = false)
     return 0;
 }
 
+// A marker with a system-scope release on M's stream, waited for: what the
+// kernels left dirty in the L2s is in memory before a buffer is freed (and
+// reused by the next allocation) or read by the host's copy engine. Needed
+// after event-timed work: the timing events are created without that release
+// (ensure_events), and without it a line written back later lands in
+// whatever buffer owns the memory by then.
+int flush_stream(hpccg_hip_matrix* M)
+{
+    if (!M->stream) return 0;
+    if (!M->ev_flush) HIP_TRY(hipEventCreateWithFlags(&M->ev_flush, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(M->ev_flush, M->stream));
+    HIP_TRY(hipEventSynchronize(M->ev_flush));
+    return 0;
+}
+
+// Host-to-device copy into a buffer of M, ordered on M's stream where the
+// kernels (or RCCL calls) that read it run (a plain hipMemcpy is ordered on
+// the null stream, which the library's non-blocking streams do not wait
+// for). Flushed on both sides: a zero fill of the same memory still dirty in
+// an L2 must not be written back over the copied data later, and the copy
+// must be in memory for every XCD. Waits, so the source may go away.
+int h2d(hpccg_hip_matrix* M, void* dst, const void* src, size_t bytes)
+{
+    TRY(flush_stream(M));
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, M->stream));
+    return flush_stream(M);
+}
+
 template <class T>
 void dev_free(hpccg_hip_matrix* M, T** p, size_t count)
 {
     if (*p) {
+        (void)flush_stream(M);
         (void)hipFree(*p);
         M->bytes -= (long long)(sizeof(T) * std::max<size_t>(1, count));
     }
@@ -365,8 +406,19 @@ void dev_free(hpccg_hip_matrix* M, T** p, size_t count)
 int free_matrix(hpccg_hip_matrix* M)
 {
     if (!M) return 0;
+    // Nothing may write into this matrix's memory once it is freed and reused:
+    // its own streams, and in a group the other members' kernels, which store
+    // into its mailbox (peer all-reduce) or read its planes -- every device of
+    // a group is drained, not just this one
+    if (M->in_group) {
+        int nd = 0;
+        if (hipGetDeviceCount(&nd) == hipSuccess)
+            for (int d = 0; d < nd; d++)
+                if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
+    }
     (void)hipSetDevice(M->device);
-    if (M->stream) (void)hipStreamSynchronize(M->stream);
+    (void)hipDeviceSynchronize();
+    (void)flush_stream(M);
     if (M->graph_exec) (void)hipGraphExecDestroy(M->graph_exec);
     for (const auto& v : M->vmm)  // diagnostics' VMM mappings: released below, not hipFree'd
         for (double** q : {&M->d_aval, &M->d_pbuf, &M->d_rbuf, &M->d_Ap, &M->d_x})
@@ -389,6 +441,7 @@ int free_matrix(hpccg_hip_matrix* M)
     if (M->d_mbox) (void)hipFree(M->d_mbox);
     if (M->d_peers) (void)hipFree(M->d_peers);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
+    if (M->ev_flush) (void)hipEventDestroy(M->ev_flush);
     for (hipEvent_t e : {M->ev_pb, M->ev_halo})
         if (e) (void)hipEventDestroy(e);
     if (M->stream) (void)hipStreamDestroy(M->stream);
@@ -525,10 +578,10 @@ int rccl_requests(hpccg_hip_matrix* M, GatherPlan& g)
     for (int q = 0; q < P; q++) mine[q] = (int)g.req[q].size();
     int* d = nullptr;
     HIP_TRY(hipMalloc(&d, sizeof(int) * (size_t)P * (P + 1)));
-    TRY(h2d(M->stream, d, mine.data(), sizeof(int) * P));
+    TRY(h2d(M, d, mine.data(), sizeof(int) * P));
     NCCL_TRY(ncclAllGather(d, d + P, P, ncclInt32, g_comm.comm, M->stream));
     std::vector<int> cnt((size_t)P * P);
-    HIP_TRY(hipMemcpyAsync(cnt.data(), d + P, sizeof(int) * P * P, hipMemcpyDeviceToHost, M->stream));
+    TRY(d2h(M->stream, cnt.data(), d + P, sizeof(int) * P * P));
     HIP_TRY(hipStreamSynchronize(M->stream));
     (void)hipFree(d);
     long long nout = 0, nin = 0;
@@ -542,7 +595,7 @@ int rccl_requests(hpccg_hip_matrix* M, GatherPlan& g)
     HIP_TRY(hipMalloc(&din, sizeof(int) * std::max(1LL, nin)));
     std::vector<int> flat;
     for (int q = 0; q < P; q++) flat.insert(flat.end(), g.req[q].begin(), g.req[q].end());
-    if (nout) TRY(h2d(M->stream, dout, flat.data(), sizeof(int) * nout));
+    if (nout) TRY(h2d(M, dout, flat.data(), sizeof(int) * nout));
     NCCL_TRY(ncclGroupStart());
     long long oo = 0, oi = 0;
     for (int q = 0; q < P; q++) {
@@ -554,7 +607,7 @@ int rccl_requests(hpccg_hip_matrix* M, GatherPlan& g)
     }
     NCCL_TRY(ncclGroupEnd());
     std::vector<int> got(std::max(1LL, nin));
-    HIP_TRY(hipMemcpyAsync(got.data(), din, sizeof(int) * std::max(1LL, nin), hipMemcpyDeviceToHost, M->stream));
+    TRY(d2h(M->stream, got.data(), din, sizeof(int) * std::max(1LL, nin)));
     HIP_TRY(hipStreamSynchronize(M->stream));
     (void)hipFree(dout);
     (void)hipFree(din);
@@ -585,7 +638,7 @@ int install_gather(hpccg_hip_matrix* M, const GatherPlan& g)
     TRY(dev_alloc(M, &M->d_send_idx, M->nsend));
     TRY(dev_alloc(M, &M->d_send_buf, M->nsend));
     if (M->nsend)
-        TRY(h2d(M->stream, M->d_send_idx, g.send_idx.data(), sizeof(int) * M->nsend));
+        TRY(h2d(M, M->d_send_idx, g.send_idx.data(), sizeof(int) * M->nsend));
     return 0;
 }
 
@@ -618,10 +671,10 @@ int exchange_plan(hpccg_hip_matrix* M, int* mode = nullptr, std::vector<int>* al
     int* d = nullptr;
     HIP_TRY(hipMalloc(&d, sizeof(int) * 4 * (g_comm.nranks + 1)));
     int mine[4] = {M->nrow, M->ghost_lo, M->ghost_hi, M->start_row};
-    TRY(h2d(M->stream, d, mine, sizeof mine));
+    TRY(h2d(M, d, mine, sizeof mine));
     NCCL_TRY(ncclAllGather(d, d + 4, 4, ncclInt32, g_comm.comm, M->stream));
     std::vector<int> all(4 * g_comm.nranks);
-    HIP_TRY(hipMemcpyAsync(all.data(), d + 4, sizeof(int) * 4 * g_comm.nranks, hipMemcpyDeviceToHost, M->stream));
+    TRY(d2h(M->stream, all.data(), d + 4, sizeof(int) * 4 * g_comm.nranks));
     HIP_TRY(hipStreamSynchronize(M->stream));
     (void)hipFree(d);
     const int md = choose_halo_mode(all.data(), g_comm.nranks);
@@ -743,10 +796,39 @@ int build_a_image(hpccg_hip_matrix* M)
     HIP_TRY(hipGetLastError());
     int fl[2] = {0, 0};
     std::vector<int> cnt(S);
-    HIP_TRY(hipMemcpyAsync(fl, d_flags, sizeof fl, hipMemcpyDeviceToHost, M->stream));
-    HIP_TRY(hipMemcpyAsync(cnt.data(), d_acount, sizeof(int) * S, hipMemcpyDeviceToHost, M->stream));
+    TRY(d2h(M->stream, fl, d_flags, sizeof fl));
+    TRY(d2h(M->stream, cnt.data(), d_acount, sizeof(int) * S));
     HIP_TRY(hipStreamSynchronize(M->stream));
     if (!fl[0]) {
+        // (diagnostics: a second read after a device-wide sync tells a late
+        // readback from a real rejection)
+        int again[2] = {0, 0};
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(again, d_flags, sizeof again, hipMemcpyDeviceToHost));
+        M->a_reject = again[0] ? 2 : 1;
+        if (!again[0]) {  // the device's columns re-checked on the host: 3 they fit (a kernel fault), 4 they do not
+            std::vector<unsigned int> sbh(S + 1);
+            HIP_TRY(hipMemcpy(sbh.data(), M->d_slice_base, sizeof(unsigned int) * (S + 1), hipMemcpyDeviceToHost));
+            std::vector<int> ch((size_t)sbh[S] * kSliceRows);
+            HIP_TRY(hipMemcpy(ch.data(), M->d_cols, sizeof(int) * ch.size(), hipMemcpyDeviceToHost));
+            bool fits = true;
+            for (int sl = 0; sl < S && fits; sl++) {
+                std::vector<int> offs;
+                for (int lane = 0; lane < kSliceRows; lane++) {
+                    int prev = INT_MIN;
+                    for (unsigned j = sbh[sl]; j < sbh[sl + 1]; j++) {
+                        const int c = ch[(size_t)j * kSliceRows + lane];
+                        if (c < 0) continue;
+                        const int o = c - M->ghost_lo - (sl * kSliceRows + lane);
+                        if (o <= prev) fits = false;
+                        prev = o;
+                        if (std::find(offs.begin(), offs.end(), o) == offs.end()) offs.push_back(o);
+                    }
+                }
+                if ((int)offs.size() > kAMax) fits = false;
+            }
+            M->a_reject = fits ? 3 : 4;
+        }
         dev_free(M, &M->d_aoff, (size_t)S * kAMax);
         return 0;
     }
@@ -766,14 +848,14 @@ int build_a_image(hpccg_hip_matrix* M)
     }
     M->a_slots = (long long)ab[S] * kSliceRows;
     TRY(dev_alloc(M, &M->d_abase, ab.size()));
-    TRY(h2d(M->stream, M->d_abase, ab.data(), sizeof(unsigned int) * ab.size()));
+    TRY(h2d(M, M->d_abase, ab.data(), sizeof(unsigned int) * ab.size()));
     TRY(dev_alloc(M, &M->d_aval, (size_t)M->a_slots));
     HIP_TRY(hipMemsetAsync(M->d_aval, 0, sizeof(double) * std::max<long long>(1, M->a_slots), M->stream));
     launch_a_fill(M->d_slice_base, S, M->d_cols, M->d_vals, M->ghost_lo, M->d_aoff, d_acount, M->d_abase,
                   M->d_aval, M->stream);
     HIP_TRY(hipGetLastError());
     std::vector<int> off((size_t)S * kAMax);
-    HIP_TRY(hipMemcpyAsync(off.data(), M->d_aoff, sizeof(int) * off.size(), hipMemcpyDeviceToHost, M->stream));
+    TRY(d2h(M->stream, off.data(), M->d_aoff, sizeof(int) * off.size()));
     HIP_TRY(hipStreamSynchronize(M->stream));
     M->has_a = 1;
     // halo-dependent units: they read rows of a ghost region ([-ghost_lo, 0)
@@ -811,7 +893,7 @@ int build_a_image(hpccg_hip_matrix* M)
             tri[s] = sizes == want ? 1 : 0;
         }
         TRY(dev_alloc(M, &M->d_atri, tri.size()));
-        TRY(h2d(M->stream, M->d_atri, tri.data(), tri.size()));
+        TRY(h2d(M, M->d_atri, tri.data(), tri.size()));
     }
     // pair windows
     const int NP = (S + 1) / 2;
@@ -834,13 +916,13 @@ int build_a_image(hpccg_hip_matrix* M)
         for (int j = 0; j < cnt[s]; j++)
             if (off[(size_t)s * kAMax + j] == 0) diag[s] = lds[(size_t)s * kAMax + j];
     TRY(dev_alloc(M, &M->d_adiag2, diag.size()));
-    TRY(h2d(M->stream, M->d_adiag2, diag.data(), sizeof(int) * diag.size()));
+    TRY(h2d(M, M->d_adiag2, diag.data(), sizeof(int) * diag.size()));
     TRY(dev_alloc(M, &M->d_alds2, lds.size()));
     TRY(dev_alloc(M, &M->d_awin2, win.size()));
     TRY(dev_alloc(M, &M->d_awn2, wn.size()));
-    TRY(h2d(M->stream, M->d_alds2, lds.data(), sizeof(int) * lds.size()));
-    TRY(h2d(M->stream, M->d_awin2, win.data(), sizeof(int) * win.size()));
-    TRY(h2d(M->stream, M->d_awn2, wn.data(), sizeof(int) * wn.size()));
+    TRY(h2d(M, M->d_alds2, lds.data(), sizeof(int) * lds.size()));
+    TRY(h2d(M, M->d_awin2, win.data(), sizeof(int) * win.size()));
+    TRY(h2d(M, M->d_awn2, wn.data(), sizeof(int) * wn.size()));
     M->alds2_doubles = std::max(1, maxd);
     M->has_pairs = 1;
     return 0;
@@ -1010,12 +1092,12 @@ int alloc_workspace(hpccg_hip_matrix* M)
         M->d_kst = reinterpret_cast<int*>(blk);
         M->d_partial = blk + kKstDoubles;
         const std::vector<unsigned long long> empty(np, kSlotEmpty);  // every dot slot starts empty
-        TRY(h2d(M->stream, M->d_partial, empty.data(), np * sizeof(double)));
+        TRY(h2d(M, M->d_partial, empty.data(), np * sizeof(double)));
     }
     M->ntickets = 2 * (ngroups + 1);
     TRY(dev_alloc(M, &M->d_tickets, M->ntickets, true));
     TRY(dev_alloc(M, &M->d_scal, 8, true));
-    HIP_TRY(hipStreamSynchronize(M->stream));  // every fill landed: other streams and peers may read them
+    TRY(flush_stream(M));  // every fill landed and written back: other streams and peers may read them
     return 0;
 }
 
@@ -1067,12 +1149,18 @@ int ensure_hist(hpccg_hip_matrix* M, int max_iter)
 // sleeps, and its wake-up cost 120-820 us per synchronous readback at the end
 // of a 200^3 solve (rocprof kernel trace, profiles/r03_200); polling returns
 // within microseconds.
-int wait_stream(hipStream_t st)
+// The end of a solve: a marker with a system-scope release (flush_stream's
+// event) behind the solve's work, polled rather than blocked on (a blocking
+// wait adds tens of us of wake-up). The release writes back what the kernels
+// left dirty in the L2s before the caller frees, reuses or copies anything.
+int wait_matrix(hpccg_hip_matrix* M)
 {
+    if (!M->ev_flush) HIP_TRY(hipEventCreateWithFlags(&M->ev_flush, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(M->ev_flush, M->stream));
     for (;;) {
-        const hipError_t e = hipStreamQuery(st);
+        const hipError_t e = hipEventQuery(M->ev_flush);
         if (e == hipSuccess) return 0;
-        if (e != hipErrorNotReady) return set_err(HPCCG_HIP_EHIP, "hipStreamQuery: %s", hipGetErrorString(e));
+        if (e != hipErrorNotReady) return set_err(HPCCG_HIP_EHIP, "hipEventQuery: %s", hipGetErrorString(e));
         __builtin_ia32_pause();
     }
 }
@@ -1804,7 +1892,7 @@ int alloc_mbox(hpccg_hip_matrix* M, bool plain = false)
     }
     M->d_mbox = static_cast<double*>(p);
     const std::vector<unsigned long long> empty(kMboxSlots, kSlotEmpty);
-    TRY(h2d(M->stream, M->d_mbox, empty.data(), bytes));
+    TRY(h2d(M, M->d_mbox, empty.data(), bytes));
     return 0;
 }
 
@@ -1843,7 +1931,7 @@ int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
         const size_t hb = sizeof(h);
         unsigned char* d = nullptr;
         HIP_TRY(hipMalloc(&d, hb * (nr + 1)));
-        TRY(h2d(M->stream, d + hb * nr, &h, hb));
+        TRY(h2d(M, d + hb * nr, &h, hb));
         NCCL_TRY(ncclAllGather(d + hb * nr, d, hb, ncclUint8, g_comm.comm, M->stream));
         HIP_TRY(hipStreamSynchronize(M->stream));
         std::vector<unsigned char> all(hb * nr);
@@ -1866,7 +1954,7 @@ int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
         hpccg_hip_matrix* Mr = Ms[r];
         HIP_TRY(hipSetDevice(Mr->device));
         if (!Mr->d_peers) HIP_TRY(hipMalloc(&Mr->d_peers, sizeof(double*) * kMaxGroupRanks));
-        TRY(h2d(Mr->stream, Mr->d_peers, tables[r].data(), sizeof(double*) * kMaxGroupRanks));
+        TRY(h2d(Mr, Mr->d_peers, tables[r].data(), sizeof(double*) * kMaxGroupRanks));
         Mr->peers_for = nr;
     }
     HIP_TRY(hipSetDevice(M->device));
@@ -2049,7 +2137,7 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     if (times)
         HIP_TRY(hipMemcpyAsync(stamps, M->d_stamps, sizeof(unsigned long long) * nstamps, hipMemcpyDeviceToHost,
                                M->stream));
-    TRY(wait_stream(M->stream));
+    TRY(wait_matrix(M));
     const auto t_end = std::chrono::steady_clock::now();
     TRY(check_device_error(Ms, P, kst + kErrBase));
     // (the fused update keeps k in kst[0] / kst[2] by parity: the later one is the count)
@@ -2208,11 +2296,11 @@ int create_from_rows(hpccg_hip_matrix** out, int nrow, int start_row, int total_
     }
     if (bad) return set_err(HPCCG_HIP_EPLAN, "column index outside the halo plan");
     TRY(dev_alloc(M, &M->d_slice_base, sb.size()));
-    TRY(h2d(M->stream, M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size()));
+    TRY(h2d(M, M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size()));
     TRY(dev_alloc(M, &M->d_cols, hc.size()));
-    TRY(h2d(M->stream, M->d_cols, hc.data(), sizeof(int) * hc.size()));
+    TRY(h2d(M, M->d_cols, hc.data(), sizeof(int) * hc.size()));
     TRY(dev_alloc(M, &M->d_vals, hv.size()));
-    TRY(h2d(M->stream, M->d_vals, hv.data(), sizeof(double) * hv.size()));
+    TRY(h2d(M, M->d_vals, hv.data(), sizeof(double) * hv.size()));
     M->has_sell = 1;
     TRY(finish_matrix(M));
     *out = guard.release();
@@ -2441,7 +2529,7 @@ int hpccg_hip_comm_allreduce_host(double* vals, int n, int op)
     hipStream_t s = nullptr;
     HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     HIP_TRY(hipMalloc(&d, sizeof(double) * n));
-    TRY(h2d(s, d, vals, sizeof(double) * n));
+    TRY(h2d_stream(s, d, vals, sizeof(double) * n));
     const ncclRedOp_t ops[3] = {ncclSum, ncclMin, ncclMax};
     NCCL_TRY(ncclAllReduce(d, d, n, ncclFloat64, ops[op], g_comm.comm, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -2583,7 +2671,7 @@ int hpccg_hip_matrix_generate(int nx, int ny, int nz, int use_7pt, hpccg_hip_mat
     M->nslots = acc * kSliceRows;
     M->width = M->uniform ? wmax : 0;
     TRY(dev_alloc(M, &M->d_slice_base, sb.size()));
-    TRY(h2d(M->stream, M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size()));
+    TRY(h2d(M, M->d_slice_base, sb.data(), sizeof(unsigned int) * sb.size()));
     TRY(dev_alloc(M, &M->d_cols, (size_t)M->nslots));
     TRY(dev_alloc(M, &M->d_vals, (size_t)M->nslots));
     M->has_sell = 1;
@@ -2892,6 +2980,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     } else if (!std::strcmp(key, "num_external")) *value = M->general ? M->ghost_hi : M->ghost_lo + M->ghost_hi;
     else if (!std::strcmp(key, "has_sell")) *value = M->has_sell;
     else if (!std::strcmp(key, "has_a")) *value = M->has_a;
+    else if (!std::strcmp(key, "a_reject")) *value = M->a_reject;
     else if (!std::strcmp(key, "has_pairs")) *value = M->has_pairs;
     else if (!std::strcmp(key, "a_width")) *value = M->a_width;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_pairs ? M->alds2_doubles : 0;
@@ -2919,7 +3008,7 @@ int hpccg_hip_solve_device(hpccg_hip_matrix* M, const double* b_dev, double* x_d
     }
     TRY(solve_impl(M, b, x, max_iter, tolerance, niters, normr, times, print));
     HIP_TRY(hipMemcpyAsync(x_dev, x, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
-    return wait_stream(M->stream);
+    return wait_matrix(M);
 }
 
 int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tolerance, int* niters,
@@ -3025,7 +3114,7 @@ int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
     double* scratch = nullptr;  // b | x of the timed solves
     HIP_TRY(hipMalloc(&scratch, 2 * sizeof(double) * n));
     auto done = [&](int rc) {
-        (void)hipStreamSynchronize(M->stream);
+        (void)flush_stream(M);  // the timed solves ran with the timing events (no system-scope release)
         (void)hipFree(scratch);
         (void)hipGetLastError();  // a refused candidate allocation only ends a phase
         M->trace.clear();         // the probe's solves are not the caller's
@@ -3042,16 +3131,19 @@ int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
     if (rc) return done(rc);
     M->place_us.push_back(us);
     double best_us = us;
-    // phase 0 places the values (copied), phase 1 the p ring (zeroed, as
-    // alloc_ring leaves it), each against the other's kept placement
-    const ptrdiff_t poff = M->d_p - M->d_pbuf;
-    for (int phase = 0; phase < 2; phase++) {
-        double** slot = phase == 0 ? &M->d_aval : &M->d_pbuf;
-        const size_t bytes = phase == 0 ? sizeof(double) * (size_t)std::max<long long>(1, M->a_slots)
-                                        : sizeof(double) * (size_t)M->pstride * M->ring_alloc;
+    // phase 0 places the values (copied), 1 the p ring, 2 r, 3 Ap (zeroed, as
+    // workspace allocation leaves them), each against the others' kept placement
+    const ptrdiff_t poff = M->d_p - M->d_pbuf, roff = M->d_r - M->d_rbuf;
+    for (int phase = 0; phase < kPlacePhases; phase++) {
+        double** const slots[kPlacePhases] = {&M->d_aval, &M->d_pbuf, &M->d_rbuf, &M->d_Ap};
+        const size_t counts[kPlacePhases] = {(size_t)std::max<long long>(1, M->a_slots),
+                                             (size_t)M->pstride * M->ring_alloc, (size_t)M->pstride, M->npad};
+        double** slot = slots[phase];
+        const size_t bytes = sizeof(double) * counts[phase];
         auto set = [&](double* q) {
             *slot = q;
             if (phase == 1) M->d_p = q + poff;
+            if (phase == 2) M->d_r = q + roff;
         };
         std::vector<double*> cand{*slot};
         size_t best = 0;
@@ -3078,11 +3170,11 @@ int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
             }
         }
         if (rc) best = 0;
-        (void)hipStreamSynchronize(M->stream);  // no launch reads the others any more
+        (void)flush_stream(M);  // no launch reads the others any more, and nothing of theirs is left in cache
         set(cand[best]);
         for (size_t i = 0; i < cand.size(); i++)
             if (i != best) (void)hipFree(cand[i]);
-        if (phase == 1 && hipMemsetAsync(cand[best], 0, bytes, M->stream) != hipSuccess && !rc)
+        if (phase > 0 && hipMemsetAsync(cand[best], 0, bytes, M->stream) != hipSuccess && !rc)
             rc = set_err(HPCCG_HIP_EHIP, "placement probe: hipMemsetAsync failed");  // the solves' values
         M->place_pick |= (int)best << (8 * phase);
         if (rc) break;
@@ -3251,10 +3343,7 @@ int hpccg_hip_ddot(int n, const double* x_dev, const double* y_dev, double* resu
     HIP_TRY(hipGetLastError());
     if (g_comm.nranks > 1)
         NCCL_TRY(ncclAllReduce(g_scratch.out, g_scratch.out + 1, 1, ncclFloat64, ncclSum, g_comm.comm, g_scratch.s));
-    HIP_TRY(hipMemcpyAsync(result, g_scratch.out + (g_comm.nranks > 1 ? 1 : 0), sizeof(double), hipMemcpyDeviceToHost,
-                           g_scratch.s));
-    HIP_TRY(hipStreamSynchronize(g_scratch.s));
-    return 0;
+    return d2h(g_scratch.s, result, g_scratch.out + (g_comm.nranks > 1 ? 1 : 0), sizeof(double));
 }
 
 int hpccg_hip_waxpby(int n, double alpha, const double* x_dev, double beta, const double* y_dev, double* w_dev)

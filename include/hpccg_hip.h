@@ -246,14 +246,15 @@ int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which, unsigned long long* v
  * Times a few eager CG iterations (median SpMV + update, scratch b and x; a
  * rank of an RCCL job is timed alone, no collective call) on the current
  * placement, then on up to `tries` physically contiguous placements of the
- * values (copied) and keeps the fastest, then likewise of the p ring
- * (zeroed); frees the rest. A phase stops early, keeping its best so far, when
- * free memory falls below the candidate size + 8 GiB. Results are unchanged
- * (bitwise). Option "placement_pick" reads the kept candidates: values index
- * | ring index << 8 (0 = the placement before the probe). */
+ * values (copied) and keeps the fastest, then likewise of the p ring, r and
+ * Ap (zeroed); frees the rest. A phase stops early, keeping its best so far,
+ * when free memory falls below the candidate size + 8 GiB. Results are
+ * unchanged (bitwise). Option "placement_pick" reads the kept candidates: one
+ * byte per buffer, values | ring << 8 | r << 16 | Ap << 24 (0 = the placement
+ * before the probe). */
 int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries);
 /* The last probe's times (us per iteration: [0] the placement before the
- * probe, then the values candidates, then the ring candidates): returns their
+ * probe, then the values, ring, r and Ap candidates in turn): returns their
  * count, copies up to cap. */
 int hpccg_hip_diag_placement(const hpccg_hip_matrix* M, double* us_out, int cap);
 /* Diagnostic (option dbg_timeline 1): block timeline of the last SpMV launch

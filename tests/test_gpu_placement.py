@@ -1,7 +1,7 @@
 """The placement probe (hpccg_hip_probe_placement):
 moving the values image and the p ring to other physical memory changes no
 result (bitwise), the probe records one time per candidate, keeps the fastest
-values and then the fastest ring placement, and the creation-time probe follows hpccg_hip_set_placement_probe."""
+values, then ring, r and Ap placement, and the creation-time probe follows hpccg_hip_set_placement_probe."""
 import numpy as np
 import pytest
 
@@ -18,12 +18,14 @@ def test_probe_keeps_bits(hp, gpu, kernel):
     assert M.placement().size == 0  # small image: the automatic probe is off
     base = solve_bits(hp, M, prob.b, 40)
     us = M.probe_placement(3)
-    assert us.shape == (7,) and np.all(us > 0)
+    assert us.shape == (13,) and np.all(us > 0)
     pick = M.get_option("placement_pick")
-    v, r = pick & 255, pick >> 8
-    assert v == int(np.argmin(us[:4]))  # values: the fastest of before + 3 candidates
-    ring = us[4:]
-    assert r == (int(np.argmin(ring)) + 1 if ring.min() < us[v] else 0)
+    best = us[0]
+    for phase in range(4):  # values, ring, r, Ap: each keeps the fastest so far
+        cand = us[1 + 3 * phase:4 + 3 * phase]
+        want = int(np.argmin(cand)) + 1 if cand.min() < best else 0
+        assert (pick >> (8 * phase)) & 255 == want, (phase, us, pick)
+        best = min(best, cand.min())
     assert solve_bits(hp, M, prob.b, 40) == base
     import torch
     assert solve_bits(hp, M, torch.as_tensor(prob.b, device=gpu), 40, gpu=gpu) == base
@@ -43,11 +45,11 @@ def test_probe_at_creation(hp, gpu):
     try:
         hp.set_placement_probe(2)
         M = hp.Matrix.from_hpc(prob)
-        assert M.placement().shape == (5,), {k: M.get_option(k) for k in ("has_a", "spmv_kernel", "a_width")}
+        assert M.placement().shape == (9,), {k: M.get_option(k) for k in ("has_a", "a_reject", "spmv_kernel", "a_width")}
         assert solve_bits(hp, M, prob.b, 30) == base
         M.close()
         G = hp.Matrix.generate(32, 32, 32)
-        assert G.placement().shape == (5,), {k: G.get_option(k) for k in ("has_a", "spmv_kernel", "a_width")}
+        assert G.placement().shape == (9,), {k: G.get_option(k) for k in ("has_a", "a_reject", "spmv_kernel", "a_width")}
         G.close()
         with pytest.raises(hp.HPCCGError):
             hp.set_placement_probe(-2)
@@ -69,7 +71,7 @@ def test_probe_group_members(hp, gpu):
 
     base = run()
     for M in Ms:
-        assert M.probe_placement(2).shape == (5,)
+        assert M.probe_placement(2).shape == (9,)
     assert run() == base
     for M in Ms:
         M.close()

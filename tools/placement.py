@@ -67,7 +67,7 @@ def probe_ab(hp, torch, args):
             r, sp = make_measure(hp, torch, M, b, x, args.max_iter)()
             print(json.dumps({"round": rnd, "probe": tries, "setup_s": round(setup_s, 3),
                               "probe_us": [round(float(v), 2) for v in M.placement()],
-                              "pick": [M.get_option("placement_pick") & 255, M.get_option("placement_pick") >> 8], "it_per_s": round(r, 1),
+                              "pick": [(M.get_option("placement_pick") >> (8 * i)) & 255 for i in range(4)], "it_per_s": round(r, 1),
                               "spmv_us": round(sp, 2)}), flush=True)
             M.close()
             del b, x
