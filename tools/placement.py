@@ -32,12 +32,13 @@ def main():
     ap.add_argument("--which", default="0,1,2,3")
     ap.add_argument("--mode", type=int, default=0, help="0 hipMalloc, 1 contiguous, 2/3/4 VMM 2 MB/64 MB/1 GB")
     ap.add_argument("--max-iter", type=int, default=200)
-    ap.add_argument("--probe", type=int, default=0, help="candidates of the creation probe (A/B mode)")
+    ap.add_argument("--probe", default="0", help="candidates of the creation probe (A/B mode; a list "
+                                                   "such as 6,10 alternates those counts after 0)")
     args = ap.parse_args()
     import torch
     hp = load_pkg()
     hp.set_device(0)
-    if args.probe:
+    if args.probe != "0":
         return probe_ab(hp, torch, args)
     hp.set_placement_probe(0)  # the creation placement as hipMalloc leaves it
     M = hp.Matrix.generate(args.n, args.n, args.n, use_7pt=args.stencil == 7)
@@ -57,7 +58,7 @@ def main():
 
 def probe_ab(hp, torch, args):
     for rnd in range(args.rounds):
-        for tries in (0, args.probe):
+        for tries in [0] + [int(v) for v in args.probe.split(",")]:
             hp.set_placement_probe(tries)
             t0 = time.perf_counter()
             M = hp.Matrix.generate(args.n, args.n, args.n, use_7pt=args.stencil == 7)
