@@ -526,6 +526,9 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
         }
         if (i < a.nslices) st_sc1(sp + i, slot_empty());
         v = wave_sum(v);
+        // the empties land before the group sum is published: within one launch
+        // (fused update) the same slots take the r.r partials after p.Ap's total
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) st_sc1(gp + g, v);
         if (g != top_group(m)) return;
         for (int j0 = 0; j0 < ng; j0 += kWave) {  // every other group's reducer came before
@@ -542,6 +545,7 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
         }
         const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
         for (int j = lane; j < ng; j += kWave) st_sc1(gp + j, slot_empty());
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as above: before pready)
         if (lane == 0) finish_dot(a, tot, which, k);
         return;
     }
@@ -563,6 +567,7 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
     // group reducer (this wave): sc1 loads of the group's partials
     const double v = wave_sum(i < a.nslices ? ld_sc1(sp + i) : 0.0);
     if (i < a.nslices) st_sc1(sp + i, slot_empty());
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the empties land before the publish
     if (lane == 0) {
         st_sc1(gp + g, v);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -578,6 +583,7 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
     if (role != 2) return;
     const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
     for (int j = lane; j < ng; j += kWave) st_sc1(gp + j, slot_empty());
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
         finish_dot(a, tot, which, k);
         __hip_atomic_store(gt + ng, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
