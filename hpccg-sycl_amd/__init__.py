@@ -154,10 +154,11 @@ def _ptr(a) -> int:
     if isinstance(a, int):
         return a
     if a.is_cuda:
+        import time
         import torch
         s = torch.cuda.current_stream(a.device)
-        while not s.query():  # polled: a blocking synchronize sleeps and wakes ~0.1 ms late
-            pass
+        while not s.query():  # polled (a blocking synchronize wakes ~0.1 ms late), the GIL released
+            time.sleep(0)
     return a.data_ptr()
 
 

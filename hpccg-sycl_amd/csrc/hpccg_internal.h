@@ -15,8 +15,12 @@ constexpr int kSliceRows = 512;
 constexpr int kNumXcd = 8;  // MI355X: 8 XCDs, blocks dealt round-robin
 constexpr int kReadyStride = 16;  // doubles between the fused update's p.Ap ready slots (128 B)
 
-// Indices into the device scalar block.
-enum Scalar : int { kRR = 0, kPAP = 1 };
+// Indices into the device scalar block (g = scal[0..], loc = scal[2..]).
+// kRRPar: with the fused update (a.fupd) r.r is also kept in two slots by the
+// parity of the iteration that reads it, g[kRRPar + (k & 1)] = r_{k-1}.r_{k-1},
+// so no block of a launch -- the ghost blocks are outside the launch's
+// p.Ap -> update -> r.r chain -- can read the r.r its own launch writes.
+enum Scalar : int { kRR = 0, kPAP = 1, kRRPar = 4 };
 
 // Stamp slots (SURVEY 8(a) TICK/TOCK classes, HPCCG.cpp:71-72); stamps are
 // stored at [k * kNumStampSlots + slot] for iteration k (0 = the prologue),
@@ -200,6 +204,10 @@ void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);
 void launch_cg_end(const CgArgs& a, hipStream_t s);
+// peer all-reduce self-test: rounds x both scalars through peer_allreduce, results to out[2 * rounds]
+void launch_peer_selftest(const CgArgs& a, int rounds, double* out, hipStream_t s);
+// solve start: state zeroed (spin budget set), every dot slot empty, tickets zero
+void launch_rearm(int* kst, double* partial, int np, unsigned int* tickets, int nt, int budget, hipStream_t s);
 void launch_cg_xflush(const CgArgs& a, hipStream_t s);  // pending deferred x updates
 
 // In-process rank group all-reduce of one CG scalar: g[which] of every rank =

@@ -281,6 +281,17 @@ __device__ __forceinline__ double* cur_p(const CgArgs& a, int k)
 // 100^3 same-process A/B: the ticket's round trip made every block of the
 // short update kernel wait (update 10.3 -> 23.6 us with r.r folded by tickets).
 // ---------------------------------------------------------------------------
+// A/B switches (tools/ab_libs.sh builds; never set in the product build)
+#ifdef HPCCG_NO_AP_DRAIN
+constexpr bool kNoApDrain = true;
+#else
+constexpr bool kNoApDrain = false;
+#endif
+#ifdef HPCCG_VEC_STATE
+constexpr bool kScalarState = false;
+#else
+constexpr bool kScalarState = true;
+#endif
 constexpr int kGroup = 64;
 constexpr int kTopThreads = 256;
 
@@ -482,6 +493,8 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
     } else if (!a.allreduce) {
         a.g[which] = s;
     }
+    // the r.r iteration k + 1 reads, by its parity (fused update: kRRPar)
+    if (which == kRR && a.fupd) a.g[kRRPar + ((k + 1) & 1)] = s;
     if (which == kRR) a.kst[a.fupd && ((k + 1) & 1) ? 2 : 0] = k + 1;
     if (a.fupd) {  // one copy per XCD group of update blocks, 128 B apart (no single hot line)
         for (int j = 0; j < kNumXcd; j++)
@@ -526,9 +539,9 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
         }
         if (i < a.nslices) st_sc1(sp + i, slot_empty());
         v = wave_sum(v);
-        // the empties land before the group sum is published: within one launch
-        // (fused update) the same slots take the r.r partials after p.Ap's total
+#ifndef HPCCG_NO_WAITER_DRAIN
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         if (lane == 0) st_sc1(gp + g, v);
         if (g != top_group(m)) return;
         for (int j0 = 0; j0 < ng; j0 += kWave) {  // every other group's reducer came before
@@ -545,7 +558,9 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
         }
         const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
         for (int j = lane; j < ng; j += kWave) st_sc1(gp + j, slot_empty());
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as above: before pready)
+#ifndef HPCCG_NO_WAITER_DRAIN
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         if (lane == 0) finish_dot(a, tot, which, k);
         return;
     }
@@ -674,7 +689,7 @@ __device__ __forceinline__ bool spmv_begin(const CgArgs& a, bool prologue, IterS
     bool run;
     if constexpr (kScalar) {
         st.k = iter_k_s<kFU>(a);
-        if (kFuse) st.rr = sld(a.g + kRR);
+        if (kFuse) st.rr = sld(a.g + (kFU ? kRRPar + a.kpar : kRR));
         const double h1 = sld(a.hist + max(st.k - 2, 0));  // r_{k-2}.r_{k-2} (k >= 2)
         run = st.k < a.max_iter && sqrt(st.k == 1 ? (kFuse ? st.rr : sld(a.hist)) : h1) > a.tol;
         if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -689,7 +704,7 @@ __device__ __forceinline__ bool spmv_begin(const CgArgs& a, bool prologue, IterS
         return run;
     }
     st.k = iter_k<kFU>(a);
-    if (kFuse) st.rr = a.g[kRR];
+    if (kFuse) st.rr = a.g[kFU ? kRRPar + a.kpar : kRR];
     run = cg_run(a, st.k, kFuse, st.rr);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         publish_iter(a, st.k, run);
@@ -933,7 +948,9 @@ __device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
     if ((int)blockIdx.x < a.gbase) return false;
     if (prologue) return true;
     const int k = iter_k<kFU>(a);
-    const double rr = a.g[kRR];
+    // fused update: this launch's r.r completion rewrites g[kRR] while ghost
+    // blocks may still start (they are outside its chain): the parity slot
+    const double rr = a.g[kFU ? kRRPar + a.kpar : kRR];
     if (!cg_run(a, k, true, rr)) return true;
     const double beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
     const double* __restrict__ pold = (k == 1) ? a.r : cur_p(a, k - 1);
@@ -980,7 +997,7 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue, uns
     // timeline, 7-pt 256^3: update blocks spent 3.5 of their 5.6 us before the
     // p.Ap total was in hand). A no-op launch after the end loads r for nothing.
     const int k = iter_k_s<true>(a);
-    const double rr = sld(a.g + kRR);  // r_{k-1}.r_{k-1}: the previous launch's
+    const double rr = sld(a.g + kRRPar + a.kpar);  // r_{k-1}.r_{k-1}: the previous launch's
     const Rows rv = ld(a.r + row);
     const Rows rv2 = nsl > 1 ? ld(a.r + row + kSliceRows) : Rows{{0.0, 0.0}};
     asm volatile("" ::: "memory");  // the prefetch stays ahead of the test
@@ -1166,7 +1183,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
         return;
     }
     IterState st;
-    if (!spmv_begin<kFuse, kFU, true>(a, prologue, st)) return;
+    if (!spmv_begin<kFuse, kFU, kScalarState>(a, prologue, st)) return;
     if (s < 0) return;
     if constexpr (kTL) tl_stamp(a, 2);
     const int wdt = kW > 0 ? kW : (int)(a.abase[s + 1] - a.abase[s]);
@@ -1232,7 +1249,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
             const double d = offp[kCtr] == 0 ? spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum, &ctr)
                                              : spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
             if (prologue) return;
-            if constexpr (kFU) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Ap landed before the partial
+            if constexpr (kFU && !kNoApDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Ap landed before the partial
             const double bs = block_sum<kBlock>(d);
             complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
             if constexpr (kTL) tl_end(a, 0);
@@ -1268,7 +1285,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
     // fused update: this wave's write-through Ap has landed before the block's
     // partial can be published (the update blocks read it once the p.Ap total
     // is out); explicit, not left to how __syncthreads() lowers
-    if constexpr (kFU) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (kFU && !kNoApDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const double bs = block_sum<kBlock>(d);
     complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
     if constexpr (kTL) tl_end(a, 0);
@@ -1848,6 +1865,32 @@ __global__ void k_stamp(CgArgs a, int slot, bool prologue)
 
 __global__ void k_end(CgArgs a) { mark_end(a); }
 
+// The peer all-reduce's creation-time self-test (peer_autotest): one lane runs
+// `rounds` all-reduces of each scalar slot through the kernels' own
+// peer_allreduce, contribution (prank + 1) + 0.5 k + 0.25 which.
+__global__ void k_peer_selftest(CgArgs a, int rounds, double* out)
+{
+    if (threadIdx.x != 0) return;
+    for (int k = 0; k < rounds; k++)
+        for (int which = 0; which < 2; which++)
+            out[2 * k + which] = peer_allreduce(a, (double)(a.prank + 1) + 0.5 * k + 0.25 * which, which, k);
+}
+
+// Every solve starts here, stream-ordered before its prologue (HPCCG.cpp:
+// 342-356 starts from r = b - A x with nothing carried over): the iteration
+// state and error record zeroed with the spin budget set, every dot slot --
+// slice partials, group sums, the fused update's p.Ap ready slots -- empty,
+// the arrival tickets zero. No solve then depends on what an earlier solve,
+// an aborted one or the placement probe's timed solves left in them.
+__global__ __launch_bounds__(256) void k_rearm(int* kst, double* partial, int np, unsigned int* tickets, int nt,
+                                               int budget)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < 2 * kKstDoubles) kst[i] = i == kErrBase + kErrBudget ? budget : 0;
+    if (i < np) partial[i] = slot_empty();
+    if (i < nt) tickets[i] = 0u;
+}
+
 // After the loop: x += alpha_j p_j for the iterations since the last batched
 // update (niters = kst[0] - 1 is final here).
 __global__ __launch_bounds__(kBlock) void k_xflush(CgArgs a)
@@ -2294,6 +2337,18 @@ void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s)
 }
 
 void launch_cg_end(const CgArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_end, dim3(1), dim3(64), 0, s, a); }
+
+void launch_peer_selftest(const CgArgs& a, int rounds, double* out, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_peer_selftest, dim3(1), dim3(64), 0, s, a, rounds, out);
+}
+
+void launch_rearm(int* kst, double* partial, int np, unsigned int* tickets, int nt, int budget, hipStream_t s)
+{
+    int cnt = np > nt ? np : nt;
+    if (cnt < 2 * kKstDoubles) cnt = 2 * kKstDoubles;
+    hipLaunchKernelGGL(k_rearm, dim3((cnt + 255) / 256), dim3(256), 0, s, kst, partial, np, tickets, nt, budget);
+}
 
 void launch_group_sum(const GroupSum& gs, hipStream_t s)
 {

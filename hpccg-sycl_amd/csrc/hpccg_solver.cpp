@@ -114,7 +114,10 @@ struct GroupCtx {
 thread_local GroupCtx g_group_ctx;
 int g_halo_mode = 0;  // 0 auto (slab when it serves every rank), 1 slab only, 2 gather
 int g_keep_sell = 0;  // keep the SELL-512 image beside SELL-512-A (kernel A/B, diagnostics)
-int g_place_tries = -1;  // placement probe at creation: -1 auto, 0 off, n candidates
+// placement probe at creation: -1 auto (images over kPlaceMinBytes), 0 off, n
+// candidates. Off by default since round 4: the probe's gain is
+// box-dependent and it is asked for explicitly (bench.py --placement).
+int g_place_tries = 0;
 constexpr int kPlaceAuto = 6;        // candidates of the automatic probe
 constexpr int kPlacePhases = 4;      // values, p ring, r, Ap
 constexpr double kPlaceMinBytes = 512e6;  // auto: only images that stream from HBM
@@ -216,6 +219,8 @@ struct hpccg_hip_matrix {
     hipStream_t stream = nullptr, stream2 = nullptr;
     hipEvent_t ev_pb = nullptr, ev_halo = nullptr;
     hipEvent_t ev_flush = nullptr;  // flush_stream's marker (default flags: system-scope release)
+    hipEvent_t ev_mid = nullptr;    // wait_matrix: blocking-sync marker before a solve's last graph chunk
+    int mid_pending = 0;            // ev_mid was recorded for the solve in flight
     long long nnz = 0, nslots = 0;
     int nslices = 0, grid = 0, width = 0, uniform = 0;
     int kernel = 0;       // SpMV kernel in use (SpmvKernel)
@@ -274,7 +279,8 @@ struct hpccg_hip_matrix {
     int solve_dirty = 0;       // a solve started and did not finish cleanly: reset the dot slots first
     int rhalo_group = 1;       // r-halo: the r.r all-reduce inside the planes' RCCL group (1) or before it (0)
     // peer-memory all-reduce of the CG scalars (option peer_allreduce)
-    int peer_ar = 0;
+    int peer_ar = -1;                  // option peer_allreduce: -1 auto (peer_ar_of), 0 off, 1 on
+    int peer_auto_ok = 0;              // auto: the creation-time self-test passed on every rank
     double* d_mbox = nullptr;          // this rank's mailbox (kMboxSlots, uncached / fine-grained)
     double** d_peers = nullptr;        // device table: every rank's mailbox, as this rank addresses it
     int peers_for = 0;                 // ranks the table was built for (0: none)
@@ -320,17 +326,14 @@ struct hpccg_hip_matrix {
 
 namespace {
 
-// Large device buffers (experiment, HPCCG_CONTIG=1): physically contiguous
-// allocations (hipDeviceMallocContiguous), falling back to hipMalloc.
+// Large device buffers. Never physically contiguous allocations
+// (hipDeviceMallocContiguous): on this stack they corrupted OTHER live
+// buffers and later allocations -- wrong b / x0 seen by the next solve, a
+// matrix image whose uploaded columns the A pass rejected -- even while the
+// contiguous buffers were held and never freed (DESIGN.md 4,
+// tools/diag_carry.py, profiles/r04_carry/).
 hipError_t big_malloc(void** p, size_t b)
 {
-    static const bool contig = [] {
-        const char* e = std::getenv("HPCCG_CONTIG");
-        return e && e[0] == '1';
-    }();
-    if (contig && b >= (16u << 20) && hipExtMallocWithFlags(p, b, hipDeviceMallocContiguous) == hipSuccess)
-        return hipSuccess;
-    (void)hipGetLastError();
     return hipMalloc(p, b);
 }
 
@@ -442,6 +445,7 @@ int free_matrix(hpccg_hip_matrix* M)
     if (M->d_peers) (void)hipFree(M->d_peers);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
     if (M->ev_flush) (void)hipEventDestroy(M->ev_flush);
+    if (M->ev_mid) (void)hipEventDestroy(M->ev_mid);
     for (hipEvent_t e : {M->ev_pb, M->ev_halo})
         if (e) (void)hipEventDestroy(e);
     if (M->stream) (void)hipStreamDestroy(M->stream);
@@ -1024,7 +1028,17 @@ bool rhalo_of(const hpccg_hip_matrix* M)
 // the members' kernels wait for each other inside the GPU, so they must run
 // side by side: eager launches on their own streams, at most two members
 // (GPU_MAX_HW_QUEUES = 4 queues hold two members' two streams each).
-bool peer_ar_of(const hpccg_hip_matrix* M) { return M->peer_ar && multi_of(M) && (!M->in_group || M->nranks <= 2); }
+// Auto (-1, the default): a process's rank of an RCCL job whose creation-time
+// self-test passed on every rank (peer_autotest), and the 1-rank emulation;
+// never an in-process group (its members would have to run side by side,
+// eagerly, instead of in one graph).
+bool emulated_multi(const hpccg_hip_matrix* M);
+bool peer_ar_of(const hpccg_hip_matrix* M)
+{
+    if (!multi_of(M) || M->peer_ar == 0) return false;
+    if (M->peer_ar > 0) return !M->in_group || M->nranks <= 2;
+    return !M->in_group && (emulated_multi(M) || M->peer_auto_ok);
+}
 
 // Both dots folded into their producing kernels (slot completion, no
 // k_finalize launch): same-process A/B against p.Ap folded + r.r through
@@ -1157,11 +1171,20 @@ int wait_matrix(hpccg_hip_matrix* M)
 {
     if (!M->ev_flush) HIP_TRY(hipEventCreateWithFlags(&M->ev_flush, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(M->ev_flush, M->stream));
+    // a long solve: sleep (blocking sync) until its last graph chunk starts,
+    // then poll only that tail -- a whole solve's spin held a host core
+    // (under the box's CPU quota an RCCL job's ranks would starve
+    // its proxy threads), while the blocking wait's late wake-up is hidden
+    // behind the chunk still running
+    if (M->mid_pending) {
+        M->mid_pending = 0;
+        HIP_TRY(hipEventSynchronize(M->ev_mid));
+    }
     for (;;) {
         const hipError_t e = hipEventQuery(M->ev_flush);
         if (e == hipSuccess) return 0;
         if (e != hipErrorNotReady) return set_err(HPCCG_HIP_EHIP, "hipEventQuery: %s", hipGetErrorString(e));
-        __builtin_ia32_pause();
+        std::this_thread::yield();
     }
 }
 
@@ -1351,11 +1374,15 @@ int enqueue_allreduce(hpccg_hip_matrix* M, const CgArgs& a, int which)
 
 int ensure_events(hpccg_hip_matrix* M, int slots)
 {
+    static const bool fence = [] {  // diagnostics: HPCCG_EVENT_FENCE=1 keeps the release
+        const char* e = std::getenv("HPCCG_EVENT_FENCE");
+        return e && e[0] == '1';
+    }();
     while ((int)M->ev.size() < 4 * slots) {
         hipEvent_t e;
         // no system-scope release at the record: a timed kernel's interval
         // would otherwise include writing back the caches it left dirty
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+        HIP_TRY(hipEventCreateWithFlags(&e, fence ? hipEventDefault : hipEventDisableSystemFence));
         M->ev.push_back(e);
     }
     return 0;
@@ -1877,22 +1904,88 @@ int clear_state(hpccg_hip_matrix* M)
 
 // A mailbox for the peer all-reduce: uncached device memory where the runtime
 // gives it (every load and store goes to memory: other GPUs write it over
-// xGMI), else fine-grained, else plain; every slot empty.
-int alloc_mbox(hpccg_hip_matrix* M, bool plain = false)
+// xGMI), else fine-grained; every slot empty. A plain (coarse-grained)
+// allocation is not used: nothing makes another GPU's stores into it visible
+// to this GPU's polls through its L2. Returns 1 when neither kind
+// could be allocated.
+int alloc_mbox(hpccg_hip_matrix* M)
 {
     const size_t bytes = sizeof(double) * kMboxSlots;
     void* p = nullptr;
-    if (plain || hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) {
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
-        if (plain || hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+        if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
             (void)hipGetLastError();
-            HIP_TRY(hipMalloc(&p, bytes));
+            return 1;
         }
     }
     M->d_mbox = static_cast<double*>(p);
     const std::vector<unsigned long long> empty(kMboxSlots, kSlotEmpty);
     TRY(h2d(M, M->d_mbox, empty.data(), bytes));
+    return 0;
+}
+
+// Collective over an RCCL job: every rank exports its mailbox (IPC handle),
+// all-gathers the handles and maps the others'. Every rank makes the same
+// RCCL calls whatever fails locally; *all_ok is the minimum over the ranks
+// (0: some rank could not take part, nothing is mapped).
+int map_peer_mailboxes(hpccg_hip_matrix* M, std::vector<double*>& table, int* all_ok)
+{
+    const int nr = M->nranks;
+    int ok = 1;
+    if (!M->d_mbox) {
+        const int rc = alloc_mbox(M);
+        if (rc > 1 || rc < 0) return rc;
+        ok = rc == 0;
+    }
+    hipIpcMemHandle_t h;
+    std::memset(&h, 0, sizeof h);
+    if (ok && hipIpcGetMemHandle(&h, M->d_mbox) != hipSuccess) {
+        (void)hipGetLastError();
+        ok = 0;
+    }
+    const size_t hb = sizeof(h), rec = hb + 8;  // handle | ok flag (padded)
+    std::vector<unsigned char> mine(rec, 0);
+    std::memcpy(mine.data(), &h, hb);
+    mine[hb] = (unsigned char)ok;
+    unsigned char* d = nullptr;
+    HIP_TRY(hipMalloc(&d, rec * (nr + 1)));
+    TRY(h2d(M, d + rec * nr, mine.data(), rec));
+    NCCL_TRY(ncclAllGather(d + rec * nr, d, rec, ncclUint8, g_comm.comm, M->stream));
+    std::vector<unsigned char> all(rec * nr);
+    TRY(d2h(M->stream, all.data(), d, rec * nr));
+    (void)hipFree(d);
+    int every = 1;
+    for (int q = 0; q < nr; q++) every = every && all[rec * q + hb] != 0;
+    int mapped = every;
+    for (int q = 0; q < nr && mapped; q++) {
+        if (q == M->rank) {
+            table[q] = M->d_mbox;
+            continue;
+        }
+        hipIpcMemHandle_t hq;
+        std::memcpy(&hq, all.data() + rec * q, hb);
+        void* ptr = nullptr;
+        if (hipIpcOpenMemHandle(&ptr, hq, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            (void)hipGetLastError();
+            mapped = 0;
+            break;
+        }
+        M->ipc_opened.push_back(ptr);
+        table[q] = static_cast<double*>(ptr);
+    }
+    // every rank learns whether every rank mapped every mailbox
+    int* f = nullptr;
+    HIP_TRY(hipMalloc(&f, 2 * sizeof(int)));
+    TRY(h2d(M, f, &mapped, sizeof(int)));
+    NCCL_TRY(ncclAllReduce(f, f + 1, 1, ncclInt32, ncclMin, g_comm.comm, M->stream));
+    TRY(d2h(M->stream, all_ok, f + 1, sizeof(int)));
+    (void)hipFree(f);
+    if (!*all_ok) {
+        for (void* ptr : M->ipc_opened) (void)hipIpcCloseMemHandle(ptr);
+        M->ipc_opened.clear();
+    }
     return 0;
 }
 
@@ -1914,41 +2007,19 @@ int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
     if (P > 1 || nr == 1) {
         for (int r = 0; r < P; r++) {
             HIP_TRY(hipSetDevice(Ms[r]->device));
-            if (!Ms[r]->d_mbox) TRY(alloc_mbox(Ms[r]));
+            if (!Ms[r]->d_mbox && alloc_mbox(Ms[r]))
+                return set_err(HPCCG_HIP_EINVAL, "peer_allreduce: no uncached or fine-grained mailbox memory");
         }
         for (int r = 0; r < P; r++)
             for (int q = 0; q < P; q++) tables[r][q] = Ms[q]->d_mbox;
     } else {  // one process per GPU: IPC handles through RCCL
         if (!g_comm.comm) return set_err(HPCCG_HIP_EINVAL, "peer_allreduce: no communicator");
-        if (!M->d_mbox) TRY(alloc_mbox(M));
-        hipIpcMemHandle_t h;
-        if (hipIpcGetMemHandle(&h, M->d_mbox) != hipSuccess) {  // not exportable: a plain allocation
-            (void)hipGetLastError();
-            (void)hipFree(M->d_mbox);
-            TRY(alloc_mbox(M, true));
-            HIP_TRY(hipIpcGetMemHandle(&h, M->d_mbox));
-        }
-        const size_t hb = sizeof(h);
-        unsigned char* d = nullptr;
-        HIP_TRY(hipMalloc(&d, hb * (nr + 1)));
-        TRY(h2d(M, d + hb * nr, &h, hb));
-        NCCL_TRY(ncclAllGather(d + hb * nr, d, hb, ncclUint8, g_comm.comm, M->stream));
-        HIP_TRY(hipStreamSynchronize(M->stream));
-        std::vector<unsigned char> all(hb * nr);
-        HIP_TRY(hipMemcpy(all.data(), d, hb * nr, hipMemcpyDeviceToHost));
-        (void)hipFree(d);
-        for (int q = 0; q < nr; q++) {
-            if (q == M->rank) {
-                tables[0][q] = M->d_mbox;
-                continue;
-            }
-            hipIpcMemHandle_t hq;
-            std::memcpy(&hq, all.data() + hb * q, hb);
-            void* ptr = nullptr;
-            HIP_TRY(hipIpcOpenMemHandle(&ptr, hq, hipIpcMemLazyEnablePeerAccess));
-            M->ipc_opened.push_back(ptr);
-            tables[0][q] = static_cast<double*>(ptr);
-        }
+        int all_ok = 0;
+        TRY(map_peer_mailboxes(M, tables[0], &all_ok));
+        if (!all_ok)
+            return set_err(HPCCG_HIP_EINVAL,
+                           "peer_allreduce: a rank's mailbox could not be exported or mapped (uncached or "
+                           "fine-grained memory over IPC)");
     }
     for (int r = 0; r < P; r++) {
         hpccg_hip_matrix* Mr = Ms[r];
@@ -1958,6 +2029,68 @@ int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
         Mr->peers_for = nr;
     }
     HIP_TRY(hipSetDevice(M->device));
+    return 0;
+}
+
+// Option peer_allreduce auto (-1, the default): at creation, every rank of an
+// RCCL job maps the others' mailboxes and runs kPeerTestRounds peer
+// all-reduces of both scalars through the kernels' own code (k_peer_selftest,
+// bounded waits), each checked bitwise on the host against the rank-ordered
+// sum; when every rank passes (RCCL min), the scalars are summed in the
+// kernels from then on and the iteration is one launch (fused update) plus
+// r's planes; otherwise RCCL's all-reduces stay. Collective: every rank
+// creates its matrix.
+constexpr int kPeerTestRounds = 64;
+
+int reset_dot_state(hpccg_hip_matrix* M);
+
+int peer_autotest(hpccg_hip_matrix* M)
+{
+    M->peer_auto_ok = 0;
+    const int nr = M->nranks;
+    if (nr > kMaxGroupRanks) return 0;
+    std::vector<double*> table(kMaxGroupRanks, nullptr);
+    int all_ok = 0;
+    TRY(map_peer_mailboxes(M, table, &all_ok));
+    if (!all_ok) return 0;
+    if (!M->d_peers) HIP_TRY(hipMalloc(&M->d_peers, sizeof(double*) * kMaxGroupRanks));
+    TRY(h2d(M, M->d_peers, table.data(), sizeof(double*) * kMaxGroupRanks));
+    M->peers_for = nr;
+    CgArgs a = make_args(M, M->d_b, M->d_x, 2, 0.0);
+    a.peer_ar = 1;
+    a.prank = M->rank;
+    a.pranks = nr;
+    a.mbox = M->d_mbox;
+    a.peers = M->d_peers;
+    const long long budget = std::min<long long>(200000000LL, M->spin_us * 100);  // at most 2 s
+    launch_rearm(M->d_kst, M->d_partial, (int)M->npartial, M->d_tickets, M->ntickets, (int)budget, M->stream);
+    double* out = nullptr;
+    HIP_TRY(hipMalloc(&out, sizeof(double) * 2 * kPeerTestRounds));
+    launch_peer_selftest(a, kPeerTestRounds, out, M->stream);
+    HIP_TRY(hipGetLastError());
+    std::vector<double> got(2 * kPeerTestRounds);
+    int err[kErrWords];
+    TRY(d2h(M->stream, got.data(), out, sizeof(double) * got.size()));
+    TRY(d2h(M->stream, err, M->d_kst + kErrBase, sizeof err));
+    (void)hipFree(out);
+    int ok = err[0] == kErrNone;
+    for (int k = 0; k < kPeerTestRounds && ok; k++)
+        for (int which = 0; which < 2; which++) {
+            double want = 0.0;  // k_peer_selftest's contributions, summed in rank order
+            for (int q = 0; q < nr; q++) want += (double)(q + 1) + 0.5 * k + 0.25 * which;
+            if (std::memcmp(&want, &got[2 * k + which], sizeof want) != 0) ok = 0;
+        }
+    int* f = nullptr;
+    HIP_TRY(hipMalloc(&f, 2 * sizeof(int)));
+    TRY(h2d(M, f, &ok, sizeof(int)));
+    NCCL_TRY(ncclAllReduce(f, f + 1, 1, ncclInt32, ncclMin, g_comm.comm, M->stream));
+    TRY(d2h(M->stream, &all_ok, f + 1, sizeof(int)));
+    (void)hipFree(f);
+    if (!all_ok) {  // a rank's waits may have given up: every mailbox empty again
+        TRY(reset_dot_state(M));
+        return 0;
+    }
+    M->peer_auto_ok = 1;
     return 0;
 }
 
@@ -1983,7 +2116,9 @@ int reset_dot_state(hpccg_hip_matrix* M)
 int check_device_error(hpccg_hip_matrix* const* Ms, int P, const int* err0)
 {
     static const char* what[] = {"", "slice partials of a dot group", "group sums of a dot",
-                                 "the p.Ap total (fused update)"};
+                                 "the p.Ap total (fused update)",
+                                 "another rank's contribution (peer all-reduce)"};
+    static const char* where[] = {"", "group", "group", "ready slot", "slot (dot * 2 + parity)"};
     int bad_rank = -1, e[kErrWords];
     for (int r = 0; r < P && bad_rank < 0; r++) {
         if (r == 0) {
@@ -2002,10 +2137,10 @@ int check_device_error(hpccg_hip_matrix* const* Ms, int P, const int* err0)
         return set_err(HPCCG_HIP_EHIP, "rank %d: a device wait timed out on another rank (code %d); solve abandoned",
                        rank, e[kErrAllRanks]);
     return set_err(HPCCG_HIP_EHIP,
-                   "rank %d: device wait timed out after %.0f us waiting for %s (block %d, group %d, iteration %d, "
+                   "rank %d: device wait timed out after %.0f us waiting for %s (block %d, %s %d, iteration %d, "
                    "dot %s); solve abandoned, dot slots reset",
-                   rank, (double)Ms[bad_rank]->spin_us, e[0] > 0 && e[0] <= 3 ? what[e[0]] : "?", e[1], e[2], e[3],
-                   e[4] == kPAP ? "p.Ap" : "r.r");
+                   rank, (double)Ms[bad_rank]->spin_us, e[0] > 0 && e[0] <= kErrPeerWait ? what[e[0]] : "?", e[1],
+                   e[0] > 0 && e[0] <= kErrPeerWait ? where[e[0]] : "slot", e[2], e[3], e[4] == kPAP ? "p.Ap" : "r.r");
 }
 
 // Solve on the ranks Ms[0..P) (P > 1: an in-process group; P == 1: this
@@ -2046,11 +2181,14 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     for (int r = 0; r < P; r++) {
         HIP_TRY(hipSetDevice(Ms[r]->device));
         av[r] = make_args(Ms[r], b_dev[r], x_dev[r], max_iter, tol);
-        // the last solve returned an error part-way: its slots may hold partials
+        // the last solve returned an error part-way: the peer mailbox too
         if (Ms[r]->solve_dirty) TRY(reset_dot_state(Ms[r]));
         Ms[r]->solve_dirty = 1;
-        TRY(clear_state(Ms[r]));  // iteration state, error record, spin budget
-        HIP_TRY(hipMemsetAsync(Ms[r]->d_tickets, 0, sizeof(unsigned int) * Ms[r]->ntickets, Ms[r]->stream));
+        // every solve starts from the same device state: iteration state,
+        // error record and spin budget, every dot and ready slot empty,
+        // tickets zero (one stream-ordered launch)
+        launch_rearm(Ms[r]->d_kst, Ms[r]->d_partial, (int)Ms[r]->npartial, Ms[r]->d_tickets, Ms[r]->ntickets,
+                     (int)std::min<long long>(Ms[r]->spin_us * 100, INT_MAX), Ms[r]->stream);
         HIP_TRY(hipMemsetAsync(Ms[r]->d_stamps, 0,
                                sizeof(unsigned long long) * (size_t)(max_iter + 2) * kNumStampSlots, Ms[r]->stream));
     }
@@ -2101,7 +2239,15 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
                 HIP_TRY(hipEventRecord(gev[r], Ms[r]->stream));
                 HIP_TRY(hipStreamWaitEvent(M->stream, gev[r], 0));
             }
-            for (; done + chunk <= iters; done += chunk) HIP_TRY(hipGraphLaunch(M->graph_exec, M->stream));
+            for (; done + chunk <= iters; done += chunk) {
+                if (done + 2 * chunk > iters && done > 0) {  // before the last chunk: wait_matrix sleeps to here
+                    if (!M->ev_mid)
+                        HIP_TRY(hipEventCreateWithFlags(&M->ev_mid, hipEventDisableTiming | hipEventBlockingSync));
+                    HIP_TRY(hipEventRecord(M->ev_mid, M->stream));
+                    M->mid_pending = 1;
+                }
+                HIP_TRY(hipGraphLaunch(M->graph_exec, M->stream));
+            }
             if (P > 1) {
                 HIP_TRY(hipEventRecord(gev[0], M->stream));
                 for (int r = 1; r < P; r++) HIP_TRY(hipStreamWaitEvent(Ms[r]->stream, gev[0], 0));
@@ -2207,6 +2353,9 @@ int finish_matrix(hpccg_hip_matrix* M)
     if (M->has_a && !g_keep_sell) drop_sell(M);
     M->kernel = choose_kernel(M);
     TRY(alloc_workspace(M));
+    // an RCCL job's ranks: the peer all-reduce self-test (collective)
+    if (M->nranks > 1 && !M->in_group && g_comm.comm && M->peer_ar < 0 && !std::getenv("HPCCG_NO_PEER_AUTO"))
+        TRY(peer_autotest(M));
     if (g_place_tries == 0 || M->in_group || !M->has_a) return 0;
     const int tries = g_place_tries > 0 ? g_place_tries : ((double)M->a_slots * 8.0 >= kPlaceMinBytes ? kPlaceAuto : 0);
     return tries ? hpccg_hip_probe_placement(M, tries) : 0;
@@ -2899,7 +3048,7 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         if (value < 1 || value > 20000000LL) return set_err(HPCCG_HIP_EINVAL, "spin_budget_us must be 1..2e7");
         M->spin_us = value;
     } else if (!std::strcmp(key, "peer_allreduce")) {
-        M->peer_ar = value ? 1 : 0;
+        M->peer_ar = value < 0 ? -1 : (value ? 1 : 0);
     } else if (!std::strcmp(key, "rhalo_group")) {
         // changes captured RCCL work that no kernel argument records: rebuild the graph
         if (M->rhalo_group != (value ? 1 : 0) && M->graph_exec) {
@@ -3065,11 +3214,13 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_u
 // Physical placement probe: the CG iteration rate of a large
 // image depends on where in HBM its values and the p ring were placed (306-350
 // us per 200^3 SpMV on one box, same code, same virtual layout). Time a few
-// CG iterations on the creation placement and on `tries` physically
-// contiguous candidates (each allocated while the earlier ones are held, so
-// each lands elsewhere), keep the fastest, free the rest. Values are copied,
-// the ring is zeroed as alloc_ring leaves it; nothing else moves and no
-// result changes.
+// CG iterations on the creation placement and on `tries` candidate
+// allocations (each allocated while the earlier ones are held, so each lands
+// elsewhere), keep the fastest, free the rest. Values are copied, the ring is
+// zeroed as alloc_ring leaves it; nothing else moves and no result changes.
+// Off unless asked for (hpccg_hip_set_placement_probe / bench.py --placement).
+// Round 3's contiguous candidates found the fast placements and corrupted
+// other buffers (big_malloc); plain candidates are safe and rarely faster.
 constexpr int kPlaceIters = 10;  // CG iterations per candidate (eager, event-timed)
 
 // Median SpMV + update time (us) of iterations 2.. of a short eager solve on
@@ -3086,7 +3237,7 @@ int probe_time(hpccg_hip_matrix* M, const double* b, double* x, double* us)
     int it = 0;
     double normr = 0.0;
     int rc = 0;
-    if (hipMemsetAsync(x, 0, sizeof(double) * std::max(1, M->nrow), M->stream) != hipSuccess)
+    if (hipMemsetAsync(x, 0, sizeof(double) * M->npad, M->stream) != hipSuccess)
         rc = set_err(HPCCG_HIP_EHIP, "placement probe: hipMemsetAsync failed");
     if (!rc) rc = solve_ranks(&M, 1, &b, &x, kPlaceIters, 0.0, &it, &normr, nullptr, 0);
     M->nranks = nr;
@@ -3101,6 +3252,23 @@ int probe_time(hpccg_hip_matrix* M, const double* b, double* x, double* us)
     return 0;
 }
 
+// The probe's candidates are plain allocations (big_malloc's reason). The
+// diagnostics of its side effects (tools/diag_carry.py) can ask for others:
+// HPCCG_PROBE_ALLOC = hipExtMallocWithFlags flags (4: contiguous -- this
+// corrupts other buffers, diagnostics only), HPCCG_PROBE_KEEP=1 holds the
+// dropped candidates for the life of the process instead of freeing them.
+static unsigned probe_alloc_flags()
+{
+    const char* e = std::getenv("HPCCG_PROBE_ALLOC");
+    return e && *e ? (unsigned)std::atoi(e) : hipDeviceMallocDefault;
+}
+static bool probe_keep()
+{
+    const char* e = std::getenv("HPCCG_PROBE_KEEP");
+    return e && e[0] == '1';
+}
+static std::vector<double*> g_probe_held;
+
 int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
 {
     if (!M) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
@@ -3110,8 +3278,10 @@ int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
     if (!tries || !M->has_a || !M->d_aval || !M->d_pbuf) return 0;
     HIP_TRY(hipSetDevice(M->device));
     HIP_TRY(hipStreamSynchronize(M->stream));
-    const size_t n = (size_t)std::max(1, M->nrow);
-    double* scratch = nullptr;  // b | x of the timed solves
+    // b | x of the timed solves, each padded to npad rows like the solver's
+    // own vectors (the slice kernels load whole slices)
+    const size_t n = M->npad;
+    double* scratch = nullptr;
     HIP_TRY(hipMalloc(&scratch, 2 * sizeof(double) * n));
     auto done = [&](int rc) {
         (void)flush_stream(M);  // the timed solves ran with the timing events (no system-scope release)
@@ -3151,7 +3321,7 @@ int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
             size_t fr = 0, tot = 0;
             if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < bytes + (size_t(8) << 30)) break;  // headroom
             double* q = nullptr;
-            if (hipExtMallocWithFlags(reinterpret_cast<void**>(&q), bytes, hipDeviceMallocContiguous) != hipSuccess)
+            if (hipExtMallocWithFlags(reinterpret_cast<void**>(&q), bytes, probe_alloc_flags()) != hipSuccess)
                 break;
             cand.push_back(q);
             const hipError_t e = phase == 0 ? hipMemcpyAsync(q, cand[0], bytes, hipMemcpyDeviceToDevice, M->stream)
@@ -3173,7 +3343,12 @@ int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
         (void)flush_stream(M);  // no launch reads the others any more, and nothing of theirs is left in cache
         set(cand[best]);
         for (size_t i = 0; i < cand.size(); i++)
-            if (i != best) (void)hipFree(cand[i]);
+            if (i != best) {
+                if (probe_keep())
+                    g_probe_held.push_back(cand[i]);  // diagnostics: never handed out again
+                else
+                    (void)hipFree(cand[i]);
+            }
         if (phase > 0 && hipMemsetAsync(cand[best], 0, bytes, M->stream) != hipSuccess && !rc)
             rc = set_err(HPCCG_HIP_EHIP, "placement probe: hipMemsetAsync failed");  // the solves' values
         M->place_pick |= (int)best << (8 * phase);

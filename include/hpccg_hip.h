@@ -117,9 +117,9 @@ int hpccg_hip_set_halo_mode(int mode);
  * (process-wide; default 0 frees it once the A image exists). Only for
  * kernel A/B comparisons ("spmv_kernel" 0 on a stencil matrix). */
 int hpccg_hip_set_keep_sell(int keep);
-/* Placement probe of matrices created afterwards (process-wide): -1 auto
- * (default: 6 candidates when the SELL-512-A values exceed 512 MB, off
- * otherwise and for in-process group members), 0 off, 1..16 candidates. See
+/* Placement probe of matrices created afterwards (process-wide): 0 off (the
+ * default), -1 auto (6 candidates when the SELL-512-A values exceed 512 MB,
+ * off otherwise and for in-process group members), 1..16 candidates. See
  * hpccg_hip_probe_placement. Replaces nothing in the reference. */
 int hpccg_hip_set_placement_probe(int tries);
 /* nrow, ncol (incl. ghosts), stored nnz, matrix slots (incl. padding),
@@ -235,7 +235,8 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_u
  * the old one is held until the matrix is destroyed, so the new one lands on
  * other physical memory): which & 255 = 0 the SELL-512-A values, 1 the p
  * ring, 2 r, 3 Ap, 4 x; which >> 8 = the allocation: 0 hipMalloc, 1
- * physically contiguous (hipDeviceMallocContiguous), 2/3/4 the VMM API
+ * physically contiguous (hipDeviceMallocContiguous -- corrupts other buffers
+ * of the process on this stack, DESIGN.md 5: diagnostics only), 2/3/4 the VMM API
  * (hipMemCreate + hipMemMap) at 2 MB / 64 MB / 1 GB virtual alignment. The
  * new virtual address goes to *va_out (may be NULL). For measuring the effect
  * of physical placement on the kernels' rate. Replaces nothing in the
@@ -245,8 +246,9 @@ int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which, unsigned long long* v
  * placement of its values and p ring (306-350 us per 200^3 SpMV on one box).
  * Times a few eager CG iterations (median SpMV + update, scratch b and x; a
  * rank of an RCCL job is timed alone, no collective call) on the current
- * placement, then on up to `tries` physically contiguous placements of the
- * values (copied) and keeps the fastest, then likewise of the p ring, r and
+ * placement, then on up to `tries` candidate allocations of the values
+ * (plain hipMalloc: contiguous ones corrupted other buffers; copied) and
+ * keeps the fastest, then likewise of the p ring, r and
  * Ap (zeroed); frees the rest. A phase stops early, keeping its best so far,
  * when free memory falls below the candidate size + 8 GiB. Results are
  * unchanged (bitwise). Option "placement_pick" reads the kept candidates: one

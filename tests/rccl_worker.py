@@ -31,6 +31,8 @@ def main():
     b, _, _ = M.vectors()
     n = c["nx"] * c["ny"] * c["nz"]
     x = torch.zeros(n, dtype=torch.float64, device=f"cuda:{local}")
+    auto = M.get_option("peer_allreduce")  # the creation-time self-test's verdict (auto mode)
+    M.set_option("peer_allreduce", 0)  # first the scalars through RCCL
     _, it, nr, times = hp.HPCCG(M, b, x, max_iter=500, device=True)
     tr = M.last_trace()
     ref_tr = [unhex(t) for t in c["trace_normr"]]
@@ -44,7 +46,8 @@ def main():
     # the update fused into the SpMV launch): two ranks, so the rank-order sum
     # is RCCL's sum bit for bit -- the whole solve must be
     got = (it, nr, tr.tobytes(), x.cpu().numpy().tobytes())
-    M.set_option("peer_allreduce", 1)
+    assert auto == 1, "the peer all-reduce self-test failed on two GPUs"
+    M.set_option("peer_allreduce", -1)  # the default
     x.zero_()
     _, it2, nr2, _ = hp.HPCCG(M, b, x, max_iter=500, device=True)
     assert M.get_option("peer_allreduce") == 1 and M.get_option("fuse_update") == (1 if M.get_option("spmv_kernel") == 1 else 0)

@@ -119,3 +119,35 @@ def test_reference_main_linked_to_our_library(gpu, tmp_path):
     ref = open(os.path.join(ROOT, "tests", "golden", "ref_cli_20x20x20.txt")).read()
     compare_to_reference(out, ref)
     assert keys(out) == keys(ref)  # the reference's own report code: exact key set
+
+
+def test_cli_yaml_fractions_at_200(hp, gpu, tmp_path):
+    """the CLI's GPU Summary reports the format-compulsory
+    fraction of the 8 TB/s peak (<= 1) beside SURVEY 8(d)'s credited one
+    (labelled as credited: it exceeds 1 at 200^3 because SELL-512-A stores no
+    per-entry column), and the compulsory one agrees with bench.py's roofline
+    frac -- hipEvents around the SpMV launch of an eager solve, the same bytes
+    plus the side blocks' -- within 5 %."""
+    out = run_cli(os.path.join(ROOT, "hpccg-sycl_amd", "bin", "test_HPCCG"), (200, 200, 200), tmp_path,
+                  env={"HPCCG_DEVICE_GENERATE": "1", "HPCCG_MAX_ITER": "120"})
+    v = values(out)
+    comp = float(v["GPU Summary/SPARSEMV compulsory fraction of 8 TB/s HBM peak"])
+    cred = float(v["GPU Summary/SPARSEMV credited fraction of 8 TB/s (can exceed 1)"])
+    assert 0.3 < comp <= 1.0, comp
+    assert cred > comp
+    import torch
+    M = hp.Matrix.generate(200, 200, 200)
+    b, _, _ = M.vectors()
+    n = 200 ** 3
+    x = torch.zeros(n, dtype=torch.float64, device=gpu)
+    hp.HPCCG(M, b, x, max_iter=40, device=True)  # warm
+    M.set_option("event_timing", 1)
+    x.zero_()
+    hp.HPCCG(M, b, x, max_iter=120, device=True)
+    kt = M.kernel_times()
+    launch_s = kt["spmv_ms"] / kt["spmv_launches"] * 1e-3
+    q = M.get_option("x_ring") - 1
+    side = (16.0 + 8.0 * q) / q * n if M.get_option("x_defer") == 2 else 0.0
+    bench_frac = (8.0 * M.info()["slots"] + 32.0 * n + side) / launch_s / 8e12
+    M.close()
+    assert abs(comp - bench_frac) <= 0.05 * bench_frac, (comp, bench_frac)

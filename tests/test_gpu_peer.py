@@ -97,3 +97,34 @@ def test_peer_allreduce_wait_is_bounded(hp, gpu):
     assert time.time() - t0 < 20.0
     got, _, _ = _group(hp, (16, 16, 12), False, {}, 1, max_iter=30)
     assert got == ref
+
+
+def test_peer_allreduce_auto_default(hp, gpu):
+    """Option peer_allreduce -1 (auto, the default): the multi-rank iteration
+    of the 1-rank emulation sums its scalars in the kernels and runs the update
+    inside the SpMV launch (one launch per iteration plus r's planes), while a
+    single rank and an in-process group keep their own paths; bitwise the plain
+    solve either way. (An RCCL job decides at creation from a collective
+    self-test: tests/rccl_worker.py.)"""
+    import torch
+    hp.comm_init(hp.comm_unique_id(), 1, 0)
+    try:
+        M = hp.Matrix.generate(40, 36, 30)
+        b, _, _ = M.vectors()
+        assert M.get_option("peer_allreduce") == 0  # one rank: nothing to sum
+        outs = []
+        for fc in (0, 2):
+            M.set_option("force_comm", fc)
+            x = torch.zeros(40 * 36 * 30, dtype=torch.float64, device=gpu)
+            _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=120, device=True)
+            outs.append((it, nr, M.last_trace().tobytes(), x.cpu().numpy().tobytes()))
+            assert M.get_option("fuse_update") == 1
+            assert M.get_option("peer_allreduce") == (1 if fc == 2 else 0)
+        assert outs[0] == outs[1]
+        M.close()
+    finally:
+        hp.comm_destroy()
+    Ms = hp.group_generate(24, 20, 9, 2)
+    assert all(m.get_option("peer_allreduce") == 0 for m in Ms)
+    for m in Ms:
+        m.close()

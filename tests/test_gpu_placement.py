@@ -54,7 +54,7 @@ def test_probe_at_creation(hp, gpu):
         with pytest.raises(hp.HPCCGError):
             hp.set_placement_probe(-2)
     finally:
-        hp.set_placement_probe(-1)
+        hp.set_placement_probe(0)
 
 
 def test_probe_group_members(hp, gpu):
