@@ -281,17 +281,6 @@ __device__ __forceinline__ double* cur_p(const CgArgs& a, int k)
 // 100^3 same-process A/B: the ticket's round trip made every block of the
 // short update kernel wait (update 10.3 -> 23.6 us with r.r folded by tickets).
 // ---------------------------------------------------------------------------
-// A/B switches (tools/ab_libs.sh builds; never set in the product build)
-#ifdef HPCCG_NO_AP_DRAIN
-constexpr bool kNoApDrain = true;
-#else
-constexpr bool kNoApDrain = false;
-#endif
-#ifdef HPCCG_VEC_STATE
-constexpr bool kScalarState = false;
-#else
-constexpr bool kScalarState = true;
-#endif
 constexpr int kGroup = 64;
 constexpr int kTopThreads = 256;
 
@@ -319,7 +308,10 @@ __device__ __forceinline__ int ngroups_of(const CgArgs& a) { return (a.nslices +
 // its own group sums after both. The fused update completes both dots in one
 // launch: with separate ranges no slot is reused within a launch, so a
 // waiter's resets need no drain before it publishes (they only have to land
-// before the next launch, which the kernel boundary guarantees).
+// before the next launch, which the kernel boundary guarantees). This is the
+// one invariant the slot completion relies on; round 3's drains before each
+// publish cost the 100^3 fused launch ~1 us on its critical path
+// (profiles/r04_carry/ab100_drains.log) and are gone.
 __device__ __forceinline__ double* slice_slots(const CgArgs& a, int which) { return a.partial + which * a.nslices; }
 __device__ __forceinline__ double* group_slots(const CgArgs& a, int which, int ng)
 {
@@ -537,11 +529,11 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        // the resets need no drain: each dot owns its slot range (slice_slots,
+        // group_slots), so no slot is read again within this launch, and the
+        // next launch starts after the kernel boundary (k_rearm at solve start)
         if (i < a.nslices) st_sc1(sp + i, slot_empty());
         v = wave_sum(v);
-#ifndef HPCCG_NO_WAITER_DRAIN
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         if (lane == 0) st_sc1(gp + g, v);
         if (g != top_group(m)) return;
         for (int j0 = 0; j0 < ng; j0 += kWave) {  // every other group's reducer came before
@@ -558,9 +550,6 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
         }
         const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
         for (int j = lane; j < ng; j += kWave) st_sc1(gp + j, slot_empty());
-#ifndef HPCCG_NO_WAITER_DRAIN
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         if (lane == 0) finish_dot(a, tot, which, k);
         return;
     }
@@ -1183,7 +1172,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
         return;
     }
     IterState st;
-    if (!spmv_begin<kFuse, kFU, kScalarState>(a, prologue, st)) return;
+    if (!spmv_begin<kFuse, kFU, true>(a, prologue, st)) return;
     if (s < 0) return;
     if constexpr (kTL) tl_stamp(a, 2);
     const int wdt = kW > 0 ? kW : (int)(a.abase[s + 1] - a.abase[s]);
@@ -1249,7 +1238,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
             const double d = offp[kCtr] == 0 ? spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum, &ctr)
                                              : spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
             if (prologue) return;
-            if constexpr (kFU && !kNoApDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Ap landed before the partial
+            if constexpr (kFU) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Ap landed before the partial
             const double bs = block_sum<kBlock>(d);
             complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
             if constexpr (kTL) tl_end(a, 0);
@@ -1285,7 +1274,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
     // fused update: this wave's write-through Ap has landed before the block's
     // partial can be published (the update blocks read it once the p.Ap total
     // is out); explicit, not left to how __syncthreads() lowers
-    if constexpr (kFU && !kNoApDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (kFU) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const double bs = block_sum<kBlock>(d);
     complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
     if constexpr (kTL) tl_end(a, 0);

@@ -287,7 +287,8 @@ struct hpccg_hip_matrix {
     std::vector<void*> ipc_opened;     // peers' mailboxes mapped from other processes
     double* d_hist = nullptr;
     unsigned long long* d_stamps = nullptr;
-    double* d_emul = nullptr;  // force_comm 2: self-exchange receive buffer
+    double* d_emul = nullptr;  // force_comm 2: self-exchange receive buffer (two planes)
+    int emul_plane = 0;        // force_comm 2: rows per plane (the largest column offset; 0 unknown)
     int hist_cap = 0;
     long long stamp_cap = 0;
     // pinned readback of a solve's results (state, scalars, r.r history, timer
@@ -862,6 +863,8 @@ int build_a_image(hpccg_hip_matrix* M)
     TRY(d2h(M->stream, off.data(), M->d_aoff, sizeof(int) * off.size()));
     HIP_TRY(hipStreamSynchronize(M->stream));
     M->has_a = 1;
+    for (int sl = 0; sl < S; sl++)
+        if (cnt[sl] > 0) M->emul_plane = std::max(M->emul_plane, off[(size_t)sl * kAMax + cnt[sl] - 1]);
     // halo-dependent units: they read rows of a ghost region ([-ghost_lo, 0)
     // or [n, n + ghost_hi), which the halo exchange writes); rows of the
     // zeroed guard zones beyond are never written and do not count
@@ -1122,7 +1125,13 @@ bool emulated_multi(const hpccg_hip_matrix* M)
 {
     return M->nranks == 1 && M->force_comm == 2 && g_comm.comm && g_comm.nranks == 1 && !M->in_group;
 }
-size_t emul_rows(const hpccg_hip_matrix* M) { return std::min<size_t>(M->nrow, 40000); }  // a 200^2 plane
+// The plane an interior z-slab rank of this problem exchanges with each
+// neighbour: the stencil's largest column offset (nx ny + nx + 1 for the
+// 27-point stencil, from the A image's offsets), else a 200^2 plane.
+size_t emul_rows(const hpccg_hip_matrix* M)
+{
+    return std::min<size_t>(M->nrow, M->emul_plane > 0 ? (size_t)M->emul_plane : 40000);
+}
 bool multi_of(const hpccg_hip_matrix* M) { return M->nranks > 1 || emulated_multi(M); }
 
 // Pinned readback layout: kst + error record (64 B), the scalars (64 B), then
@@ -1133,7 +1142,7 @@ static_assert(sizeof(int) * (kErrBase + kErrWords) <= kRbScal, "readback layout"
 
 int ensure_hist(hpccg_hip_matrix* M, int max_iter)
 {
-    if (emulated_multi(M) && !M->d_emul) TRY(dev_alloc(M, &M->d_emul, emul_rows(M), true));
+    if (emulated_multi(M) && !M->d_emul) TRY(dev_alloc(M, &M->d_emul, 2 * emul_rows(M), true));
     const int need = std::max(2, max_iter + 1);
     if (need > M->hist_cap) {
         dev_free(M, &M->d_hist, M->hist_cap);
@@ -1323,12 +1332,14 @@ int enqueue_halo(hpccg_hip_matrix* M, double* p, hipStream_t st, double* dst = n
     if (!dst) dst = p;
     if (g_comm.nranks == 1) {
         if (!emulated_multi(M)) return 0;
-        // force_comm 2: one rank sends a slab plane's worth of its first rows
-        // to itself, through the same RCCL calls and streams
+        // force_comm 2: an interior rank's two planes (its first and last
+        // rows) sent to itself, through the same RCCL calls and streams
         const size_t cnt = emul_rows(M);
         NCCL_TRY(ncclGroupStart());
         NCCL_TRY(ncclRecv(M->d_emul, cnt, ncclFloat64, 0, g_comm.comm, st));
         NCCL_TRY(ncclSend(p, cnt, ncclFloat64, 0, g_comm.comm, st));
+        NCCL_TRY(ncclRecv(M->d_emul + cnt, cnt, ncclFloat64, 0, g_comm.comm, st));
+        NCCL_TRY(ncclSend(p + M->nrow - cnt, cnt, ncclFloat64, 0, g_comm.comm, st));
         NCCL_TRY(ncclGroupEnd());
         return 0;
     }
@@ -1571,10 +1582,12 @@ int exch_rr_rhalo(const Ranks& R)
     NCCL_TRY(ncclGroupStart());
     if (a.allreduce && M->rhalo_group)
         NCCL_TRY(ncclAllReduce(a.loc + kRR, a.g + kRR, 1, ncclFloat64, ncclSum, g_comm.comm, M->stream));
-    if (g_comm.nranks == 1) {  // force_comm 2
+    if (g_comm.nranks == 1) {  // force_comm 2: an interior rank's two planes, to itself
         const size_t cnt = emul_rows(M);
         NCCL_TRY(ncclRecv(M->d_emul, cnt, ncclFloat64, 0, g_comm.comm, M->stream));
         NCCL_TRY(ncclSend(a.r, cnt, ncclFloat64, 0, g_comm.comm, M->stream));
+        NCCL_TRY(ncclRecv(M->d_emul + cnt, cnt, ncclFloat64, 0, g_comm.comm, M->stream));
+        NCCL_TRY(ncclSend(a.r + M->nrow - cnt, cnt, ncclFloat64, 0, g_comm.comm, M->stream));
     } else {
         const int r = g_comm.rank;
         if (r > 0) {
@@ -3411,7 +3424,7 @@ int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which, unsigned long long* v
     case 4: buf = &M->d_x; n = M->npad; break;
     default: return set_err(HPCCG_HIP_EINVAL, "which must be 0..4");
     }
-    if (mode < 0 || mode > 4) return set_err(HPCCG_HIP_EINVAL, "mode must be 0..4");
+    if (mode < 0 || mode > 6) return set_err(HPCCG_HIP_EINVAL, "mode must be 0..6");
     if (!*buf) return set_err(HPCCG_HIP_EINVAL, "buffer %d not allocated", which);
     double* nb = nullptr;
     const size_t bytes = sizeof(double) * n;
@@ -3419,6 +3432,10 @@ int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which, unsigned long long* v
         HIP_TRY(big_malloc(reinterpret_cast<void**>(&nb), bytes));
     } else if (mode == 1) {
         HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocContiguous));
+    } else if (mode == 5) {  // fine-grained (coherent) device memory
+        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocFinegrained));
+    } else if (mode == 6) {
+        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocUncached));
     } else {  // VMM at 2 MB, 64 MB or 1 GB virtual alignment
         const size_t align = mode == 2 ? (size_t(1) << 21) : mode == 3 ? (size_t(1) << 26) : (size_t(1) << 30);
         TRY(vmm_alloc(M, bytes, align, &nb));

@@ -236,7 +236,8 @@ int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_u
  * other physical memory): which & 255 = 0 the SELL-512-A values, 1 the p
  * ring, 2 r, 3 Ap, 4 x; which >> 8 = the allocation: 0 hipMalloc, 1
  * physically contiguous (hipDeviceMallocContiguous -- corrupts other buffers
- * of the process on this stack, DESIGN.md 5: diagnostics only), 2/3/4 the VMM API
+ * of the process on this stack, DESIGN.md 5: diagnostics only), 5 fine-grained
+ * (hipDeviceMallocFinegrained), 6 uncached, 2/3/4 the VMM API
  * (hipMemCreate + hipMemMap) at 2 MB / 64 MB / 1 GB virtual alignment. The
  * new virtual address goes to *va_out (may be NULL). For measuring the effect
  * of physical placement on the kernels' rate. Replaces nothing in the

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--7pt", dest="s7", action="store_true")
     ap.add_argument("--variants", default="0:0:1,1:0:1,2:0:1,2:1:1,2:0:0,2:1:0",
-                    help="force_comm:overlap:use_graph triples, optionally :spmv_kernel[:rhalo_group[:peer_allreduce]]")
+                    help="force_comm:overlap:use_graph triples, optionally :spmv_kernel[:rhalo_group[:peer_allreduce (-1 auto)]]")
     args = ap.parse_args()
     import torch
     hp = load_pkg()
@@ -44,7 +44,7 @@ def main():
             fc, ovl, graph = f[:3]
             M.set_option("spmv_kernel", f[3] if len(f) > 3 else -1)
             M.set_option("rhalo_group", f[4] if len(f) > 4 else 1)
-            M.set_option("peer_allreduce", f[5] if len(f) > 5 else 0)
+            M.set_option("peer_allreduce", f[5] if len(f) > 5 else -1)
             M.set_option("force_comm", fc)
             M.set_option("overlap", ovl)
             M.set_option("use_graph", graph)
