@@ -126,6 +126,12 @@ struct CgArgs {
     int prank, pranks;
     double* mbox;
     double* const* peers;
+    // r-halo by pull (option halo_pull): the neighbours read this rank's first
+    // rsend_lo and last rsend_hi rows of r straight from its memory, so the
+    // update stores those rows write-through and drains them before its r.r
+    // partial (0, 0: off)
+    int rsend_lo, rsend_hi;
+    int su2;                      // direct kernel: two slices per unit block (k_spmv_a2s; units are slice pairs)
 };
 // Block timeline (dbg_timeline), per unit of the ring pair kernel: [0] block
 // index | HW_ID << 32, [1] entry, [2] iteration state read, [3] windows staged
@@ -206,6 +212,10 @@ void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);
 void launch_cg_end(const CgArgs& a, hipStream_t s);
 // peer all-reduce self-test: rounds x both scalars through peer_allreduce, results to out[2 * rounds]
 void launch_peer_selftest(const CgArgs& a, int rounds, double* out, hipStream_t s);
+// r-halo by pull: ghost planes of r read from the neighbours' boundary rows
+// (system-scope loads) before the SpMV launch; lo_cnt rows lo_src -> lo_dst, hi likewise
+void launch_pull(const CgArgs& a, const double* lo_src, double* lo_dst, int lo_cnt, const double* hi_src, double* hi_dst,
+                 int hi_cnt, hipStream_t s, bool force = false);
 // solve start: state zeroed (spin budget set), every dot slot empty, tickets zero
 void launch_rearm(int* kst, double* partial, int np, unsigned int* tickets, int nt, int budget, hipStream_t s);
 void launch_cg_xflush(const CgArgs& a, hipStream_t s);  // pending deferred x updates

@@ -242,6 +242,27 @@ __device__ __forceinline__ void st_vec(const CgArgs& a, double* __restrict__ bas
     }
 }
 
+// halo_pull: is slice s among the rows the neighbours pull from this rank's r
+// (the first rsend_lo, the last rsend_hi)? Its r is stored write-through (one
+// 16-B sc1 store, the rows past n masked: the ghost_hi plane follows them) and
+// drained before the block's r.r partial, so a neighbour's pull -- ordered
+// after this rank's r.r contribution -- reads it from memory.
+__device__ __forceinline__ bool pulled_slice(const CgArgs& a, int s)
+{
+    return (a.rsend_lo > 0 && s * kSliceRows < a.rsend_lo) ||
+           (a.rsend_hi > 0 && (s + 1) * kSliceRows > a.n - a.rsend_hi);
+}
+__device__ __forceinline__ void st_r_through(const CgArgs& a, int row, const Rows& o)
+{
+    if (row + kRpt <= a.n) {
+        const d2v v = {o.v[0], o.v[1]};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(a.r + row), "v"(v) : "memory");
+    } else {
+        for (int i = 0; i < kRpt; i++)
+            if (row + i < a.n) asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(a.r + row + i), "v"(o.v[i]) : "memory");
+    }
+}
+
 // p of iteration k lives in ring buffer k % nring: the update of p reads
 // p_{k-1} from the previous buffer, and with x deferral the last nring p's
 // stay available for the batched x update.
@@ -1028,11 +1049,15 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue, uns
         asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(apw) : "v"(a.Ap + row) : "memory");
     // each slice exactly as k_update forms it: r, its partial with block_sum<256>'s shape
     // (wave sums, then the four in wave order), both slices through one barrier
+    const bool wt = pulled_slice(a, s) || (nsl > 1 && pulled_slice(a, s + 1));  // (block-uniform)
     auto slice = [&](const Rows& r_, const d2v& ap_, int rw) -> double {
         Rows rn;
         rn.v[0] = r_.v[0] + (-alpha) * ap_.x;
         rn.v[1] = r_.v[1] + (-alpha) * ap_.y;
-        st_vec(a, a.r, rw, rn);
+        if (wt)
+            st_r_through(a, rw, rn);
+        else
+            st_vec(a, a.r, rw, rn);
         double d = 0.0;
 #pragma unroll
         for (int i = 0; i < kRpt; i++)
@@ -1047,6 +1072,7 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue, uns
         ws2[0][threadIdx.x / kWave] = wa;
         ws2[1][threadIdx.x / kWave] = wb;
     }
+    if (wt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (pulled rows landed before the partial)
     __syncthreads();
     if (threadIdx.x >= kWave) return true;
     double bsj = 0.0;  // lane j: slice s + j's partial
@@ -1278,6 +1304,83 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
     const double bs = block_sum<kBlock>(d);
     complete_dot(a, spmv_units(a, 1), s, s, bs, kPAP, st.k);
     if constexpr (kTL) tl_end(a, 0);
+}
+
+// ---------------------------------------------------------------------------
+// The direct kernel over slice pairs (a.su2; option direct_spu 2, automatic
+// where the slices need between one and two rounds of resident blocks, e.g.
+// 100^3's 1954 against 256 CUs x 6 blocks): one 256-thread block runs slice
+// 2P, then slice 2P + 1, each exactly as k_spmv_a's width-kW loop does (the
+// same loads, products and order, the partial with block_sum's shape), and
+// hands both partials over like the pair kernel (two lanes, spu 2). The launch
+// is then one round of blocks: the 100^3 block timeline had the second round of
+// 418 slices running on a GPU whose unit blocks fell from 4.1 to 1.0 per CU
+// over the launch's second half. Same bits as k_spmv_a.
+// ---------------------------------------------------------------------------
+template <int kW, bool kNT, bool kFuse, int kPre, bool kFU>
+__global__ __launch_bounds__(kBlock) void k_spmv_a2s(CgArgs a, bool prologue)
+{
+    static_assert(kW > 0 && kPre > 0 && kPre <= kW, "uniform width, early loads");
+    const int P = unit_of(a);
+    const int s0 = P >= 0 ? 2 * P : a.nslices;
+    Rows vpre[kPre];
+    int offp[kW];
+    auto early = [&](int s) {
+        const double* __restrict__ vp0 = a.aval + (size_t)s * kW * kSliceRows + (size_t)threadIdx.x * kRpt;
+#pragma unroll
+        for (int j = 0; j < kPre; j++) vpre[j] = ld_m<kNT>(vp0 + (size_t)j * kSliceRows);
+#pragma unroll
+        for (int j = 0; j < kW; j++) offp[j] = a.aoff[(size_t)s * kAMax + j];
+    };
+    if (s0 < a.nslices) early(s0);
+    if constexpr (kFU) {
+        if (fused_update(a, prologue)) return;
+    }
+    if (side_flush<1, kW == 7 ? 8 : 4, kFU>(a, prologue)) return;
+    if (ghost_store<kFU>(a, prologue)) return;
+    IterState st;
+    if (!spmv_begin<kFuse, kFU, true>(a, prologue, st)) return;
+    if (s0 >= a.nslices) return;
+    const int nsl = min(2, a.nslices - s0);
+    double bs[2] = {0.0, 0.0};
+#pragma unroll 1
+    for (int h = 0; h < nsl; h++) {
+        const int s = s0 + h;
+        if (h > 0) early(s);
+        const int row = s * kSliceRows + threadIdx.x * kRpt;
+        const double* __restrict__ xr = cur_p(a, st.k) + row;
+        const double* __restrict__ rr_ = a.r + row;
+        const double* __restrict__ py = rr_;
+        if constexpr (kFuse) py = ((st.k == 1) ? a.r : cur_p(a, st.k - 1)) + row;
+        const double* __restrict__ vp = a.aval + (size_t)s * kW * kSliceRows + (size_t)threadIdx.x * kRpt;
+        double sum[kRpt] = {0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < kW; j++) {
+            const Rows v = j < kPre ? vpre[j] : ld_m<kNT>(vp + (size_t)j * kSliceRows);
+            const int oj = offp[j];
+            Rows xv;
+            if constexpr (kFuse) {
+                const Rows rv = ld_u(rr_ + oj);
+                const Rows yv = ld_u(py + oj);
+#pragma unroll
+                for (int i = 0; i < kRpt; i++) xv.v[i] = rv.v[i] + st.beta * yv.v[i];
+            } else {
+                xv = ld_u(xr + oj);
+            }
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xv.v[i];
+        }
+        const double d = spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
+        if (prologue) continue;
+        if constexpr (kFU) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Ap landed before the partial
+        bs[h] = block_sum<kBlock>(d);
+        __syncthreads();  // block_sum's wave sums are read before the next slice rewrites them
+    }
+    if (prologue || threadIdx.x >= kWave) return;
+    const int lane = threadIdx.x;
+    const double b1 = __shfl(bs[1], 0, kWave);  // both partials are valid in thread 0
+    const double bsj = lane == 0 ? bs[0] : (lane == 1 ? b1 : 0.0);
+    complete_dot_lanes(a, spmv_units(a, 2), P, s0, nsl, bsj, kPAP, st.k);
 }
 
 // ---------------------------------------------------------------------------
@@ -1828,11 +1931,16 @@ __global__ __launch_bounds__(kBlock) void k_update(CgArgs a)
             st_vec(a, a.x, row, xn);
         }
     }
-    st_vec(a, a.r, row, rn);
+    const bool wt = pulled_slice(a, s);  // (block-uniform)
+    if (wt)
+        st_r_through(a, row, rn);
+    else
+        st_vec(a, a.r, row, rn);
     double d = 0.0;
 #pragma unroll
     for (int i = 0; i < kRpt; i++)
         if (row + i < a.n) d += rn.v[i] * rn.v[i];
+    if (wt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // landed before the partial is published
     const double bs = block_sum<kBlock>(d);
     complete_dot(a, update_units(a), s, s, bs, kRR, k);
 }
@@ -1853,6 +1961,48 @@ __global__ void k_stamp(CgArgs a, int slot, bool prologue)
 }
 
 __global__ void k_end(CgArgs a) { mark_end(a); }
+
+// r-halo by pull (option halo_pull): before the SpMV launch of iteration k
+// (k_host's parity as the fused launch reads it), this rank's ghost planes of
+// r are read straight from the neighbours' boundary rows -- another GPU's
+// memory through IPC, or another group member's buffer -- with system-scope
+// loads (sc0 sc1: from memory, never a copy cached in this GPU's L2). The
+// neighbour stored those rows write-through and drained them before its r.r
+// partial (pulled_slice), and this rank's previous launch waited for that
+// contribution (peer all-reduce, or RCCL's after the neighbour's kernel end),
+// so the rows are r_{k-1}; the neighbour rewrites them only after this
+// rank's p.Ap of iteration k, which follows this kernel. Plain stores here:
+// the SpMV launch reading them starts after this kernel ends. A solve that
+// has ended leaves them alone.
+__global__ __launch_bounds__(256) void k_pull(CgArgs a, const double* __restrict__ lo_src, double* __restrict__ lo_dst,
+                                              int lo_cnt, const double* __restrict__ hi_src,
+                                              double* __restrict__ hi_dst, int hi_cnt, int force)
+{
+    if (!force) {  // (force: the creation-time test, outside a solve)
+        const int k = a.fupd ? (a.kst[1] ? a.max_iter : a.kst[a.kpar ? 2 : 0]) : a.kst[0];
+        const double rr = a.g[a.fupd ? kRRPar + a.kpar : kRR];
+        if (k >= a.max_iter || !(sqrt(k == 1 ? rr : a.hist[max(k - 2, 0)]) > a.tol)) return;  // cg_run
+        if (blockIdx.x == 0 && threadIdx.x == 0) stamp(a, k, kStampHalo);
+    }
+    constexpr int kU = 4;  // loads in flight per thread
+    const int tot = lo_cnt + hi_cnt;
+    const int stride = (int)(gridDim.x * blockDim.x) * kU;
+    for (int i0 = (int)(blockIdx.x * blockDim.x + threadIdx.x); i0 < tot; i0 += stride) {
+        double v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int i = i0 + u * (int)(gridDim.x * blockDim.x);
+            v[u] = i < tot ? __hip_atomic_load(i < lo_cnt ? lo_src + i : hi_src + (i - lo_cnt), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM)
+                           : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int i = i0 + u * (int)(gridDim.x * blockDim.x);
+            if (i < tot) (i < lo_cnt ? lo_dst[i] : hi_dst[i - lo_cnt]) = v[u];
+        }
+    }
+}
 
 // The peer all-reduce's creation-time self-test (peer_autotest): one lane runs
 // `rounds` all-reduces of each scalar slot through the kernels' own
@@ -2202,7 +2352,7 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         hipLaunchKernelGGL((k_spmv_a<7, true, true, 7, true, true, true>), sg, dim3(kBlock), 0, s, b, prologue);
         return;
     }
-    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 27 && !a.nt && a.apre != 0) {
+    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 27 && !a.nt && a.apre != 0 && !a.su2) {
         hipLaunchKernelGGL((k_spmv_a<27, false, true, 4, false, true, true>), sg, dim3(kBlock), 0, s, b, prologue);
         return;
     }
@@ -2262,7 +2412,19 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         break;
     }
     case kSpmvDirect:
-        if (a.a_width == 27) {
+        if (a.su2 && a.a_width == 27 && a.apre != 0) {  // slice pairs per block (direct_spu 2)
+#define HPCCG_A2S(NT)                                                                                            \
+    do {                                                                                                         \
+        if (fu)                                                                                                  \
+            hipLaunchKernelGGL((k_spmv_a2s<27, NT, true, 4, true>), sg, dim3(kBlock), 0, s, b, prologue);        \
+        else if (fuse)                                                                                           \
+            hipLaunchKernelGGL((k_spmv_a2s<27, NT, true, 4, false>), sg, dim3(kBlock), 0, s, b, prologue);       \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_spmv_a2s<27, NT, false, 4, false>), sg, dim3(kBlock), 0, s, b, prologue);      \
+    } while (0)
+            if (a.nt) HPCCG_A2S(true); else HPCCG_A2S(false);
+#undef HPCCG_A2S
+        } else if (a.a_width == 27) {
             if (a.apre == 0) {
                 if (a.nt) HPCCG_A(27, true, 0); else HPCCG_A(27, false, 0);
             } else {
@@ -2326,6 +2488,16 @@ void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s)
 }
 
 void launch_cg_end(const CgArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_end, dim3(1), dim3(64), 0, s, a); }
+
+void launch_pull(const CgArgs& a, const double* lo_src, double* lo_dst, int lo_cnt, const double* hi_src, double* hi_dst,
+                 int hi_cnt, hipStream_t s, bool force)
+{
+    const int tot = lo_cnt + hi_cnt;
+    if (tot <= 0) return;
+    const int grid = (tot + 4 * 256 - 1) / (4 * 256);
+    hipLaunchKernelGGL(k_pull, dim3(grid), dim3(256), 0, s, a, lo_src, lo_dst, lo_cnt, hi_src, hi_dst, hi_cnt,
+                       force ? 1 : 0);
+}
 
 void launch_peer_selftest(const CgArgs& a, int rounds, double* out, hipStream_t s)
 {

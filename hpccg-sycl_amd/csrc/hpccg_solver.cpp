@@ -236,6 +236,7 @@ struct hpccg_hip_matrix {
     int nt_store = -1;    // CG vector stores non-temporal (-1 auto: nt_store_effective)
     int a2_ring = kA2RingDefault;  // pair kernel: LDS-DMA value ring depth per wave (0: register loads; uniform widths 27 and 7)
     int tri = 1;          // direct kernel, width 7: x triple from adjacent lanes where the slice allows
+    int direct_spu = -1;  // direct kernel: slices per unit block, 1 or 2 (k_spmv_a2s); -1 auto (direct_su2)
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
                           // 2 also the multi-rank iteration with a self send/recv as its halo
@@ -281,6 +282,13 @@ struct hpccg_hip_matrix {
     // peer-memory all-reduce of the CG scalars (option peer_allreduce)
     int peer_ar = -1;                  // option peer_allreduce: -1 auto (peer_ar_of), 0 off, 1 on
     int peer_auto_ok = 0;              // auto: the creation-time self-test passed on every rank
+    // r-halo by pull (option halo_pull: -1 auto, 0 the RCCL / peer-copy planes, 1 on)
+    int halo_pull = -1;
+    int pull_auto_ok = 0;              // RCCL job: the creation-time pull test passed on every rank
+    double* d_pull_lo = nullptr;       // rank - 1's r (its local row 0), mapped here (RCCL job)
+    double* d_pull_hi = nullptr;       // rank + 1's r
+    int pull_lo_n = 0;                 // rank - 1's row count
+    std::vector<void*> ipc_r_opened;   // the neighbours' r buffers mapped from other processes
     double* d_mbox = nullptr;          // this rank's mailbox (kMboxSlots, uncached / fine-grained)
     double** d_peers = nullptr;        // device table: every rank's mailbox, as this rank addresses it
     int peers_for = 0;                 // ranks the table was built for (0: none)
@@ -435,6 +443,7 @@ int free_matrix(hpccg_hip_matrix* M)
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (void* p : M->ipc_opened) (void)hipIpcCloseMemHandle(p);
+    for (void* p : M->ipc_r_opened) (void)hipIpcCloseMemHandle(p);
     if (M->h_rb) (void)hipHostFree(M->h_rb);
     for (void* p : M->graveyard) (void)hipFree(p);
     for (const auto& v : M->vmm) {
@@ -1043,6 +1052,21 @@ bool peer_ar_of(const hpccg_hip_matrix* M)
     return !M->in_group && (emulated_multi(M) || M->peer_auto_ok);
 }
 
+// The r-halo by pull (option halo_pull, -1 auto the default): each rank's
+// k_pull reads its ghost planes of r from the neighbours' boundary rows before
+// the SpMV launch (an in-process group's members' buffers; another process's
+// through IPC, when the creation-time test passed on every rank; the 1-rank
+// emulation pulls its own rows into scratch) instead of the RCCL send/recv
+// group (or peer copies) after the update: no RCCL call left in the iteration
+// when the scalars are summed in the kernels.
+bool rhalo_of(const hpccg_hip_matrix* M);
+bool pull_of(const hpccg_hip_matrix* M)
+{
+    if (!rhalo_of(M) || M->halo_pull == 0) return false;
+    if (M->in_group || emulated_multi(M)) return true;
+    return M->pull_auto_ok != 0;  // (an RCCL job: its neighbours' r mapped and tested at creation)
+}
+
 // Both dots folded into their producing kernels (slot completion, no
 // k_finalize launch): same-process A/B against p.Ap folded + r.r through
 // k_finalize, 100^3 19249 vs 17814 CG it/s, 200^3 2619 vs 2543, 7-pt 256^3
@@ -1225,6 +1249,24 @@ bool fuse_update_effective(const hpccg_hip_matrix* M)
            x_defer_effective(M) == 2;
 }
 
+// The direct kernel over slice pairs (k_spmv_a2s, width 27 with its early
+// loads): automatic where one block per slice takes between one and two
+// rounds of the GPU's resident blocks (6 per CU at its 77 VGPRs), so pairs
+// fit in one round -- 100^3's 1954 slices on 256 CUs -- and no partial second
+// round runs on a half-empty GPU. Not for unit subsets (the eager overlap).
+bool direct_su2(const hpccg_hip_matrix* M)
+{
+    if (M->kernel != kSpmvDirect || M->a_width != 27 || M->a_pre == 0 || M->direct_spu == 1) return false;
+    if (multi_of(M) && !rhalo_of(M)) return false;
+    if (M->direct_spu == 2) return true;
+    static const int resident = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return 6 * cus;
+    }();
+    return M->nslices > resident && (M->nslices + 1) / 2 <= resident;
+}
+
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
 {
     CgArgs a;
@@ -1250,7 +1292,8 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.pready = M->d_partial + (M->npartial - kNumXcd * kReadyStride);
     a.rev = M->rev_update ? 1 : 0;
     a.nring = a.xdefer ? x_ring_effective(M) : (a.fuse_p ? 2 : 1);
-    const int units = M->kernel == kSpmvPairs ? (M->nslices + 1) / 2 : M->nslices;
+    a.su2 = direct_su2(M) ? 1 : 0;
+    const int units = (M->kernel == kSpmvPairs || a.su2) ? (M->nslices + 1) / 2 : M->nslices;
     a.s0 = 0;
     a.sn0 = units;
     a.s1 = a.sn1 = 0;
@@ -1281,6 +1324,10 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
         a.peers = M->d_peers;
     }
     a.stamps = M->d_stamps;
+    if (pull_of(M)) {  // the rows the neighbours pull go write-through (pulled_slice)
+        a.rsend_lo = emulated_multi(M) ? (int)emul_rows(M) : M->send_lo;
+        a.rsend_hi = emulated_multi(M) ? (int)emul_rows(M) : M->send_hi;
+    }
     a.slice_base = M->d_slice_base;
     a.cols = M->d_cols;
     a.vals = M->d_vals;
@@ -1547,6 +1594,10 @@ int exch_allreduce(const Ranks& R, int which)
 // after the rank-ordered sum (whose stream waited for every member's update).
 int exch_rr_rhalo(const Ranks& R)
 {
+    if (pull_of(R.M[0])) {  // the planes are pulled before the next SpMV: the r.r all-reduce only
+        if (!R.a[0].allreduce) return 0;  // (peer all-reduce: summed in the kernels)
+        return R.P > 1 ? group_allreduce(R, kRR) : enqueue_allreduce(R.M[0], R.a[0], kRR);
+    }
     if (R.P > 1) {
         if (R.a[0].allreduce) {
             TRY(group_allreduce(R, kRR));
@@ -1650,6 +1701,44 @@ bool overlap_ok(const Ranks& R)
     return true;
 }
 
+// The r-halo by pull (pull_of): rank r's ghost planes of r from its
+// neighbours' boundary rows, on its stream, right before its SpMV launch.
+int enqueue_pull(const Ranks& R, int r, const CgArgs& a)
+{
+    hpccg_hip_matrix* M = R.M[r];
+    const double *lo_src = nullptr, *hi_src = nullptr;
+    double *lo_dst = a.r - M->ghost_lo, *hi_dst = a.r + M->nrow;
+    int lo = 0, hi = 0;
+    if (R.P > 1) {  // an in-process group: the members' own buffers
+        if (r > 0 && M->ghost_lo) {
+            lo = M->ghost_lo;
+            lo_src = R.a[r - 1].r + R.M[r - 1]->nrow - lo;
+        }
+        if (r < R.P - 1 && M->ghost_hi) {
+            hi = M->ghost_hi;
+            hi_src = R.a[r + 1].r;
+        }
+    } else if (emulated_multi(M)) {  // an interior rank's two planes: its own rows into scratch
+        lo = hi = (int)emul_rows(M);
+        lo_src = a.r;
+        hi_src = a.r + M->nrow - hi;
+        lo_dst = M->d_emul;
+        hi_dst = M->d_emul + lo;
+    } else {  // an RCCL job: the neighbours' r, IPC-mapped at creation
+        if (M->ghost_lo) {
+            lo = M->ghost_lo;
+            lo_src = M->d_pull_lo ? M->d_pull_lo + M->pull_lo_n - lo : nullptr;
+        }
+        if (M->ghost_hi) {
+            hi = M->ghost_hi;
+            hi_src = M->d_pull_hi;
+        }
+        if ((lo && !lo_src) || (hi && !hi_src)) return set_err(HPCCG_HIP_EINVAL, "halo_pull: a neighbour's r is not mapped");
+    }
+    launch_pull(a, lo_src, lo_dst, lo, hi_src, hi_dst, hi, M->stream);
+    return 0;
+}
+
 int enqueue_spmv_overlapped(const Ranks& R, int slot, int k_host)
 {
     for (int r = 0; r < R.P; r++) {
@@ -1725,11 +1814,13 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
                 launch_cg_p_boundary(R.a[r], R.M[r]->send_lo, R.M[r]->send_hi, R.M[r]->stream);
         }
         if (multi && !R.a[0].rhalo) TRY(exch_halo(R, k_host, false));  // (rhalo: r's planes came with r.r)
+        const bool pull = multi && pull_of(R.M[0]);
         for (int r = 0; r < R.P; r++) {
             hpccg_hip_matrix* M = R.M[r];
             CgArgs a = R.a[r];
             a.kpar = k_host & 1;  // fused update: the parity slot of k (iter_k)
             TRY(use_device(R, r));
+            if (pull) TRY(enqueue_pull(R, r, a));  // r's ghost planes for this SpMV
             if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
             launch_cg_spmv(a, M->kernel, false, M->stream);
             if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
@@ -2057,6 +2148,114 @@ constexpr int kPeerTestRounds = 64;
 
 int reset_dot_state(hpccg_hip_matrix* M);
 
+// Option halo_pull auto in an RCCL job (collective, at creation): every rank
+// exports its r buffer (IPC handle, the offset of local row 0, its row
+// count), maps its two neighbours', and tests a pull: each rank stores
+// 0.5 g + 1 at every global row g of its first send_lo and last send_hi rows,
+// the ranks meet (an RCCL all-reduce), each pulls its ghost planes with the
+// kernels' own k_pull and checks them on the host. Used only when every rank
+// passes (RCCL min); otherwise r's planes stay on RCCL.
+int pull_autotest(hpccg_hip_matrix* M)
+{
+    M->pull_auto_ok = 0;
+    const int nr = M->nranks, me = M->rank;
+    hipIpcMemHandle_t h;
+    std::memset(&h, 0, sizeof h);
+    int ok = M->d_rbuf != nullptr;
+    if (ok && hipIpcGetMemHandle(&h, M->d_rbuf) != hipSuccess) {
+        (void)hipGetLastError();
+        ok = 0;
+    }
+    const size_t hb = sizeof h, rec = hb + 16;  // handle | offset of row 0 (B) | nrow | ok
+    std::vector<unsigned char> mine(rec, 0);
+    std::memcpy(mine.data(), &h, hb);
+    const long long off = (long long)((char*)M->d_r - (char*)M->d_rbuf);
+    std::memcpy(mine.data() + hb, &off, 8);
+    std::memcpy(mine.data() + hb + 8, &M->nrow, 4);
+    std::memcpy(mine.data() + hb + 12, &ok, 4);
+    unsigned char* d = nullptr;
+    HIP_TRY(hipMalloc(&d, rec * (nr + 1)));
+    TRY(h2d(M, d + rec * nr, mine.data(), rec));
+    NCCL_TRY(ncclAllGather(d + rec * nr, d, rec, ncclUint8, g_comm.comm, M->stream));
+    std::vector<unsigned char> all(rec * nr);
+    TRY(d2h(M->stream, all.data(), d, rec * nr));
+    (void)hipFree(d);
+    auto field = [&](int q, size_t at, void* out, size_t n) { std::memcpy(out, all.data() + rec * q + at, n); };
+    int mapped = 1;
+    for (int side = 0; side < 2 && mapped; side++) {
+        const int q = side == 0 ? me - 1 : me + 1;
+        const int need = side == 0 ? M->ghost_lo : M->ghost_hi;
+        if (q < 0 || q >= nr || need == 0) continue;
+        int qok = 0, qn = 0;
+        long long qoff = 0;
+        field(q, hb + 12, &qok, 4);
+        field(q, hb + 8, &qn, 4);
+        field(q, hb, &qoff, 8);
+        hipIpcMemHandle_t hq;
+        field(q, 0, &hq, hb);
+        void* ptr = nullptr;
+        if (!qok || hipIpcOpenMemHandle(&ptr, hq, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            (void)hipGetLastError();
+            mapped = 0;
+            break;
+        }
+        M->ipc_r_opened.push_back(ptr);
+        double* base = reinterpret_cast<double*>(static_cast<char*>(ptr) + qoff);
+        if (side == 0) {
+            M->d_pull_lo = base;
+            M->pull_lo_n = qn;
+        } else {
+            M->d_pull_hi = base;
+        }
+    }
+    int* f = nullptr;
+    HIP_TRY(hipMalloc(&f, 2 * sizeof(int)));
+    auto all_min = [&](int v, int* out) -> int {
+        TRY(h2d(M, f, &v, sizeof(int)));
+        NCCL_TRY(ncclAllReduce(f, f + 1, 1, ncclInt32, ncclMin, g_comm.comm, M->stream));
+        TRY(d2h(M->stream, out, f + 1, sizeof(int)));
+        return 0;
+    };
+    int all_ok = 0;
+    TRY(all_min(mapped, &all_ok));
+    if (all_ok) {
+        // the test pattern in this rank's sent rows, then every rank pulls
+        auto pattern = [&](long long g) { return 0.5 * (double)g + 1.0; };
+        std::vector<double> v;
+        for (int i = 0; i < M->send_lo; i++) v.push_back(pattern((long long)M->start_row + i));
+        if (M->send_lo) TRY(h2d(M, M->d_r, v.data(), sizeof(double) * v.size()));
+        v.clear();
+        for (int i = M->nrow - M->send_hi; i < M->nrow; i++) v.push_back(pattern((long long)M->start_row + i));
+        if (M->send_hi) TRY(h2d(M, M->d_r + M->nrow - M->send_hi, v.data(), sizeof(double) * v.size()));
+        int dummy = 0;
+        TRY(all_min(1, &dummy));  // every rank's rows are in place
+        CgArgs a = make_args(M, M->d_b, M->d_x, 2, 0.0);
+        const int lo = M->d_pull_lo ? M->ghost_lo : 0, hi = M->d_pull_hi ? M->ghost_hi : 0;
+        launch_pull(a, M->d_pull_lo ? M->d_pull_lo + M->pull_lo_n - lo : nullptr, M->d_r - M->ghost_lo, lo,
+                    M->d_pull_hi, M->d_r + M->nrow, hi, M->stream, true);
+        HIP_TRY(hipGetLastError());
+        std::vector<double> gl(lo), gh(hi);
+        if (lo) TRY(d2h(M->stream, gl.data(), M->d_r - lo, sizeof(double) * lo));
+        if (hi) TRY(d2h(M->stream, gh.data(), M->d_r + M->nrow, sizeof(double) * hi));
+        int good = 1;
+        for (int i = 0; i < lo && good; i++) good = gl[i] == pattern((long long)M->start_row - lo + i);
+        for (int i = 0; i < hi && good; i++) good = gh[i] == pattern((long long)M->start_row + M->nrow + i);
+        TRY(all_min(good, &all_ok));
+        TRY(all_min(1, &dummy));  // no rank clears its rows while another still pulls
+        HIP_TRY(hipMemsetAsync(M->d_rbuf, 0, sizeof(double) * (size_t)M->pstride, M->stream));
+        TRY(flush_stream(M));
+    }
+    (void)hipFree(f);
+    if (!all_ok) {
+        for (void* ptr : M->ipc_r_opened) (void)hipIpcCloseMemHandle(ptr);
+        M->ipc_r_opened.clear();
+        M->d_pull_lo = M->d_pull_hi = nullptr;
+        return 0;
+    }
+    M->pull_auto_ok = 1;
+    return 0;
+}
+
 int peer_autotest(hpccg_hip_matrix* M)
 {
     M->peer_auto_ok = 0;
@@ -2366,12 +2565,18 @@ int finish_matrix(hpccg_hip_matrix* M)
     if (M->has_a && !g_keep_sell) drop_sell(M);
     M->kernel = choose_kernel(M);
     TRY(alloc_workspace(M));
-    // an RCCL job's ranks: the peer all-reduce self-test (collective)
-    if (M->nranks > 1 && !M->in_group && g_comm.comm && M->peer_ar < 0 && !std::getenv("HPCCG_NO_PEER_AUTO"))
-        TRY(peer_autotest(M));
-    if (g_place_tries == 0 || M->in_group || !M->has_a) return 0;
-    const int tries = g_place_tries > 0 ? g_place_tries : ((double)M->a_slots * 8.0 >= kPlaceMinBytes ? kPlaceAuto : 0);
-    return tries ? hpccg_hip_probe_placement(M, tries) : 0;
+    if (g_place_tries != 0 && !M->in_group && M->has_a) {
+        const int tries =
+            g_place_tries > 0 ? g_place_tries : ((double)M->a_slots * 8.0 >= kPlaceMinBytes ? kPlaceAuto : 0);
+        if (tries) TRY(hpccg_hip_probe_placement(M, tries));
+    }
+    // an RCCL job's ranks (collective, after the probe: it may move r): the
+    // peer all-reduce and the halo pull self-tests
+    if (M->nranks > 1 && !M->in_group && g_comm.comm) {
+        if (M->peer_ar < 0 && !std::getenv("HPCCG_NO_PEER_AUTO")) TRY(peer_autotest(M));
+        if (M->halo_pull != 0 && !M->general && !std::getenv("HPCCG_NO_PULL_AUTO")) TRY(pull_autotest(M));
+    }
+    return 0;
 }
 
 template <class RowLen, class RowAt>
@@ -3062,6 +3267,11 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->spin_us = value;
     } else if (!std::strcmp(key, "peer_allreduce")) {
         M->peer_ar = value < 0 ? -1 : (value ? 1 : 0);
+    } else if (!std::strcmp(key, "direct_spu")) {  // -1 auto, 1 or 2 slices per unit block
+        if (value != -1 && value != 1 && value != 2) return set_err(HPCCG_HIP_EINVAL, "direct_spu must be -1, 1 or 2");
+        M->direct_spu = (int)value;
+    } else if (!std::strcmp(key, "halo_pull")) {  // -1 auto, 0 off (the RCCL / peer-copy planes), 1 on where possible
+        M->halo_pull = value < 0 ? -1 : (value ? 1 : 0);
     } else if (!std::strcmp(key, "rhalo_group")) {
         // changes captured RCCL work that no kernel argument records: rebuild the graph
         if (M->rhalo_group != (value ? 1 : 0) && M->graph_exec) {
@@ -3129,6 +3339,8 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "rhalo_group")) *value = M->rhalo_group;
     else if (!std::strcmp(key, "peer_allreduce")) *value = peer_ar_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "rhalo")) *value = rhalo_of(M) ? 1 : 0;
+    else if (!std::strcmp(key, "halo_pull")) *value = pull_of(M) ? 1 : 0;
+    else if (!std::strcmp(key, "direct_spu")) *value = direct_su2(M) ? 2 : 1;
     else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
     else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;
     else if (!std::strcmp(key, "stage16")) *value = M->stage16;
@@ -3318,6 +3530,7 @@ int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
     // workspace allocation leaves them), each against the others' kept placement
     const ptrdiff_t poff = M->d_p - M->d_pbuf, roff = M->d_r - M->d_rbuf;
     for (int phase = 0; phase < kPlacePhases; phase++) {
+        if (phase == 2 && M->pull_auto_ok) continue;  // the neighbours have this r mapped (halo_pull)
         double** const slots[kPlacePhases] = {&M->d_aval, &M->d_pbuf, &M->d_rbuf, &M->d_Ap};
         const size_t counts[kPlacePhases] = {(size_t)std::max<long long>(1, M->a_slots),
                                              (size_t)M->pstride * M->ring_alloc, (size_t)M->pstride, M->npad};

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--7pt", dest="s7", action="store_true")
     ap.add_argument("--variants", default="0:0:1,1:0:1,2:0:1,2:1:1,2:0:0,2:1:0",
-                    help="force_comm:overlap:use_graph triples, optionally :spmv_kernel[:rhalo_group[:peer_allreduce (-1 auto)]]")
+                    help="force_comm:overlap:use_graph triples, optionally :spmv_kernel[:rhalo_group[:peer_allreduce[:halo_pull]]] (-1 auto)")
     args = ap.parse_args()
     import torch
     hp = load_pkg()
@@ -45,6 +45,7 @@ def main():
             M.set_option("spmv_kernel", f[3] if len(f) > 3 else -1)
             M.set_option("rhalo_group", f[4] if len(f) > 4 else 1)
             M.set_option("peer_allreduce", f[5] if len(f) > 5 else -1)
+            M.set_option("halo_pull", f[6] if len(f) > 6 else -1)
             M.set_option("force_comm", fc)
             M.set_option("overlap", ovl)
             M.set_option("use_graph", graph)
@@ -70,6 +71,7 @@ def main():
                               "kernel": M.get_option("spmv_kernel"), "fuse_p": M.get_option("fuse_p"),
                               "rhalo": M.get_option("rhalo"), "rhalo_group": M.get_option("rhalo_group"),
                               "peer_allreduce": M.get_option("peer_allreduce"),
+                              "halo_pull": M.get_option("halo_pull"),
                               "fuse_update": M.get_option("fuse_update"),
                               "niters": it,
                               "trace_equal_first": traces[v] == next(iter(traces.values()))}), flush=True)
