@@ -131,7 +131,6 @@ struct CgArgs {
     // update stores those rows write-through and drains them before its r.r
     // partial (0, 0: off)
     int rsend_lo, rsend_hi;
-    int su2;                      // direct kernel: two slices per unit block (k_spmv_a2s; units are slice pairs)
 };
 // Block timeline (dbg_timeline), per unit of the ring pair kernel: [0] block
 // index | HW_ID << 32, [1] entry, [2] iteration state read, [3] windows staged

@@ -1307,83 +1307,6 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 }
 
 // ---------------------------------------------------------------------------
-// The direct kernel over slice pairs (a.su2; option direct_spu 2, automatic
-// where the slices need between one and two rounds of resident blocks, e.g.
-// 100^3's 1954 against 256 CUs x 6 blocks): one 256-thread block runs slice
-// 2P, then slice 2P + 1, each exactly as k_spmv_a's width-kW loop does (the
-// same loads, products and order, the partial with block_sum's shape), and
-// hands both partials over like the pair kernel (two lanes, spu 2). The launch
-// is then one round of blocks: the 100^3 block timeline had the second round of
-// 418 slices running on a GPU whose unit blocks fell from 4.1 to 1.0 per CU
-// over the launch's second half. Same bits as k_spmv_a.
-// ---------------------------------------------------------------------------
-template <int kW, bool kNT, bool kFuse, int kPre, bool kFU>
-__global__ __launch_bounds__(kBlock) void k_spmv_a2s(CgArgs a, bool prologue)
-{
-    static_assert(kW > 0 && kPre > 0 && kPre <= kW, "uniform width, early loads");
-    const int P = unit_of(a);
-    const int s0 = P >= 0 ? 2 * P : a.nslices;
-    Rows vpre[kPre];
-    int offp[kW];
-    auto early = [&](int s) {
-        const double* __restrict__ vp0 = a.aval + (size_t)s * kW * kSliceRows + (size_t)threadIdx.x * kRpt;
-#pragma unroll
-        for (int j = 0; j < kPre; j++) vpre[j] = ld_m<kNT>(vp0 + (size_t)j * kSliceRows);
-#pragma unroll
-        for (int j = 0; j < kW; j++) offp[j] = a.aoff[(size_t)s * kAMax + j];
-    };
-    if (s0 < a.nslices) early(s0);
-    if constexpr (kFU) {
-        if (fused_update(a, prologue)) return;
-    }
-    if (side_flush<1, kW == 7 ? 8 : 4, kFU>(a, prologue)) return;
-    if (ghost_store<kFU>(a, prologue)) return;
-    IterState st;
-    if (!spmv_begin<kFuse, kFU, true>(a, prologue, st)) return;
-    if (s0 >= a.nslices) return;
-    const int nsl = min(2, a.nslices - s0);
-    double bs[2] = {0.0, 0.0};
-#pragma unroll 1
-    for (int h = 0; h < nsl; h++) {
-        const int s = s0 + h;
-        if (h > 0) early(s);
-        const int row = s * kSliceRows + threadIdx.x * kRpt;
-        const double* __restrict__ xr = cur_p(a, st.k) + row;
-        const double* __restrict__ rr_ = a.r + row;
-        const double* __restrict__ py = rr_;
-        if constexpr (kFuse) py = ((st.k == 1) ? a.r : cur_p(a, st.k - 1)) + row;
-        const double* __restrict__ vp = a.aval + (size_t)s * kW * kSliceRows + (size_t)threadIdx.x * kRpt;
-        double sum[kRpt] = {0.0, 0.0};
-#pragma unroll
-        for (int j = 0; j < kW; j++) {
-            const Rows v = j < kPre ? vpre[j] : ld_m<kNT>(vp + (size_t)j * kSliceRows);
-            const int oj = offp[j];
-            Rows xv;
-            if constexpr (kFuse) {
-                const Rows rv = ld_u(rr_ + oj);
-                const Rows yv = ld_u(py + oj);
-#pragma unroll
-                for (int i = 0; i < kRpt; i++) xv.v[i] = rv.v[i] + st.beta * yv.v[i];
-            } else {
-                xv = ld_u(xr + oj);
-            }
-#pragma unroll
-            for (int i = 0; i < kRpt; i++) sum[i] = sum[i] + v.v[i] * xv.v[i];
-        }
-        const double d = spmv_rows_out<kFuse, kFU>(a, st, prologue, row, sum);
-        if (prologue) continue;
-        if constexpr (kFU) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Ap landed before the partial
-        bs[h] = block_sum<kBlock>(d);
-        __syncthreads();  // block_sum's wave sums are read before the next slice rewrites them
-    }
-    if (prologue || threadIdx.x >= kWave) return;
-    const int lane = threadIdx.x;
-    const double b1 = __shfl(bs[1], 0, kWave);  // both partials are valid in thread 0
-    const double bsj = lane == 0 ? bs[0] : (lane == 1 ? b1 : 0.0);
-    complete_dot_lanes(a, spmv_units(a, 2), P, s0, nsl, bsj, kPAP, st.k);
-}
-
-// ---------------------------------------------------------------------------
 // SELL-512-A with x from LDS windows shared by slice pairs: block P owns
 // slices 2P and 2P + 1 with 512 threads (waves 0-3 slice 2P, 4-7 slice
 // 2P + 1, two rows per thread). The pair's windows (one per offset cluster:
@@ -2352,7 +2275,7 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         hipLaunchKernelGGL((k_spmv_a<7, true, true, 7, true, true, true>), sg, dim3(kBlock), 0, s, b, prologue);
         return;
     }
-    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 27 && !a.nt && a.apre != 0 && !a.su2) {
+    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 27 && !a.nt && a.apre != 0) {
         hipLaunchKernelGGL((k_spmv_a<27, false, true, 4, false, true, true>), sg, dim3(kBlock), 0, s, b, prologue);
         return;
     }
@@ -2412,19 +2335,7 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         break;
     }
     case kSpmvDirect:
-        if (a.su2 && a.a_width == 27 && a.apre != 0) {  // slice pairs per block (direct_spu 2)
-#define HPCCG_A2S(NT)                                                                                            \
-    do {                                                                                                         \
-        if (fu)                                                                                                  \
-            hipLaunchKernelGGL((k_spmv_a2s<27, NT, true, 4, true>), sg, dim3(kBlock), 0, s, b, prologue);        \
-        else if (fuse)                                                                                           \
-            hipLaunchKernelGGL((k_spmv_a2s<27, NT, true, 4, false>), sg, dim3(kBlock), 0, s, b, prologue);       \
-        else                                                                                                     \
-            hipLaunchKernelGGL((k_spmv_a2s<27, NT, false, 4, false>), sg, dim3(kBlock), 0, s, b, prologue);      \
-    } while (0)
-            if (a.nt) HPCCG_A2S(true); else HPCCG_A2S(false);
-#undef HPCCG_A2S
-        } else if (a.a_width == 27) {
+        if (a.a_width == 27) {
             if (a.apre == 0) {
                 if (a.nt) HPCCG_A(27, true, 0); else HPCCG_A(27, false, 0);
             } else {

@@ -236,7 +236,6 @@ struct hpccg_hip_matrix {
     int nt_store = -1;    // CG vector stores non-temporal (-1 auto: nt_store_effective)
     int a2_ring = kA2RingDefault;  // pair kernel: LDS-DMA value ring depth per wave (0: register loads; uniform widths 27 and 7)
     int tri = 1;          // direct kernel, width 7: x triple from adjacent lanes where the slice allows
-    int direct_spu = -1;  // direct kernel: slices per unit block, 1 or 2 (k_spmv_a2s); -1 auto (direct_su2)
     int fold = -1;        // -1 auto: 2 (p.Ap folded into the SpMV)
     int force_comm = 0;   // diagnostics: 1 scalars through the RCCL communicator even at one rank;
                           // 2 also the multi-rank iteration with a self send/recv as its halo
@@ -1249,24 +1248,6 @@ bool fuse_update_effective(const hpccg_hip_matrix* M)
            x_defer_effective(M) == 2;
 }
 
-// The direct kernel over slice pairs (k_spmv_a2s, width 27 with its early
-// loads): automatic where one block per slice takes between one and two
-// rounds of the GPU's resident blocks (6 per CU at its 77 VGPRs), so pairs
-// fit in one round -- 100^3's 1954 slices on 256 CUs -- and no partial second
-// round runs on a half-empty GPU. Not for unit subsets (the eager overlap).
-bool direct_su2(const hpccg_hip_matrix* M)
-{
-    if (M->kernel != kSpmvDirect || M->a_width != 27 || M->a_pre == 0 || M->direct_spu == 1) return false;
-    if (multi_of(M) && !rhalo_of(M)) return false;
-    if (M->direct_spu == 2) return true;
-    static const int resident = [] {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return 6 * cus;
-    }();
-    return M->nslices > resident && (M->nslices + 1) / 2 <= resident;
-}
-
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
 {
     CgArgs a;
@@ -1292,8 +1273,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.pready = M->d_partial + (M->npartial - kNumXcd * kReadyStride);
     a.rev = M->rev_update ? 1 : 0;
     a.nring = a.xdefer ? x_ring_effective(M) : (a.fuse_p ? 2 : 1);
-    a.su2 = direct_su2(M) ? 1 : 0;
-    const int units = (M->kernel == kSpmvPairs || a.su2) ? (M->nslices + 1) / 2 : M->nslices;
+    const int units = M->kernel == kSpmvPairs ? (M->nslices + 1) / 2 : M->nslices;
     a.s0 = 0;
     a.sn0 = units;
     a.s1 = a.sn1 = 0;
@@ -3267,9 +3247,6 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->spin_us = value;
     } else if (!std::strcmp(key, "peer_allreduce")) {
         M->peer_ar = value < 0 ? -1 : (value ? 1 : 0);
-    } else if (!std::strcmp(key, "direct_spu")) {  // -1 auto, 1 or 2 slices per unit block
-        if (value != -1 && value != 1 && value != 2) return set_err(HPCCG_HIP_EINVAL, "direct_spu must be -1, 1 or 2");
-        M->direct_spu = (int)value;
     } else if (!std::strcmp(key, "halo_pull")) {  // -1 auto, 0 off (the RCCL / peer-copy planes), 1 on where possible
         M->halo_pull = value < 0 ? -1 : (value ? 1 : 0);
     } else if (!std::strcmp(key, "rhalo_group")) {
@@ -3340,7 +3317,6 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "peer_allreduce")) *value = peer_ar_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "rhalo")) *value = rhalo_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "halo_pull")) *value = pull_of(M) ? 1 : 0;
-    else if (!std::strcmp(key, "direct_spu")) *value = direct_su2(M) ? 2 : 1;
     else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
     else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;
     else if (!std::strcmp(key, "stage16")) *value = M->stage16;

@@ -169,3 +169,35 @@ def test_three_rank_plan_interior_rank():
     import oracle
     ref = oracle.hpccg(oracle.generate(6, 5, 12), max_iter=40)
     assert check_trace(out[0][2], ref["trace"], RTRANS_RTOL_MULTI) >= 5
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+@pytest.mark.parametrize("use_7pt", [False, True])
+def test_pull_halo_contract(world, use_7pt):
+    """The halo pull (k_pull) reads rank r-1's last ghost_lo(r)
+    rows and rank r+1's first ghost_hi(r) rows of r; the update writes exactly
+    the rows the slab plan sends (send_hi(r-1), send_lo(r+1)) write-through.
+    For the z-slab plan those must coincide: every pulled row is a sent row,
+    and the pull moves what RCCL's send/recv would."""
+    hp = load_pkg()
+    nx, ny, nz = 7, 5, 4
+    n = nx * ny * nz
+    info = []
+    for r in range(world):
+        prob = hp.generate_matrix(nx, ny, nz, rank=r, size=world, use_7pt=use_7pt)
+        rp, cols, _ = prob.to_csr()
+        plan = hp.halo_plan(rp, cols, r * n, n * world)
+        info += [n, plan["ghost_lo"], plan["ghost_hi"], r * n]
+        prob.close()
+    info = np.array(info, dtype=np.int32)
+    sends = [hp.slab_plan(world, r, info) for r in range(world)]
+    for r in range(world):
+        glo, ghi = info[4 * r + 1], info[4 * r + 2]
+        if r > 0:
+            assert glo > 0 and glo == sends[r - 1][1]
+        else:
+            assert glo == 0
+        if r < world - 1:
+            assert ghi > 0 and ghi == sends[r + 1][0]
+        else:
+            assert ghi == 0
