@@ -131,6 +131,19 @@ struct CgArgs {
     // update stores those rows write-through and drains them before its r.r
     // partial (0, 0: off)
     int rsend_lo, rsend_hi;
+    // In-launch pull (pull_in; halo_pull 2): the iteration's last launch --
+    // the fused SpMV launch's ghost blocks, or trailing blocks of k_update --
+    // reads the neighbours' boundary rows of r_k into pl_dst once its own r.r
+    // completion (after the peer all-reduce) has published k + 1; pl_lo /
+    // pl_hi rows from pl_src_lo / pl_src_hi (an in-process group: the members'
+    // buffers; an RCCL job: IPC-mapped; the emulation: its own rows)
+    int pull_in;
+    int send;  // one past the last side-flush block (set per launch)
+    int pl_lo, pl_hi;
+    const double* pl_src_lo;
+    const double* pl_src_hi;
+    double* pl_dst_lo;
+    double* pl_dst_hi;
 };
 // Block timeline (dbg_timeline), per unit of the ring pair kernel: [0] block
 // index | HW_ID << 32, [1] entry, [2] iteration state read, [3] windows staged
@@ -164,6 +177,7 @@ enum DevError : int {
     kErrTopWait = 2,    // the top waiter: group sums missing
     kErrReadyWait = 3,  // a fused update block: the launch's p.Ap total missing
     kErrPeerWait = 4,   // peer all-reduce: another rank's contribution missing
+    kErrPullWait = 5,   // in-launch pull: the launch's r.r completion missing
 };
 constexpr long long kSpinTicksDefault = 100000000;  // 1 s
 

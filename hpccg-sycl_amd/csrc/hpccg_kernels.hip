@@ -462,21 +462,30 @@ __device__ __forceinline__ double top_sum_wave(Ld ld, int ng, int lane)
 // rank's mailbox (system-scope stores: the mailboxes of other GPUs are
 // IPC-mapped), then -- bounded -- until all pranks slots of its own mailbox
 // are full, and the sum in rank order from 0.0 (k_group_sum's order: bitwise
-// the in-process group's all-reduce). Its slots are emptied for iteration
-// k + 2, the next user of this parity; a rank writes them again only after it
-// has this rank's contributions to iteration k + 1, stored after the reset.
+// the in-process group's all-reduce), summed from the poll that found them
+// all full (no second round trip). Its slots are emptied for iteration k + 2,
+// the next user of this parity; a rank writes them again only after it has
+// this rank's contribution to iteration k + 1 of the same dot, which a later
+// launch stores (each dot's all-reduce runs once per launch), and a launch's
+// stores have landed when it ends: so no drain after the reset, except where
+// one kernel runs several rounds of one dot (drain: the self-test).
 // Returns NaN when the wait gave up (the solve is void then).
-__device__ __forceinline__ double peer_allreduce(const CgArgs& a, double s, int which, int k)
+__device__ __forceinline__ double peer_allreduce(const CgArgs& a, double s, int which, int k, bool drain = false)
 {
     const int base = (which * 2 + (k & 1)) * (kMboxSlots / 4);
     for (int q = 0; q < a.pranks; q++)
         __hip_atomic_store(a.peers[q] + base + a.prank, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     double* const mb = a.mbox + base;
     unsigned t0 = 0, polls = 0;
+    double tot;
     for (;;) {
         bool full = true;
-        for (int q = 0; q < a.pranks; q++)
-            full = full && slot_full(__hip_atomic_load(mb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        tot = 0.0;
+        for (int q = 0; q < a.pranks; q++) {
+            const double v = __hip_atomic_load(mb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            full = full && slot_full(v);
+            tot += v;
+        }
         if (full) break;
         if ((++polls & 15) == 0 && wait_expired(a, t0)) {
             abort_solve(a, kErrPeerWait, which * 2 + (k & 1), k, which);
@@ -484,11 +493,9 @@ __device__ __forceinline__ double peer_allreduce(const CgArgs& a, double s, int 
         }
         __builtin_amdgcn_s_sleep(1);
     }
-    double tot = 0.0;
-    for (int q = 0; q < a.pranks; q++) tot += __hip_atomic_load(mb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     for (int q = 0; q < a.pranks; q++)
         __hip_atomic_store(mb + q, slot_empty(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return tot;
 }
 
@@ -508,7 +515,8 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
     }
     // the r.r iteration k + 1 reads, by its parity (fused update: kRRPar)
     if (which == kRR && a.fupd) a.g[kRRPar + ((k + 1) & 1)] = s;
-    if (which == kRR) a.kst[a.fupd && ((k + 1) & 1) ? 2 : 0] = k + 1;
+    // (write-through: an in-launch pull's blocks on other XCDs wait for it)
+    if (which == kRR) st_sc1_i(a.kst + (a.fupd && ((k + 1) & 1) ? 2 : 0), k + 1);
     if (a.fupd) {  // one copy per XCD group of update blocks, 128 B apart (no single hot line)
         for (int j = 0; j < kNumXcd; j++)
             st_sc1(a.pready + kReadyStride * j, which == kPAP ? s : slot_empty());  // p.Ap: the update blocks
@@ -909,7 +917,7 @@ __host__ __device__ constexpr int side_blocks(int nslices, int nring, int spu)
 template <int kSpu, int kB, bool kFU = false>
 __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
 {
-    if ((int)blockIdx.x < a.sgrid || (int)blockIdx.x >= a.gbase) return false;  // (gbase <= ubase)
+    if ((int)blockIdx.x < a.sgrid || (int)blockIdx.x >= a.send) return false;
     if (prologue) return true;
     const int k = iter_k<kFU>(a);
     if (k < 2 || !cg_run(a, k, false)) return true;
@@ -943,7 +951,7 @@ __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
 
 // ---------------------------------------------------------------------------
 // r-halo (a.rhalo): the ghost blocks of the SpMV launch (index >= a.gbase,
-// after the unit and side blocks) store p_k = r + beta p_{k-1} at the ghost
+// the launch's last blocks) store p_k = r + beta p_{k-1} at the ghost
 // rows, k_p_update's expression on the received r planes and the p_{k-1}
 // ghosts the previous launch stored (k == 1: p_1 = r + 0 r). The neighbour
 // forms the same rows of its own p_k with the same expression and the same
@@ -952,6 +960,55 @@ __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
 // ---------------------------------------------------------------------------
 // kFU: the launch's instantiation (a.fupd is set only with the direct kernel;
 // a run-time choice here cost the 7-pt fused instantiation 26 VGPRs)
+//
+// In-launch pull (a.pull_in): once the iteration's r.r completion -- in this
+// launch (fused update) or in k_update -- has published k + 1 (after the peer
+// all-reduce: every rank's r_k is final, its boundary rows stored
+// write-through and drained before its r.r partial, pulled_slice), the
+// neighbours' boundary rows of r_k are read with system-scope loads into this
+// rank's ghost rows of r, which the next launch reads (k_pull's work, without
+// k_pull's launch). Nothing in this launch reads those ghost rows afterwards:
+// the unit blocks read r_{k-1}'s ghosts for p_k before their p.Ap partials,
+// which the r.r completion waits behind, and ghost_store's thread that reads
+// a ghost row is the thread that rewrites it (same index sequence, program
+// order). The neighbour overwrites its rows only after this rank's next p.Ap
+// contribution, which follows this launch. bl / nbl: this block among the
+// pull blocks.
+__device__ __forceinline__ void pull_rows(const CgArgs& a, int k, int bl, int nbl)
+{
+    if (k + 1 >= a.max_iter) return;  // no SpMV reads them
+    const int* const slot = a.kst + ((a.fupd && ((k + 1) & 1)) ? 2 : 0);
+    unsigned t0 = 0, polls = 0;
+    int v;
+    while ((v = ld_sc1_i(slot)) < k + 1) {
+        if ((++polls & 15) == 0 && wait_expired(a, t0)) {
+            if ((threadIdx.x & (kWave - 1)) == 0) abort_solve(a, kErrPullWait, bl, k, kRR);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (v != k + 1) return;  // the solve was aborted
+    if (bl == 0 && threadIdx.x == 0) stamp(a, k + 1, kStampHalo);
+    constexpr int kU = 4;  // loads in flight per thread
+    const int tot = a.pl_lo + a.pl_hi;
+    const int nth = nbl * (int)blockDim.x;
+    for (int i0 = bl * (int)blockDim.x + (int)threadIdx.x; i0 < tot; i0 += kU * nth) {
+        double w[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int i = i0 + u * nth;
+            w[u] = i < tot ? __hip_atomic_load(i < a.pl_lo ? a.pl_src_lo + i : a.pl_src_hi + (i - a.pl_lo),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                           : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int i = i0 + u * nth;
+            if (i < tot) (i < a.pl_lo ? a.pl_dst_lo[i] : a.pl_dst_hi[i - a.pl_lo]) = w[u];
+        }
+    }
+}
+
 template <bool kFU>
 __device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
 {
@@ -966,18 +1023,20 @@ __device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
     const double* __restrict__ pold = (k == 1) ? a.r : cur_p(a, k - 1);
     double* __restrict__ pk = cur_p(a, k);
     const int nlo = a.ghost_lo, tot = a.ghost_lo + a.ghost_hi;
-    const int stride = (int)(gridDim.x - a.gbase) * (int)blockDim.x;
-    for (int i = ((int)blockIdx.x - a.gbase) * (int)blockDim.x + (int)threadIdx.x; i < tot; i += stride) {
+    const int bl = (int)blockIdx.x - a.gbase, nbl = (int)gridDim.x - a.gbase;  // (the last blocks)
+    for (int i = bl * (int)blockDim.x + (int)threadIdx.x; i < tot; i += nbl * (int)blockDim.x) {
         const int row = i < nlo ? i - nlo : a.n + (i - nlo);
         pk[row] = a.r[row] + beta * pold[row];
     }
+    if constexpr (kFU)
+        if (a.pull_in) pull_rows(a, k, bl, nbl);
     return true;
 }
 
 // ---------------------------------------------------------------------------
 // Fused update (a.fupd; one rank, direct kernel): the SpMV launch of iteration
-// k ends with a.grid update blocks (index >= a.ubase, dispatched after every
-// unit and side block) that do k_update's work -- r = r - alpha Ap and the r.r
+// k ends with a.grid update blocks (index a.ubase .. a.gbase - 1, dispatched
+// after every unit and side block; ghost blocks follow them) that do k_update's work -- r = r - alpha Ap and the r.r
 // partial (HPCCG.cpp:382-384, 367), the same expressions in the same order --
 // once the launch's p.Ap total is in its self-validating slots (a.pready:
 // kNumXcd copies 128 B apart, block b polls copy b mod kNumXcd, so no single
@@ -990,7 +1049,7 @@ __device__ __forceinline__ bool ghost_store(const CgArgs& a, bool prologue)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue, unsigned long long* tw = nullptr)
 {
-    if ((int)blockIdx.x < a.ubase) return false;
+    if ((int)blockIdx.x < a.ubase || (int)blockIdx.x >= a.gbase) return false;
     if (prologue) return true;
     const int bl = (int)blockIdx.x - a.ubase;  // a.ubase is a multiple of kNumXcd
     const int spu = a.fu2 ? 2 : 1;
@@ -1805,6 +1864,15 @@ __device__ __forceinline__ void x_accumulate(const CgArgs& a, int row, int j0, i
 template <bool kPrologue>
 __global__ __launch_bounds__(kBlock) void k_update(CgArgs a)
 {
+    if ((int)blockIdx.x >= a.grid) {  // in-launch pull blocks (a.pull_in), after the update's
+        int k = 0;
+        if constexpr (!kPrologue) {
+            if (!a.kst[5]) return;  // publish_iter's {k, run}
+            k = a.kst[4];
+        }
+        pull_rows(a, k, (int)blockIdx.x - a.grid, (int)gridDim.x - a.grid);
+        return;
+    }
     int k = 0;
     const int s = a.rev ? xcd_slice_rev(a.grid) : xcd_slice(a.grid);
     const int row = s * kSliceRows + threadIdx.x * kRpt;
@@ -1935,7 +2003,7 @@ __global__ void k_peer_selftest(CgArgs a, int rounds, double* out)
     if (threadIdx.x != 0) return;
     for (int k = 0; k < rounds; k++)
         for (int which = 0; which < 2; which++)
-            out[2 * k + which] = peer_allreduce(a, (double)(a.prank + 1) + 0.5 * k + 0.25 * which, which, k);
+            out[2 * k + which] = peer_allreduce(a, (double)(a.prank + 1) + 0.5 * k + 0.25 * which, which, k, true);
 }
 
 // Every solve starts here, stream-ordered before its prologue (HPCCG.cpp:
@@ -2258,17 +2326,21 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     // fused update: a.grid update blocks after the side blocks, from a block
     // index that is a multiple of kNumXcd (their XCD-aware slice order)
     const bool fu = !prologue && a.fupd && kernel == kSpmvDirect && fuse;
-    // r-halo: ghost blocks after the side blocks store p_k at the ghost rows
-    // (about four rows per thread)
+    // r-halo: ghost blocks, the launch's last, store p_k at the ghost rows
     const int gtot = a.ghost_lo + a.ghost_hi;
     const int gthreads = kernel == kSpmvPairs ? 2 * kBlock : kBlock;
-    const int nghost = (fuse && a.rhalo && gtot > 0) ? (gtot + 4 * gthreads - 1) / (4 * gthreads) : 0;
+    // (about four rows per thread); the fused launch's also pull r_k (a.pull_in)
+    const int ptot = (fu && a.pull_in) ? a.pl_lo + a.pl_hi : 0;
+    const int gmax = gtot > ptot ? gtot : ptot;
+    const int nghost = (fuse && a.rhalo && gmax > 0) ? (gmax + 4 * gthreads - 1) / (4 * gthreads) : 0;
     CgArgs b = a;
-    b.ubase = fu ? (a.sgrid + nside + nghost + kNumXcd - 1) / kNumXcd * kNumXcd : 0;
-    b.gbase = nghost ? a.sgrid + nside : (fu ? b.ubase : INT_MAX);
+    b.send = a.sgrid + nside;
     // update units: one slice per block, or two (a.fu2: four rows per thread)
     const int ugrid = a.fu2 ? (((a.nslices + 1) / 2 + kNumXcd - 1) / kNumXcd * kNumXcd) : a.grid;
-    const dim3 sg(fu ? b.ubase + ugrid : a.sgrid + nside + nghost);
+    // fused update: [units | side | pad to kNumXcd | update | ghost]; else [units | side | ghost]
+    b.ubase = fu ? (b.send + kNumXcd - 1) / kNumXcd * kNumXcd : 0;
+    b.gbase = nghost ? (fu ? b.ubase + ugrid : b.send) : INT_MAX;
+    const dim3 sg((fu ? b.ubase + ugrid : b.send) + nghost);
     // diagnostics: the block-timeline instantiations of the two fused-update defaults
     if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 7 && a.nt && a.atri &&
         (a.apre < 0 || a.apre == 7)) {
@@ -2387,10 +2459,13 @@ void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s
 
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)
 {
+    // in-launch pull: trailing blocks, about four rows per thread
+    const int ptot = a.pull_in ? a.pl_lo + a.pl_hi : 0;
+    const dim3 grid(a.grid + (ptot + 4 * kBlock - 1) / (4 * kBlock));
     if (prologue)
-        hipLaunchKernelGGL((k_update<true>), dim3(a.grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_update<true>), grid, dim3(kBlock), 0, s, a);
     else
-        hipLaunchKernelGGL((k_update<false>), dim3(a.grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((k_update<false>), grid, dim3(kBlock), 0, s, a);
 }
 
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s)

@@ -281,7 +281,7 @@ struct hpccg_hip_matrix {
     // peer-memory all-reduce of the CG scalars (option peer_allreduce)
     int peer_ar = -1;                  // option peer_allreduce: -1 auto (peer_ar_of), 0 off, 1 on
     int peer_auto_ok = 0;              // auto: the creation-time self-test passed on every rank
-    // r-halo by pull (option halo_pull: -1 auto, 0 the RCCL / peer-copy planes, 1 on)
+    // r-halo by pull (option halo_pull: -1 auto, 0 the RCCL / peer-copy planes, 1 k_pull, 2 in-launch)
     int halo_pull = -1;
     int pull_auto_ok = 0;              // RCCL job: the creation-time pull test passed on every rank
     double* d_pull_lo = nullptr;       // rank - 1's r (its local row 0), mapped here (RCCL job)
@@ -1066,6 +1066,17 @@ bool pull_of(const hpccg_hip_matrix* M)
     return M->pull_auto_ok != 0;  // (an RCCL job: its neighbours' r mapped and tested at creation)
 }
 
+// In-launch pull (halo_pull 2, and auto): no k_pull launch -- the
+// iteration's last launch pulls r_k once its own r.r completion is in, which
+// needs the global sum inside the kernel (the peer all-reduce) and r.r folded
+// into its producer (no k_finalize after it). Emulated (force_comm 2, one
+// GPU), per iteration against k_pull: 100^3 +3.1 vs +5.0-5.6 us, 200^3 +5.2
+// vs +6.8-7.3, 7-pt 256^3 +3.9-4.0 vs +6.0-6.5 (profiles/r04_inlaunch).
+bool pull_in_of(const hpccg_hip_matrix* M, const CgArgs& a)
+{
+    return pull_of(M) && M->halo_pull != 1 && a.peer_ar && fold_of(a, kRR);
+}
+
 // Both dots folded into their producing kernels (slot completion, no
 // k_finalize launch): same-process A/B against p.Ap folded + r.r through
 // k_finalize, 100^3 19249 vs 17814 CG it/s, 200^3 2619 vs 2543, 7-pt 256^3
@@ -1243,7 +1254,9 @@ bool fuse_update_effective(const hpccg_hip_matrix* M)
     const bool want = M->fuse_update != 0;
     // several ranks: only with the in-kernel peer all-reduce (the update needs
     // the global p.Ap inside the launch), and not in an in-process group
-    const bool ranks_ok = (M->nranks == 1 && !M->force_comm) || (peer_ar_of(M) && !M->in_group);
+    // (2: also an in-process group -- tests only, members small enough to be
+    // resident side by side: the update blocks wait for the other member's p.Ap)
+    const bool ranks_ok = (M->nranks == 1 && !M->force_comm) || (peer_ar_of(M) && (!M->in_group || M->fuse_update == 2));
     return want && ranks_ok && M->kernel == kSpmvDirect && fuse_p_effective(M) && fold_effective(M) == 1 &&
            x_defer_effective(M) == 2;
 }
@@ -1307,6 +1320,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     if (pull_of(M)) {  // the rows the neighbours pull go write-through (pulled_slice)
         a.rsend_lo = emulated_multi(M) ? (int)emul_rows(M) : M->send_lo;
         a.rsend_hi = emulated_multi(M) ? (int)emul_rows(M) : M->send_hi;
+        a.pull_in = pull_in_of(M, a) ? 1 : 0;  // (pl_*: pull_plan, once the ranks' r are known)
     }
     a.slice_base = M->d_slice_base;
     a.cols = M->d_cols;
@@ -1681,25 +1695,27 @@ bool overlap_ok(const Ranks& R)
     return true;
 }
 
-// The r-halo by pull (pull_of): rank r's ghost planes of r from its
-// neighbours' boundary rows, on its stream, right before its SpMV launch.
-int enqueue_pull(const Ranks& R, int r, const CgArgs& a)
+// The r-halo by pull (pull_of): where rank r's ghost planes of r come from,
+// into av[r].pl_* (k_pull's operands, or the in-launch pull's).
+int pull_plan(hpccg_hip_matrix* const* Ms, CgArgs* av, int P, int r)
 {
-    hpccg_hip_matrix* M = R.M[r];
+    hpccg_hip_matrix* M = Ms[r];
+    CgArgs& a = av[r];
     const double *lo_src = nullptr, *hi_src = nullptr;
     double *lo_dst = a.r - M->ghost_lo, *hi_dst = a.r + M->nrow;
     int lo = 0, hi = 0;
-    if (R.P > 1) {  // an in-process group: the members' own buffers
+    if (P > 1) {  // an in-process group: the members' own buffers
         if (r > 0 && M->ghost_lo) {
             lo = M->ghost_lo;
-            lo_src = R.a[r - 1].r + R.M[r - 1]->nrow - lo;
+            lo_src = av[r - 1].r + Ms[r - 1]->nrow - lo;
         }
-        if (r < R.P - 1 && M->ghost_hi) {
+        if (r < P - 1 && M->ghost_hi) {
             hi = M->ghost_hi;
-            hi_src = R.a[r + 1].r;
+            hi_src = av[r + 1].r;
         }
     } else if (emulated_multi(M)) {  // an interior rank's two planes: its own rows into scratch
-        lo = hi = (int)emul_rows(M);
+        // (halo_pull 3, diagnostics: none -- the iteration's cost without its halo)
+        lo = hi = M->halo_pull == 3 ? 0 : (int)emul_rows(M);
         lo_src = a.r;
         hi_src = a.r + M->nrow - hi;
         lo_dst = M->d_emul;
@@ -1715,8 +1731,19 @@ int enqueue_pull(const Ranks& R, int r, const CgArgs& a)
         }
         if ((lo && !lo_src) || (hi && !hi_src)) return set_err(HPCCG_HIP_EINVAL, "halo_pull: a neighbour's r is not mapped");
     }
-    launch_pull(a, lo_src, lo_dst, lo, hi_src, hi_dst, hi, M->stream);
+    a.pl_lo = lo;
+    a.pl_hi = hi;
+    a.pl_src_lo = lo_src;
+    a.pl_src_hi = hi_src;
+    a.pl_dst_lo = lo_dst;
+    a.pl_dst_hi = hi_dst;
     return 0;
+}
+
+// k_pull: rank r's ghost planes right before its SpMV launch, on its stream.
+void enqueue_pull(const Ranks& R, int r, const CgArgs& a)
+{
+    launch_pull(a, a.pl_src_lo, a.pl_dst_lo, a.pl_lo, a.pl_src_hi, a.pl_dst_hi, a.pl_hi, R.M[r]->stream);
 }
 
 int enqueue_spmv_overlapped(const Ranks& R, int slot, int k_host)
@@ -1800,7 +1827,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
             CgArgs a = R.a[r];
             a.kpar = k_host & 1;  // fused update: the parity slot of k (iter_k)
             TRY(use_device(R, r));
-            if (pull) TRY(enqueue_pull(R, r, a));  // r's ghost planes for this SpMV
+            if (pull && !a.pull_in) enqueue_pull(R, r, a);  // r's ghost planes for this SpMV
             if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
             launch_cg_spmv(a, M->kernel, false, M->stream);
             if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
@@ -2309,8 +2336,9 @@ int check_device_error(hpccg_hip_matrix* const* Ms, int P, const int* err0)
 {
     static const char* what[] = {"", "slice partials of a dot group", "group sums of a dot",
                                  "the p.Ap total (fused update)",
-                                 "another rank's contribution (peer all-reduce)"};
-    static const char* where[] = {"", "group", "group", "ready slot", "slot (dot * 2 + parity)"};
+                                 "another rank's contribution (peer all-reduce)",
+                                 "the launch's r.r completion (in-launch pull)"};
+    static const char* where[] = {"", "group", "group", "ready slot", "slot (dot * 2 + parity)", "pull block"};
     int bad_rank = -1, e[kErrWords];
     for (int r = 0; r < P && bad_rank < 0; r++) {
         if (r == 0) {
@@ -2331,8 +2359,8 @@ int check_device_error(hpccg_hip_matrix* const* Ms, int P, const int* err0)
     return set_err(HPCCG_HIP_EHIP,
                    "rank %d: device wait timed out after %.0f us waiting for %s (block %d, %s %d, iteration %d, "
                    "dot %s); solve abandoned, dot slots reset",
-                   rank, (double)Ms[bad_rank]->spin_us, e[0] > 0 && e[0] <= kErrPeerWait ? what[e[0]] : "?", e[1],
-                   e[0] > 0 && e[0] <= kErrPeerWait ? where[e[0]] : "slot", e[2], e[3], e[4] == kPAP ? "p.Ap" : "r.r");
+                   rank, (double)Ms[bad_rank]->spin_us, e[0] > 0 && e[0] <= kErrPullWait ? what[e[0]] : "?", e[1],
+                   e[0] > 0 && e[0] <= kErrPullWait ? where[e[0]] : "slot", e[2], e[3], e[4] == kPAP ? "p.Ap" : "r.r");
 }
 
 // Solve on the ranks Ms[0..P) (P > 1: an in-process group; P == 1: this
@@ -2397,6 +2425,8 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
                 if (q != r) HIP_TRY(hipStreamWaitEvent(Ms[r]->stream, gev[q], 0));
         }
     }
+    if (multi_of(M) && pull_of(M))
+        for (int r = 0; r < P; r++) TRY(pull_plan(Ms, av.data(), P, r));
     const Ranks R{Ms, av.data(), P, gev.data()};
     if (events) TRY(ensure_events(M, iters + 1));
     TRY(enqueue_prologue(R, events));
@@ -3212,7 +3242,7 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         if (value != 1 && value != 2) return set_err(HPCCG_HIP_EINVAL, "fused_update_slices must be 1 or 2");
         M->fused_update_slices = (int)value;
     } else if (!std::strcmp(key, "fuse_update")) {
-        M->fuse_update = value < 0 ? -1 : (value ? 1 : 0);
+        M->fuse_update = value < 0 ? -1 : (value > 2 ? 2 : (int)value);
     } else if (!std::strcmp(key, "rev_update")) {
         M->rev_update = (int)value;
     } else if (!std::strcmp(key, "overlap")) {
@@ -3247,8 +3277,10 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->spin_us = value;
     } else if (!std::strcmp(key, "peer_allreduce")) {
         M->peer_ar = value < 0 ? -1 : (value ? 1 : 0);
-    } else if (!std::strcmp(key, "halo_pull")) {  // -1 auto, 0 off (the RCCL / peer-copy planes), 1 on where possible
-        M->halo_pull = value < 0 ? -1 : (value ? 1 : 0);
+    } else if (!std::strcmp(key, "halo_pull")) {
+        // -1 auto, 0 off (the RCCL / peer-copy planes), 1 k_pull where possible, 2 in-launch where the
+        // peer all-reduce runs (else 1); 3 (diagnostics, the 1-rank emulation): in-launch with no rows
+        M->halo_pull = value < 0 ? -1 : (value > 3 ? 3 : (int)value);
     } else if (!std::strcmp(key, "rhalo_group")) {
         // changes captured RCCL work that no kernel argument records: rebuild the graph
         if (M->rhalo_group != (value ? 1 : 0) && M->graph_exec) {
@@ -3316,7 +3348,12 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "rhalo_group")) *value = M->rhalo_group;
     else if (!std::strcmp(key, "peer_allreduce")) *value = peer_ar_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "rhalo")) *value = rhalo_of(M) ? 1 : 0;
-    else if (!std::strcmp(key, "halo_pull")) *value = pull_of(M) ? 1 : 0;
+    else if (!std::strcmp(key, "halo_pull")) {
+        CgArgs a{};
+        a.peer_ar = peer_ar_of(M) ? 1 : 0;
+        a.fold = fold_effective(M);
+        *value = pull_of(M) ? (pull_in_of(M, a) ? 2 : 1) : 0;
+    }
     else if (!std::strcmp(key, "a_pre")) *value = M->a_pre;
     else if (!std::strcmp(key, "lds_ep")) *value = M->lds_ep;
     else if (!std::strcmp(key, "stage16")) *value = M->stage16;

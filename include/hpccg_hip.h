@@ -171,7 +171,17 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   after the update into r's ghost planes and the SpMV forms
  *                   p_k at ghost rows itself. 1 (default): the r.r all-reduce
  *                   and the planes in one RCCL group; 0: the all-reduce first
- *   "event_timing"  1 = eager launches with hipEvents around every SpMV and
+ *   "peer_allreduce" -1 auto (default: an RCCL job whose creation-time
+ *                   self-test passed on every rank, and the force_comm 2
+ *                   emulation), 0 RCCL, 1 on: the two CG scalars summed inside
+ *                   the kernels through IPC-mapped mailboxes
+ *   "halo_pull"     r-halo by pull: -1 auto (default), 0 off (the RCCL plane
+ *                   group / peer copies), 1 k_pull before each SpMV launch,
+ *                   2 in-launch: the iteration's last launch pulls once its
+ *                   r.r completion is in (needs the peer all-reduce; auto picks
+ *                   it there, else 1); 3 diagnostics (force_comm 2 only):
+ *                   in-launch with no rows
+ *   "event_timing" 1 = eager launches with hipEvents around every SpMV and
  *                   update (hpccg_hip_kernel_times)
  *   "fuse_p"        -1 auto / 0 off: p = r + beta p formed inside the SpMV
  *                   (pair and direct kernels; on several ranks with the z-slab
@@ -181,7 +191,8 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   (k_finalize), 1 both (auto), 2 p.Ap only, 3 r.r only
  *   "fuse_update"   -1 auto (on) / 0 / 1: one rank, direct kernel: the update
  *                   runs as trailing blocks of the SpMV launch (one launch per
- *                   iteration; same bits)
+ *                   iteration; same bits); 2: also in an in-process group with
+ *                   the peer all-reduce (tests: small members only)
  *   "fused_update_slices"  1 or 2 (default): slices per fused update block
  *   "x_defer"       x += alpha p deferred over the p ring: 1 = every x_ring-th
  *                   update applies it to all rows; 2 (default) = trailing blocks

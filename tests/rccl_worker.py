@@ -52,6 +52,16 @@ def main():
     _, it2, nr2, _ = hp.HPCCG(M, b, x, max_iter=500, device=True)
     assert M.get_option("peer_allreduce") == 1 and M.get_option("fuse_update") == (1 if M.get_option("spmv_kernel") == 1 else 0)
     assert (it2, nr2, M.last_trace().tobytes(), x.cpu().numpy().tobytes()) == got
+    # the default pulls in-launch (halo_pull 2: the neighbours' r read by the
+    # fused launch's ghost blocks, or the update's trailing blocks, after r.r);
+    # k_pull before the SpMV launch (halo_pull 1) gives the same bits
+    pull_auto = M.get_option("halo_pull")
+    assert pull_auto in (0, 2)
+    M.set_option("halo_pull", 1)
+    x.zero_()
+    _, it3, nr3, _ = hp.HPCCG(M, b, x, max_iter=500, device=True)
+    assert M.get_option("halo_pull") == (1 if pull_auto else 0)
+    assert (it3, nr3, M.last_trace().tobytes(), x.cpu().numpy().tobytes()) == got
     print(f"RCCL-WORKER-OK rank {rank} graph_used={M.get_option('graph_used')}", flush=True)
     M.close()
     hp.comm_destroy()
