@@ -7,7 +7,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/mrev
-V="0:0:1,1:0:1,2:0:1:-1:1:0:0,2:0:1:-1:1:-1:0,2:0:1:-1:1:0:-1,2:0:1:-1:1:-1:-1,0:0:1"
+V="0:0:1,1:0:1,2:0:1:-1:1:0:0,2:0:1:-1:1:0:-1,2:0:1:-1:1:-1:1,2:0:1:-1:1:-1:-1,2:0:1:-1:1:-1:3,0:0:1"
 for cfg in "--n 100" "--n 200" "--n 256 --7pt"; do
   tag=$(echo "$cfg" | tr -d ' -' )
   timeout -k 10 300 python tools/comm_bench.py $cfg --variants $V > gpurun_out/mrev/comm_$tag.log 2>&1 \
