@@ -138,6 +138,12 @@ struct CgArgs {
     // pl_hi rows from pl_src_lo / pl_src_hi (an in-process group: the members'
     // buffers; an RCCL job: IPC-mapped; the emulation: its own rows)
     int pull_in;
+    // Group fold (an in-process group run in member order, both dots folded):
+    // the last member's finishing lane sums the members' local totals in rank
+    // order (k_group_sum's sum) and stores the total into every member's g:
+    // gtab[0 .. gn) the members' loc, gtab[gn .. 2 gn) their g; gn = 0 else
+    int gn;
+    double* const* gtab;
     int send;  // one past the last side-flush block (set per launch)
     int pl_lo, pl_hi;
     const double* pl_src_lo;

@@ -271,6 +271,10 @@ struct hpccg_hip_matrix {
     unsigned int* d_tickets = nullptr;
     int ntickets = 0;
     double* d_scal = nullptr;  // g[2], loc[2], spare
+    double** d_gtab = nullptr;  // group fold (last member): the members' loc, then their g
+    std::vector<double*> h_gtab;
+    int group_fold = -1;        // option group_fold: -1 auto (on where it applies), 0 off
+    int gfold_used = 0;         // the last group solve summed its dots in the last member's kernels
     int* d_kst = nullptr;      // [0, kErrBase) iteration state, then the device error record (kErrWords)
     long long spin_us = kSpinTicksDefault / 100;  // bound of every in-kernel wait (option spin_budget_us)
     int dbg_withhold = 0;      // debug: slice + 1 whose p.Ap partial is withheld (guard test)
@@ -451,6 +455,7 @@ int free_matrix(hpccg_hip_matrix* M)
         (void)hipMemAddressFree(v.res, v.res_bytes);
     }
     if (M->d_mbox) (void)hipFree(M->d_mbox);
+    if (M->d_gtab) (void)hipFree(M->d_gtab);
     if (M->d_peers) (void)hipFree(M->d_peers);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
     if (M->ev_flush) (void)hipEventDestroy(M->ev_flush);
@@ -1534,8 +1539,33 @@ int group_halo_gather(const Ranks& R, int k_host, bool prologue)
 
 // In-process all-reduce of loc[which]: one lane on rank 0's stream adds the
 // ranks' values in rank order and writes g[which] of every rank.
+// Group fold (CgArgs::gn): the last member's kernel sums the dot; the
+// others' streams only wait for it. group_gather_join runs before that
+// member's launch: its stream waits for every other member's.
+bool gfold_of(const Ranks& R) { return R.P > 1 && R.a[R.P - 1].gn > 0; }
+
+int group_gather_join(const Ranks& R)
+{
+    for (int r = 0; r < R.P - 1; r++) {
+        TRY(use_device(R, r));
+        HIP_TRY(hipEventRecord(R.ev[r], R.M[r]->stream));
+    }
+    TRY(use_device(R, R.P - 1));
+    for (int r = 0; r < R.P - 1; r++) HIP_TRY(hipStreamWaitEvent(R.M[R.P - 1]->stream, R.ev[r], 0));
+    return 0;
+}
+
 int group_allreduce(const Ranks& R, int which)
 {
+    if (gfold_of(R)) {  // summed by the last member's launch: its end releases the others
+        TRY(use_device(R, R.P - 1));
+        HIP_TRY(hipEventRecord(R.ev[R.P], R.M[R.P - 1]->stream));
+        for (int r = 0; r < R.P - 1; r++) {
+            TRY(use_device(R, r));
+            HIP_TRY(hipStreamWaitEvent(R.M[r]->stream, R.ev[R.P], 0));
+        }
+        return 0;
+    }
     GroupSum gs;
     std::memset(&gs, 0, sizeof gs);
     gs.nranks = R.P;
@@ -1827,6 +1857,8 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
             CgArgs a = R.a[r];
             a.kpar = k_host & 1;  // fused update: the parity slot of k (iter_k)
             TRY(use_device(R, r));
+            if (gfold_of(R) && r == R.P - 1) TRY(group_gather_join(R));  // (use_device(R, r) after it)
+            TRY(use_device(R, r));
             if (pull && !a.pull_in) enqueue_pull(R, r, a);  // r's ghost planes for this SpMV
             if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
             launch_cg_spmv(a, M->kernel, false, M->stream);
@@ -1847,6 +1879,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
     for (int r = 0; r < R.P; r++) {
         hpccg_hip_matrix* M = R.M[r];
         const CgArgs& a = R.a[r];
+        if (gfold_of(R) && r == R.P - 1) TRY(group_gather_join(R));
         TRY(use_device(R, r));
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], M->stream));
         launch_cg_update(a, false, M->stream);
@@ -1877,6 +1910,10 @@ int enqueue_prologue(const Ranks& R, bool events)
         if (events) HIP_TRY(hipEventRecord(M->ev[0], s));
         launch_cg_spmv(a, M->kernel, true, s);  // Ap = A p
         if (events) HIP_TRY(hipEventRecord(M->ev[1], s));
+        if (gfold_of(R) && r == R.P - 1) {
+            TRY(group_gather_join(R));
+            TRY(use_device(R, r));
+        }
         if (events) HIP_TRY(hipEventRecord(M->ev[2], s));
         launch_cg_update(a, true, s);  // r = b - Ap (+ r.r partials)
         if (events) HIP_TRY(hipEventRecord(M->ev[3], s));
@@ -2427,6 +2464,24 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     }
     if (multi_of(M) && pull_of(M))
         for (int r = 0; r < P; r++) TRY(pull_plan(Ms, av.data(), P, r));
+    // group fold: RCCL-style group sums (no peer all-reduce), both dots folded,
+    // no overlapped halo (its SpMV runs as two launches)
+    if (P > 1 && Ms[0]->group_fold != 0 && av[0].allreduce && fold_of(av[0], kPAP) && fold_of(av[0], kRR) &&
+        !Ms[0]->overlap) {
+        hpccg_hip_matrix* L = Ms[P - 1];
+        HIP_TRY(hipSetDevice(L->device));
+        if (!L->d_gtab) TRY(dev_alloc(L, &L->d_gtab, 2 * kMaxGroupRanks));
+        L->h_gtab.assign(2 * P, nullptr);
+        for (int r = 0; r < P; r++) {
+            L->h_gtab[r] = av[r].loc;
+            L->h_gtab[P + r] = av[r].g;
+        }
+        HIP_TRY(hipMemcpyAsync(L->d_gtab, L->h_gtab.data(), sizeof(double*) * 2 * P, hipMemcpyHostToDevice, L->stream));
+        HIP_TRY(hipStreamSynchronize(L->stream));  // (pageable source: done before it can change)
+        av[P - 1].gn = P;
+        av[P - 1].gtab = L->d_gtab;
+    }
+    for (int r = 0; r < P; r++) Ms[r]->gfold_used = av[P - 1].gn > 0 ? 1 : 0;
     const Ranks R{Ms, av.data(), P, gev.data()};
     if (events) TRY(ensure_events(M, iters + 1));
     TRY(enqueue_prologue(R, events));
@@ -3277,6 +3332,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->spin_us = value;
     } else if (!std::strcmp(key, "peer_allreduce")) {
         M->peer_ar = value < 0 ? -1 : (value ? 1 : 0);
+    } else if (!std::strcmp(key, "group_fold")) {
+        M->group_fold = value < 0 ? -1 : (value ? 1 : 0);
     } else if (!std::strcmp(key, "halo_pull")) {
         // -1 auto, 0 off (the RCCL / peer-copy planes), 1 k_pull where possible, 2 in-launch where the
         // peer all-reduce runs (else 1); 3 (diagnostics, the 1-rank emulation): in-launch with no rows
@@ -3347,6 +3404,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "dbg_timeline")) *value = M->d_tl ? 1 : 0;
     else if (!std::strcmp(key, "rhalo_group")) *value = M->rhalo_group;
     else if (!std::strcmp(key, "peer_allreduce")) *value = peer_ar_of(M) ? 1 : 0;
+    else if (!std::strcmp(key, "group_fold")) *value = M->gfold_used;
     else if (!std::strcmp(key, "rhalo")) *value = rhalo_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "halo_pull")) {
         CgArgs a{};

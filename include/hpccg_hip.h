@@ -175,6 +175,10 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   self-test passed on every rank, and the force_comm 2
  *                   emulation), 0 RCCL, 1 on: the two CG scalars summed inside
  *                   the kernels through IPC-mapped mailboxes
+ *   "group_fold"    in-process group run in member order with both dots
+ *                   folded: -1 auto (on) / 0: the last member's kernels sum
+ *                   the dots in rank order (k_group_sum's sum) instead of a
+ *                   k_group_sum launch per dot (get: used by the last solve)
  *   "halo_pull"     r-halo by pull: -1 auto (default), 0 off (the RCCL plane
  *                   group / peer copies), 1 k_pull before each SpMV launch,
  *                   2 in-launch: the iteration's last launch pulls once its

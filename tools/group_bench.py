@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--7pt", dest="s7", action="store_true")
-    ap.add_argument("--variants", default="1:1,1:0,0:1,0:0", help="use_graph:overlap pairs")
+    ap.add_argument("--variants", default="1:1,1:0,0:1,0:0", help="use_graph:overlap[:group_fold]")
     ap.add_argument("--no-single", action="store_true")
     args = ap.parse_args()
     import torch
@@ -68,14 +68,17 @@ def main():
         return hp.group_HPCCG(Ms, bs, xs, max_iter=args.max_iter)[1]
 
     for v in args.variants.split(","):
-            graph, overlap = (int(t) for t in v.split(":"))
+            f = [int(t) for t in v.split(":")]
+            graph, overlap = f[0], f[1]
+            gfold = f[2] if len(f) > 2 else -1  # optional third field: group_fold
             for M in Ms:
                 M.set_option("use_graph", graph)
                 M.set_option("overlap", overlap)
+                M.set_option("group_fold", gfold)
             group = timed(group_step, 1)
             print(json.dumps({
                 "n": args.n, "P": args.P, "stencil": 7 if args.s7 else 27,
-                "use_graph": graph, "overlap": overlap,
+                "use_graph": graph, "overlap": overlap, "group_fold": Ms[0].get_option("group_fold"),
                 "group_us_per_iter": round(group, 2),
                 "P_x_single_us_per_iter": round(single, 2),
                 "multi_rank_overhead_us_per_iter": round(group - single, 2),
