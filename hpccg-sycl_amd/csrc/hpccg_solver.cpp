@@ -1056,9 +1056,10 @@ bool peer_ar_of(const hpccg_hip_matrix* M)
     return !M->in_group && (emulated_multi(M) || M->peer_auto_ok);
 }
 
-// The r-halo by pull (option halo_pull, -1 auto the default): each rank's
-// k_pull reads its ghost planes of r from the neighbours' boundary rows before
-// the SpMV launch (an in-process group's members' buffers; another process's
+// The r-halo by pull (option halo_pull, -1 auto the default): each rank reads
+// its ghost planes of r from the neighbours' boundary rows -- in the
+// iteration's last launch (pull_in_of) or in a k_pull launch before the SpMV
+// launch (an in-process group's members' buffers; another process's
 // through IPC, when the creation-time test passed on every rank; the 1-rank
 // emulation pulls its own rows into scratch) instead of the RCCL send/recv
 // group (or peer copies) after the update: no RCCL call left in the iteration
@@ -1075,8 +1076,8 @@ bool pull_of(const hpccg_hip_matrix* M)
 // iteration's last launch pulls r_k once its own r.r completion is in, which
 // needs the global sum inside the kernel (the peer all-reduce) and r.r folded
 // into its producer (no k_finalize after it). Emulated (force_comm 2, one
-// GPU), per iteration against k_pull: 100^3 +3.1 vs +5.0-5.6 us, 200^3 +5.2
-// vs +6.8-7.3, 7-pt 256^3 +3.9-4.0 vs +6.0-6.5 (profiles/r04_inlaunch).
+// GPU), per iteration against k_pull: 100^3 +3.0 vs +4.8-5.2 us, 200^3
+// +3.9-4.0 vs +5.5, 7-pt 256^3 +3.6-3.7 vs +5.6-5.7 (profiles/r04_inlaunch).
 bool pull_in_of(const hpccg_hip_matrix* M, const CgArgs& a)
 {
     return pull_of(M) && M->halo_pull != 1 && a.peer_ar && fold_of(a, kRR);
