@@ -139,10 +139,12 @@ struct CgArgs {
     // buffers; an RCCL job: IPC-mapped; the emulation: its own rows)
     int pull_in;
     // Group fold (an in-process group run in member order, both dots folded):
-    // the last member's finishing lane sums the members' local totals in rank
-    // order (k_group_sum's sum) and stores the total into every member's g:
-    // gtab[0 .. gn) the members' loc, gtab[gn .. 2 gn) their g; gn = 0 else
-    int gn;
+    // the finishing lane of the phase's last member sums the members' local
+    // totals in rank order (k_group_sum's sum) and stores the total into every
+    // member's g: gtab[0 .. gn) the members' loc, gtab[gn .. 2 gn) their g;
+    // gfw: the dots this member folds (1 p.Ap: the SpMV phase's last, member
+    // gn - 1; 2 r.r: the update phase's last, member 0); grank: its index
+    int gn, gfw, grank;
     double* const* gtab;
     int send;  // one past the last side-flush block (set per launch)
     int pl_lo, pl_hi;

@@ -499,15 +499,15 @@ __device__ __forceinline__ double peer_allreduce(const CgArgs& a, double s, int 
     return tot;
 }
 
-// Group fold (CgArgs::gn, the last member of an in-process group run in
-// member order): every earlier member's launch of this phase has ended, so
-// their local totals are final; summed in rank order from 0.0 (k_group_sum's
+// Group fold (CgArgs::gfw, the last member of a phase of an in-process group
+// run in member order): every other member's launch of this phase has ended,
+// so their local totals are final; summed in rank order from 0.0 (k_group_sum's
 // sum) and stored into every member's g. Not inlined: one lane of one block
 // runs it, and inlined it cost the direct kernel a VGPR and a spill.
-__device__ __noinline__ double group_fold_sum(double* const* gtab, int gn, double s, int which)
+__device__ __noinline__ double group_fold_sum(double* const* gtab, int gn, int grank, double s, int which)
 {
     double v = 0.0;
-    for (int q = 0; q < gn; q++) v += q == gn - 1 ? s : gtab[q][which];
+    for (int q = 0; q < gn; q++) v += q == grank ? s : gtab[q][which];
     for (int q = 0; q < gn; q++) gtab[gn + q][which] = v;
     return v;
 }
@@ -525,8 +525,8 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
         a.g[which] = s;
     } else if (!a.allreduce) {
         a.g[which] = s;
-    } else if (a.gn) {
-        s = group_fold_sum(a.gtab, a.gn, s, which);
+    } else if (a.gfw & (which == kPAP ? 1 : 2)) {
+        s = group_fold_sum(a.gtab, a.gn, a.grank, s, which);
     }
     // the r.r iteration k + 1 reads, by its parity (fused update: kRRPar)
     if (which == kRR && a.fupd) a.g[kRRPar + ((k + 1) & 1)] = s;

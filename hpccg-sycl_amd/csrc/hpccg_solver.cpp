@@ -1540,28 +1540,38 @@ int group_halo_gather(const Ranks& R, int k_host, bool prologue)
 
 // In-process all-reduce of loc[which]: one lane on rank 0's stream adds the
 // ranks' values in rank order and writes g[which] of every rank.
-// Group fold (CgArgs::gn): the last member's kernel sums the dot; the
-// others' streams only wait for it. group_gather_join runs before that
-// member's launch: its stream waits for every other member's.
-bool gfold_of(const Ranks& R) { return R.P > 1 && R.a[R.P - 1].gn > 0; }
+// Group fold (CgArgs::gfw): the phase's last member's kernel sums the dot;
+// the others' streams only wait for it. The SpMV phase runs the members
+// 0 .. P-1 and member P-1 folds p.Ap; the update phase runs them in reverse and
+// member 0 folds r.r, so member 0's next SpMV follows its own update (its r
+// and p still in the MALL: the 2 x 100^3 group's SpMV ran 56-58 us after the
+// other member's launches against 42 us after its own).
+// group_gather_join runs before the folding member's launch: its stream waits
+// for every other member's.
+bool gfold_of(const Ranks& R) { return R.P > 1 && R.a[0].gn > 0; }
+int fold_member(const Ranks& R, int which) { return which == kPAP ? R.P - 1 : 0; }
 
-int group_gather_join(const Ranks& R)
+int group_gather_join(const Ranks& R, int last)
 {
-    for (int r = 0; r < R.P - 1; r++) {
+    for (int r = 0; r < R.P; r++) {
+        if (r == last) continue;
         TRY(use_device(R, r));
         HIP_TRY(hipEventRecord(R.ev[r], R.M[r]->stream));
     }
-    TRY(use_device(R, R.P - 1));
-    for (int r = 0; r < R.P - 1; r++) HIP_TRY(hipStreamWaitEvent(R.M[R.P - 1]->stream, R.ev[r], 0));
+    TRY(use_device(R, last));
+    for (int r = 0; r < R.P; r++)
+        if (r != last) HIP_TRY(hipStreamWaitEvent(R.M[last]->stream, R.ev[r], 0));
     return 0;
 }
 
 int group_allreduce(const Ranks& R, int which)
 {
-    if (gfold_of(R)) {  // summed by the last member's launch: its end releases the others
-        TRY(use_device(R, R.P - 1));
-        HIP_TRY(hipEventRecord(R.ev[R.P], R.M[R.P - 1]->stream));
-        for (int r = 0; r < R.P - 1; r++) {
+    if (gfold_of(R)) {  // summed by the folding member's launch: its end releases the others
+        const int f = fold_member(R, which);
+        TRY(use_device(R, f));
+        HIP_TRY(hipEventRecord(R.ev[R.P], R.M[f]->stream));
+        for (int r = 0; r < R.P; r++) {
+            if (r == f) continue;
             TRY(use_device(R, r));
             HIP_TRY(hipStreamWaitEvent(R.M[r]->stream, R.ev[R.P], 0));
         }
@@ -1858,7 +1868,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
             CgArgs a = R.a[r];
             a.kpar = k_host & 1;  // fused update: the parity slot of k (iter_k)
             TRY(use_device(R, r));
-            if (gfold_of(R) && r == R.P - 1) TRY(group_gather_join(R));  // (use_device(R, r) after it)
+            if (gfold_of(R) && r == R.P - 1) TRY(group_gather_join(R, r));  // (use_device(R, r) after it)
             TRY(use_device(R, r));
             if (pull && !a.pull_in) enqueue_pull(R, r, a);  // r's ghost planes for this SpMV
             if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
@@ -1877,10 +1887,11 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
         return 0;
     }
     TRY(exch_allreduce(R, kPAP));
-    for (int r = 0; r < R.P; r++) {
+    for (int i = 0; i < R.P; i++) {
+        const int r = gfold_of(R) ? R.P - 1 - i : i;  // group fold: the update phase in reverse
         hpccg_hip_matrix* M = R.M[r];
         const CgArgs& a = R.a[r];
-        if (gfold_of(R) && r == R.P - 1) TRY(group_gather_join(R));
+        if (gfold_of(R) && r == fold_member(R, kRR)) TRY(group_gather_join(R, r));
         TRY(use_device(R, r));
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], M->stream));
         launch_cg_update(a, false, M->stream);
@@ -1911,14 +1922,17 @@ int enqueue_prologue(const Ranks& R, bool events)
         if (events) HIP_TRY(hipEventRecord(M->ev[0], s));
         launch_cg_spmv(a, M->kernel, true, s);  // Ap = A p
         if (events) HIP_TRY(hipEventRecord(M->ev[1], s));
-        if (gfold_of(R) && r == R.P - 1) {
-            TRY(group_gather_join(R));
-            TRY(use_device(R, r));
-        }
+        if (gfold_of(R)) continue;  // the updates below, in reverse (fold_member)
         if (events) HIP_TRY(hipEventRecord(M->ev[2], s));
         launch_cg_update(a, true, s);  // r = b - Ap (+ r.r partials)
         if (events) HIP_TRY(hipEventRecord(M->ev[3], s));
         if (!fold_of(a, kRR)) launch_cg_finalize(a, kRR, true, s);  // rtrans, k = 1
+    }
+    for (int i = 0; gfold_of(R) && i < R.P; i++) {  // group fold: member 0 last, it folds r.r
+        const int r = R.P - 1 - i;
+        if (r == fold_member(R, kRR)) TRY(group_gather_join(R, r));
+        TRY(use_device(R, r));
+        launch_cg_update(R.a[r], true, R.M[r]->stream);
     }
     if (R.a[0].rhalo)
         TRY(exch_rr_rhalo(R));  // r_0's planes: iteration 1 forms p_1 = r_0 at the ghost rows
@@ -2469,20 +2483,28 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     // no overlapped halo (its SpMV runs as two launches)
     if (P > 1 && Ms[0]->group_fold != 0 && av[0].allreduce && fold_of(av[0], kPAP) && fold_of(av[0], kRR) &&
         !Ms[0]->overlap) {
-        hpccg_hip_matrix* L = Ms[P - 1];
-        HIP_TRY(hipSetDevice(L->device));
-        if (!L->d_gtab) TRY(dev_alloc(L, &L->d_gtab, 2 * kMaxGroupRanks));
-        L->h_gtab.assign(2 * P, nullptr);
-        for (int r = 0; r < P; r++) {
-            L->h_gtab[r] = av[r].loc;
-            L->h_gtab[P + r] = av[r].g;
+        for (int f : {P - 1, 0}) {  // the folding members: p.Ap (the SpMV phase's last), r.r (the update's)
+            hpccg_hip_matrix* L = Ms[f];
+            HIP_TRY(hipSetDevice(L->device));
+            if (!L->d_gtab) TRY(dev_alloc(L, &L->d_gtab, 2 * kMaxGroupRanks));
+            L->h_gtab.assign(2 * P, nullptr);
+            for (int r = 0; r < P; r++) {
+                L->h_gtab[r] = av[r].loc;
+                L->h_gtab[P + r] = av[r].g;
+            }
+            HIP_TRY(hipMemcpyAsync(L->d_gtab, L->h_gtab.data(), sizeof(double*) * 2 * P, hipMemcpyHostToDevice,
+                                   L->stream));
+            HIP_TRY(hipStreamSynchronize(L->stream));  // (pageable source: done before it can change)
+            av[f].gtab = L->d_gtab;
         }
-        HIP_TRY(hipMemcpyAsync(L->d_gtab, L->h_gtab.data(), sizeof(double*) * 2 * P, hipMemcpyHostToDevice, L->stream));
-        HIP_TRY(hipStreamSynchronize(L->stream));  // (pageable source: done before it can change)
-        av[P - 1].gn = P;
-        av[P - 1].gtab = L->d_gtab;
+        for (int r = 0; r < P; r++) {
+            av[r].gn = P;
+            av[r].grank = r;
+        }
+        av[P - 1].gfw |= 1;
+        av[0].gfw |= 2;
     }
-    for (int r = 0; r < P; r++) Ms[r]->gfold_used = av[P - 1].gn > 0 ? 1 : 0;
+    for (int r = 0; r < P; r++) Ms[r]->gfold_used = av[0].gn > 0 ? 1 : 0;
     const Ranks R{Ms, av.data(), P, gev.data()};
     if (events) TRY(ensure_events(M, iters + 1));
     TRY(enqueue_prologue(R, events));
