@@ -48,6 +48,13 @@ enum SpmvKernel : int {
 
 // Everything a CG kernel needs, passed by value (graph-capture friendly: all
 // per-iteration state lives in device memory, never in kernel arguments).
+// One run of rows a pull copies: src (another member's boundary rows) -> dst.
+struct PullSeg {
+    const double* src;
+    double* dst;
+    long long cnt;
+};
+
 struct CgArgs {
     int n;                 // local rows
     int nslices;           // ceil(n / kSliceRows)
@@ -146,6 +153,11 @@ struct CgArgs {
     // gn - 1; 2 r.r: the update phase's last, member 0); grank: its index
     int gn, gfw, grank;
     double* const* gtab;
+    // the group fold's pull: member 0's update (the last launch of an
+    // iteration) pulls every member's ghost planes: npseg segments of
+    // pseg_rows rows in all (psegs in device memory); 0: pl_* alone
+    const struct PullSeg* psegs;
+    int npseg, pseg_rows;
     int send;  // one past the last side-flush block (set per launch)
     int pl_lo, pl_hi;
     const double* pl_src_lo;

@@ -989,6 +989,35 @@ __device__ __forceinline__ bool side_flush(const CgArgs& a, bool prologue)
 // order). The neighbour overwrites its rows only after this rank's next p.Ap
 // contribution, which follows this launch. bl / nbl: this block among the
 // pull blocks.
+// Rows [0, lo) of src_lo and [0, hi) of src_hi into dst_lo / dst_hi, block bl
+// of nbl: system-scope loads (another GPU's or member's memory, stored
+// write-through there), plain stores (read by the next launch).
+__device__ __forceinline__ void copy_rows(const double* src_lo, double* dst_lo, int lo, const double* src_hi,
+                                          double* dst_hi, int hi, int bl, int nbl)
+{
+    constexpr int kU = 4;  // loads in flight per thread
+    const int tot = lo + hi;
+    const int nth = nbl * (int)blockDim.x;
+    for (int i0 = bl * (int)blockDim.x + (int)threadIdx.x; i0 < tot; i0 += kU * nth) {
+        double w[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int i = i0 + u * nth;
+            w[u] = i < tot ? __hip_atomic_load(i < lo ? src_lo + i : src_hi + (i - lo), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM)
+                           : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int i = i0 + u * nth;
+            if (i < tot) (i < lo ? dst_lo[i] : dst_hi[i - lo]) = w[u];
+        }
+    }
+}
+
+// kSeg: the caller may carry the group fold's segment table (k_update only:
+// the fused SpMV kernel's registers stay as they are).
+template <bool kSeg = false>
 __device__ __forceinline__ void pull_rows(const CgArgs& a, int k, int bl, int nbl)
 {
     if (k + 1 >= a.max_iter) return;  // no SpMV reads them
@@ -1004,24 +1033,14 @@ __device__ __forceinline__ void pull_rows(const CgArgs& a, int k, int bl, int nb
     }
     if (v != k + 1) return;  // the solve was aborted
     if (bl == 0 && threadIdx.x == 0) stamp(a, k + 1, kStampHalo);
-    constexpr int kU = 4;  // loads in flight per thread
-    const int tot = a.pl_lo + a.pl_hi;
-    const int nth = nbl * (int)blockDim.x;
-    for (int i0 = bl * (int)blockDim.x + (int)threadIdx.x; i0 < tot; i0 += kU * nth) {
-        double w[kU];
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int i = i0 + u * nth;
-            w[u] = i < tot ? __hip_atomic_load(i < a.pl_lo ? a.pl_src_lo + i : a.pl_src_hi + (i - a.pl_lo),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                           : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int i = i0 + u * nth;
-            if (i < tot) (i < a.pl_lo ? a.pl_dst_lo[i] : a.pl_dst_hi[i - a.pl_lo]) = w[u];
+    if constexpr (kSeg) {
+        if (a.npseg) {
+            for (int g = 0; g < a.npseg; g++)
+                copy_rows(a.psegs[g].src, a.psegs[g].dst, (int)a.psegs[g].cnt, nullptr, nullptr, 0, bl, nbl);
+            return;
         }
     }
+    copy_rows(a.pl_src_lo, a.pl_dst_lo, a.pl_lo, a.pl_src_hi, a.pl_dst_hi, a.pl_hi, bl, nbl);
 }
 
 template <bool kFU>
@@ -1885,7 +1904,7 @@ __global__ __launch_bounds__(kBlock) void k_update(CgArgs a)
             if (!a.kst[5]) return;  // publish_iter's {k, run}
             k = a.kst[4];
         }
-        pull_rows(a, k, (int)blockIdx.x - a.grid, (int)gridDim.x - a.grid);
+        pull_rows<true>(a, k, (int)blockIdx.x - a.grid, (int)gridDim.x - a.grid);
         return;
     }
     int k = 0;
@@ -2475,7 +2494,7 @@ void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s)
 {
     // in-launch pull: trailing blocks, about four rows per thread
-    const int ptot = a.pull_in ? a.pl_lo + a.pl_hi : 0;
+    const int ptot = a.pull_in ? (a.npseg ? a.pseg_rows : a.pl_lo + a.pl_hi) : 0;
     const dim3 grid(a.grid + (ptot + 4 * kBlock - 1) / (4 * kBlock));
     if (prologue)
         hipLaunchKernelGGL((k_update<true>), grid, dim3(kBlock), 0, s, a);

@@ -273,6 +273,8 @@ struct hpccg_hip_matrix {
     double* d_scal = nullptr;  // g[2], loc[2], spare
     double** d_gtab = nullptr;  // group fold (last member): the members' loc, then their g
     std::vector<double*> h_gtab;
+    PullSeg* d_pseg = nullptr;  // group fold (member 0): every member's pull, done by its update
+    std::vector<PullSeg> h_pseg;
     int group_fold = -1;        // option group_fold: -1 auto (on where it applies), 0 off
     int gfold_used = 0;         // the last group solve summed its dots in the last member's kernels
     int* d_kst = nullptr;      // [0, kErrBase) iteration state, then the device error record (kErrWords)
@@ -456,6 +458,7 @@ int free_matrix(hpccg_hip_matrix* M)
     }
     if (M->d_mbox) (void)hipFree(M->d_mbox);
     if (M->d_gtab) (void)hipFree(M->d_gtab);
+    if (M->d_pseg) (void)hipFree(M->d_pseg);
     if (M->d_peers) (void)hipFree(M->d_peers);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
     if (M->ev_flush) (void)hipEventDestroy(M->ev_flush);
@@ -1870,7 +1873,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
             TRY(use_device(R, r));
             if (gfold_of(R) && r == R.P - 1) TRY(group_gather_join(R, r));  // (use_device(R, r) after it)
             TRY(use_device(R, r));
-            if (pull && !a.pull_in) enqueue_pull(R, r, a);  // r's ghost planes for this SpMV
+            if (pull && !a.pull_in && !a.npseg) enqueue_pull(R, r, a);  // r's ghost planes for this SpMV
             if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot], M->stream));
             launch_cg_spmv(a, M->kernel, false, M->stream);
             if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 1], M->stream));
@@ -2503,6 +2506,31 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
         }
         av[P - 1].gfw |= 1;
         av[0].gfw |= 2;
+        // the r-halo by pull: member 0's update, the iteration's last launch,
+        // pulls every member's ghost planes once its r.r fold is in (every
+        // other member's update ran before it): no k_pull launch per member
+        if (multi_of(M) && pull_of(M) && !Ms[0]->general) {
+            hpccg_hip_matrix* L = Ms[0];
+            HIP_TRY(hipSetDevice(L->device));
+            if (!L->d_pseg) TRY(dev_alloc(L, &L->d_pseg, 2 * kMaxGroupRanks));
+            L->h_pseg.clear();
+            long long rows = 0;
+            for (int r = 0; r < P; r++) {
+                if (av[r].pl_lo) L->h_pseg.push_back({av[r].pl_src_lo, av[r].pl_dst_lo, av[r].pl_lo});
+                if (av[r].pl_hi) L->h_pseg.push_back({av[r].pl_src_hi, av[r].pl_dst_hi, av[r].pl_hi});
+                rows += av[r].pl_lo + av[r].pl_hi;
+            }
+            if (!L->h_pseg.empty()) {
+                HIP_TRY(hipMemcpyAsync(L->d_pseg, L->h_pseg.data(), sizeof(PullSeg) * L->h_pseg.size(),
+                                       hipMemcpyHostToDevice, L->stream));
+                HIP_TRY(hipStreamSynchronize(L->stream));
+                for (int r = 0; r < P; r++) av[r].npseg = -1;  // pulled by member 0: no k_pull
+                av[0].pull_in = 1;
+                av[0].psegs = L->d_pseg;
+                av[0].npseg = (int)L->h_pseg.size();
+                av[0].pseg_rows = (int)rows;
+            }
+        }
     }
     for (int r = 0; r < P; r++) Ms[r]->gfold_used = av[0].gn > 0 ? 1 : 0;
     const Ranks R{Ms, av.data(), P, gev.data()};
