@@ -504,11 +504,16 @@ __device__ __forceinline__ double peer_allreduce(const CgArgs& a, double s, int 
 // so their local totals are final; summed in rank order from 0.0 (k_group_sum's
 // sum) and stored into every member's g. Not inlined: one lane of one block
 // runs it, and inlined it cost the direct kernel a VGPR and a spill.
-__device__ __noinline__ double group_fold_sum(double* const* gtab, int gn, int grank, double s, int which)
+// r.r also goes to the parity slot iteration k + 1 reads (a member that runs
+// the fused update reads it there; harmless for the others).
+__device__ __noinline__ double group_fold_sum(double* const* gtab, int gn, int grank, double s, int which, int k)
 {
     double v = 0.0;
     for (int q = 0; q < gn; q++) v += q == grank ? s : gtab[q][which];
-    for (int q = 0; q < gn; q++) gtab[gn + q][which] = v;
+    for (int q = 0; q < gn; q++) {
+        gtab[gn + q][which] = v;
+        if (which == kRR) gtab[gn + q][kRRPar + ((k + 1) & 1)] = v;
+    }
     return v;
 }
 
@@ -526,7 +531,7 @@ __device__ __forceinline__ void finish_dot(const CgArgs& a, double s, int which,
     } else if (!a.allreduce) {
         a.g[which] = s;
     } else if (a.gfw & (which == kPAP ? 1 : 2)) {
-        s = group_fold_sum(a.gtab, a.gn, a.grank, s, which);
+        s = group_fold_sum(a.gtab, a.gn, a.grank, s, which, k);
     }
     // the r.r iteration k + 1 reads, by its parity (fused update: kRRPar)
     if (which == kRR && a.fupd) a.g[kRRPar + ((k + 1) & 1)] = s;

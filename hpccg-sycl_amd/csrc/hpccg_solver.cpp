@@ -1894,6 +1894,7 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
         const int r = gfold_of(R) ? R.P - 1 - i : i;  // group fold: the update phase in reverse
         hpccg_hip_matrix* M = R.M[r];
         const CgArgs& a = R.a[r];
+        if (a.fupd) continue;  // (group fold: member P-1's update ran in its SpMV launch)
         if (gfold_of(R) && r == fold_member(R, kRR)) TRY(group_gather_join(R, r));
         TRY(use_device(R, r));
         if (slot >= 0) HIP_TRY(hipEventRecord(M->ev[4 * slot + 2], M->stream));
@@ -1951,7 +1952,7 @@ int enqueue_prologue(const Ranks& R, bool events)
 int graph_chunk_of(const Ranks& R)
 {
     int chunk = std::max(1, R.M[0]->graph_iters);
-    if (R.a[0].fupd) chunk += chunk & 1;  // the parity of k is baked into each captured launch
+    if (R.a[0].fupd || R.a[R.P - 1].fupd) chunk += chunk & 1;  // the parity of k is baked into each captured launch
     if (multi_of(R.M[0]) && !R.a[0].rhalo) {
         const int ring = R.a[0].nring;
         chunk = (chunk + ring - 1) / ring * ring;
@@ -2506,6 +2507,17 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
         }
         av[P - 1].gfw |= 1;
         av[0].gfw |= 2;
+        // member P-1 folds p.Ap inside its SpMV launch, after every other
+        // member's: with the direct kernel its update runs as trailing blocks of
+        // that launch (the fused update; member 0's r.r fold also stores its
+        // parity slot), one launch less per group iteration
+        {
+            hpccg_hip_matrix* L = Ms[P - 1];
+            CgArgs& l = av[P - 1];
+            if (L->fuse_update != 0 && L->kernel == kSpmvDirect && l.fuse_p && fold_effective(L) == 1 &&
+                l.xdefer == 2)
+                l.fupd = 1;
+        }
         // the r-halo by pull: member 0's update, the iteration's last launch,
         // pulls every member's ghost planes once its r.r fold is in (every
         // other member's update ran before it): no k_pull launch per member
