@@ -274,6 +274,14 @@ class Stages:
             os._exit(124)
 
 
+def opt_or_none(M, key):
+    """An option's effective value, or None where the library predates it."""
+    try:
+        return M.get_option(key)
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -490,9 +498,9 @@ def main():
                 "device_bytes_per_gpu": M.get_option("device_bytes"),
                 "graph_replay": bool(graph_used),
                 "placement_probe": placement_report(args.placement, probe_us, pick),
-                "options": {k: M.get_option(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update",
-                                                         "overlap", "graph_chunk", "nt", "a2_ring", "nt_store",
-                                                         "fuse_update")},
+                "options": {k: opt_or_none(M, k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update",
+                                                           "overlap", "graph_chunk", "nt", "a2_ring", "nt_store",
+                                                           "fuse_update", "rhalo", "peer_allreduce", "halo_pull")},
             },
             "cg_iterations_per_s_global": round(it_per_s, 3),
             "spmv_effective_gbs": round(achieved, 1),
