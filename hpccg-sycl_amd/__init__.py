@@ -41,6 +41,11 @@ def build(jobs: int = 8) -> None:
     subprocess.run(["make", "-s", "-C", HERE, f"-j{jobs}"], check=True)
 
 
+# hpccg_hip_allgather_fn (include/hpccg_hip.h): send, recv, bytes per rank, ctx
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_ulonglong, C.c_void_p)
+_host_allgather = None  # the live callback of comm_init_host (ctypes must keep it)
+
+
 class _HPCMatrix(C.Structure):
     """HPC_Sparse_Matrix (HPC_Sparse_Matrix.hpp:54-85, non-MPI layout)."""
     _fields_ = [
@@ -76,6 +81,9 @@ def lib() -> C.CDLL:
         "hpccg_hip_set_device": (ip, [ip]),
         "hpccg_hip_comm_unique_id": (ip, [C.c_char_p]),
         "hpccg_hip_comm_init": (ip, [C.c_char_p, ip, ip]),
+        "hpccg_hip_comm_init_host": (ip, [ip, ip, ALLGATHER_FN, vp]),
+        "hpccg_hip_comm_mode": (ip, [PI]),
+        "hpccg_hip_diag_canary_check": (ip, [PI, C.c_char_p, ip]),
         "hpccg_hip_comm_destroy": (ip, []),
         "hpccg_hip_comm_size": (ip, [PI, PI]),
         "hpccg_hip_comm_allreduce_host": (ip, [PD, ip, ip]),
@@ -522,8 +530,66 @@ def comm_allreduce_host(vals, op: str = "sum") -> np.ndarray:
     return a
 
 
+def torch_allgather(data: bytes) -> list:
+    """Every rank's `data` (same length everywhere) in rank order over the
+    default torch.distributed group (gloo in this package's launchers)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, t)
+    return [o.numpy().tobytes() for o in outs]
+
+
+def comm_init_host(nranks: int, rank: int, allgather=None) -> None:
+    """Host-bootstrapped communicator (hpccg_hip_comm_init_host): the setup
+    exchanges go through allgather(bytes) -> [bytes of every rank] (default:
+    torch.distributed's default group), no RCCL; the CG iteration runs the
+    in-kernel peer all-reduce and the halo pull. Several ranks may share a GPU."""
+    global _host_allgather
+    ag = allgather or torch_allgather
+
+    def cb(send, recv, nbytes, ctx):
+        try:
+            n = int(nbytes)
+            parts = ag(C.string_at(send, n))
+            if len(parts) != nranks:
+                return 1
+            for q, part in enumerate(parts):
+                if len(part) != n:
+                    return 1
+                C.memmove(recv + q * n, part, n)
+            return 0
+        except BaseException:  # reported, and the library sees a failed exchange
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    fn = ALLGATHER_FN(cb)
+    _check(lib().hpccg_hip_comm_init_host(nranks, rank, fn, None), "comm_init_host")
+    _host_allgather = fn
+
+
+def comm_mode() -> str:
+    """'none' (one rank), 'rccl' or 'host' (hpccg_hip_comm_init_host)."""
+    m = C.c_int(0)
+    _check(lib().hpccg_hip_comm_mode(C.byref(m)), "comm_mode")
+    return {0: "none", 1: "rccl", 2: "host"}[m.value]
+
+
+def canary_check() -> tuple:
+    """(enabled, tripped canaries, report) -- canary mode is HPCCG_CANARY=1
+    when the library first allocates (hpccg_hip_diag_canary_check)."""
+    en = C.c_int(0)
+    buf = C.create_string_buffer(4096)
+    n = lib().hpccg_hip_diag_canary_check(C.byref(en), buf, 4096)
+    return bool(en.value), n, buf.value.decode(errors="replace")
+
+
 def comm_destroy() -> None:
+    global _host_allgather
     lib().hpccg_hip_comm_destroy()
+    _host_allgather = None
 
 
 def runtime_info() -> dict:

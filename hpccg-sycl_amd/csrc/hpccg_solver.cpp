@@ -86,8 +86,68 @@ struct Comm {
     ncclComm_t comm = nullptr;
     int nranks = 1;
     int rank = 0;
+    // host-bootstrapped (hpccg_hip_comm_init_host): no RCCL communicator; the
+    // setup exchanges go through the caller's all-gather, and the iteration
+    // must run without a collective (peer all-reduce + halo pull)
+    hpccg_hip_allgather_fn ag = nullptr;
+    void* ag_ctx = nullptr;
+    // RCCL: the setup collectives' stream and staging buffer
+    hipStream_t stream = nullptr;
+    unsigned char* d_buf = nullptr;
+    size_t buf_bytes = 0;
 };
 Comm g_comm;
+bool comm_host() { return g_comm.ag != nullptr; }
+bool comm_up() { return g_comm.comm != nullptr || g_comm.ag != nullptr; }
+
+void comm_reset()
+{
+    if (g_comm.comm) ncclCommDestroy(g_comm.comm);
+    if (g_comm.d_buf) (void)hipFree(g_comm.d_buf);
+    if (g_comm.stream) (void)hipStreamDestroy(g_comm.stream);
+    g_comm = Comm();
+}
+
+// All-gather of `bytes` host bytes per rank into all[nranks * bytes] (rank
+// order): RCCL staged through device memory, or the host bootstrap's
+// callback. The setup-time exchanges of make_local_matrix.cpp:185-201 /
+// :286-587 and the self-tests' verdicts go through here.
+int comm_allgather(const void* mine, void* all, size_t bytes)
+{
+    if (g_comm.nranks == 1 || !comm_up()) {
+        std::memcpy(all, mine, bytes);
+        return 0;
+    }
+    if (g_comm.ag) {
+        if (g_comm.ag(mine, all, (unsigned long long)bytes, g_comm.ag_ctx) != 0)
+            return set_err(HPCCG_HIP_EINVAL, "the host all-gather callback failed (%zu B per rank)", bytes);
+        return 0;
+    }
+    const size_t need = bytes * (size_t)(g_comm.nranks + 1);
+    if (!g_comm.stream) HIP_TRY(hipStreamCreateWithFlags(&g_comm.stream, hipStreamNonBlocking));
+    if (need > g_comm.buf_bytes) {
+        if (g_comm.d_buf) (void)hipFree(g_comm.d_buf);
+        g_comm.d_buf = nullptr;
+        g_comm.buf_bytes = 0;
+        HIP_TRY(hipMalloc(&g_comm.d_buf, need));
+        g_comm.buf_bytes = need;
+    }
+    unsigned char* d = g_comm.d_buf;
+    HIP_TRY(hipMemcpyAsync(d + bytes * g_comm.nranks, mine, bytes, hipMemcpyHostToDevice, g_comm.stream));
+    NCCL_TRY(ncclAllGather(d + bytes * g_comm.nranks, d, bytes, ncclUint8, g_comm.comm, g_comm.stream));
+    HIP_TRY(hipStreamSynchronize(g_comm.stream));
+    HIP_TRY(hipMemcpy(all, d, bytes * g_comm.nranks, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// Minimum over the ranks of one int (the self-tests' verdicts).
+int comm_min(int v, int* out)
+{
+    std::vector<int> all(std::max(1, g_comm.nranks));
+    TRY(comm_allgather(&v, all.data(), sizeof v));
+    *out = *std::min_element(all.begin(), all.end());
+    return 0;
+}
 
 // Gather halo plan (make_local_matrix.cpp:58-610, exchange_externals.cpp:51-131)
 // for partitions the z-slab plan cannot serve: the external columns get local
@@ -290,6 +350,7 @@ struct hpccg_hip_matrix {
     // r-halo by pull (option halo_pull: -1 auto, 0 the RCCL / peer-copy planes, 1 k_pull, 2 in-launch)
     int halo_pull = -1;
     int pull_auto_ok = 0;              // RCCL job: the creation-time pull test passed on every rank
+    int proto_auto_ok = 0;             // ... and the production-protocol test (protocol_autotest)
     double* d_pull_lo = nullptr;       // rank - 1's r (its local row 0), mapped here (RCCL job)
     double* d_pull_hi = nullptr;       // rank + 1's r
     int pull_lo_n = 0;                 // rank - 1's row count
@@ -340,15 +401,117 @@ struct hpccg_hip_matrix {
 
 namespace {
 
+// Canary debug mode (HPCCG_CANARY=1 in the environment when the library first
+// allocates): every matrix buffer gets kCanaryBytes of a NaN
+// pattern no kernel stores (0x7FF5C0DE in every 32-bit word) before and after
+// it, registered here, and every canary of the process is checked after each
+// solve (and by hpccg_hip_diag_canary_check). A store that runs past a buffer
+// trips the canary next to it and names the buffer and the offset. Off: one
+// plain hipMalloc per buffer, nothing registered.
+constexpr size_t kCanaryBytes = size_t(64) << 10;
+constexpr unsigned kCanaryWord = 0x7FF5C0DEu;
+struct CanaryRec {
+    char* base;    // the allocation: [canary | user bytes | canary]
+    size_t bytes;  // user bytes
+};
+std::mutex g_canary_mu;
+std::unordered_map<void*, CanaryRec> g_canary;  // user pointer -> allocation
+bool canary_on()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("HPCCG_CANARY");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 // Large device buffers. Never physically contiguous allocations
 // (hipDeviceMallocContiguous): on this stack they corrupted OTHER live
 // buffers and later allocations -- wrong b / x0 seen by the next solve, a
 // matrix image whose uploaded columns the A pass rejected -- even while the
 // contiguous buffers were held and never freed (DESIGN.md 4,
-// tools/diag_carry.py, profiles/r04_carry/).
-hipError_t big_malloc(void** p, size_t b)
+// tools/diag_carry.py, profiles/r04_carry/). The product library has no path
+// to them at all; the diagnostics variant (-DHPCCG_DIAG_CONTIG) keeps one.
+hipError_t big_malloc(void** p, size_t b, unsigned flags = hipDeviceMallocDefault)
 {
-    return hipMalloc(p, b);
+    if (!canary_on()) return flags == hipDeviceMallocDefault ? hipMalloc(p, b) : hipExtMallocWithFlags(p, b, flags);
+    void* base = nullptr;
+    const size_t tot = b + 2 * kCanaryBytes;
+    hipError_t e = flags == hipDeviceMallocDefault ? hipMalloc(&base, tot) : hipExtMallocWithFlags(&base, tot, flags);
+    if (e != hipSuccess) return e;
+    // both canaries written and landed before the buffer is handed out
+    const size_t words = kCanaryBytes / 4;
+    char* c = static_cast<char*>(base);
+    if ((e = hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(c), (int)kCanaryWord, words)) != hipSuccess ||
+        (e = hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(c + kCanaryBytes + b), (int)kCanaryWord, words)) !=
+            hipSuccess ||
+        (e = hipDeviceSynchronize()) != hipSuccess) {
+        (void)hipFree(base);
+        return e;
+    }
+    *p = c + kCanaryBytes;
+    std::lock_guard<std::mutex> lk(g_canary_mu);
+    g_canary[*p] = CanaryRec{c, b};
+    return hipSuccess;
+}
+
+// Frees what big_malloc handed out (any other device pointer: plain hipFree).
+void big_free(void* p)
+{
+    if (!p) return;
+    if (canary_on()) {
+        std::lock_guard<std::mutex> lk(g_canary_mu);
+        const auto it = g_canary.find(p);
+        if (it != g_canary.end()) {
+            p = it->second.base;
+            g_canary.erase(it);
+        }
+    }
+    (void)hipFree(p);
+}
+
+// Every registered canary checked (device-wide sync first). Returns the number
+// of tripped canaries; the first few are described in *report.
+int canary_check(std::string* report)
+{
+    if (!canary_on()) return 0;
+    if (hipDeviceSynchronize() != hipSuccess) (void)hipGetLastError();
+    std::lock_guard<std::mutex> lk(g_canary_mu);
+    std::vector<unsigned> buf(kCanaryBytes / 4);
+    int bad = 0;
+    for (const auto& kv : g_canary) {
+        const CanaryRec& c = kv.second;
+        for (int side = 0; side < 2; side++) {
+            const char* src = side == 0 ? c.base : c.base + kCanaryBytes + c.bytes;
+            if (hipMemcpy(buf.data(), src, kCanaryBytes, hipMemcpyDeviceToHost) != hipSuccess) {
+                (void)hipGetLastError();
+                continue;
+            }
+            size_t first = buf.size(), last = 0, n = 0;
+            for (size_t i = 0; i < buf.size(); i++)
+                if (buf[i] != kCanaryWord) {
+                    first = std::min(first, i);
+                    last = i;
+                    n++;
+                }
+            if (!n) continue;
+            bad++;
+            if (report && bad <= 8) {
+                char line[256];
+                // head canary: offsets before the buffer (negative); tail: past its end
+                const long long b0 = side == 0 ? -(long long)kCanaryBytes + 4 * (long long)first
+                                               : (long long)c.bytes + 4 * (long long)first;
+                const long long b1 = side == 0 ? -(long long)kCanaryBytes + 4 * (long long)last
+                                               : (long long)c.bytes + 4 * (long long)last;
+                std::snprintf(line, sizeof line,
+                              "canary %s of buffer %p (%zu B): %zu words changed, bytes [%lld, %lld] relative to "
+                              "the buffer, first word 0x%08x\n",
+                              side == 0 ? "head" : "tail", kv.first, c.bytes, n, b0, b1 + 3, buf[first]);
+                *report += line;
+            }
+        }
+    }
+    return bad;
 }
 
 // Host-to-device copy ordered on stream s (no matrix: the kernel-level API's
@@ -414,7 +577,7 @@ void dev_free(hpccg_hip_matrix* M, T** p, size_t count)
 {
     if (*p) {
         (void)flush_stream(M);
-        (void)hipFree(*p);
+        big_free(*p);
         M->bytes -= (long long)(sizeof(T) * std::max<size_t>(1, count));
     }
     *p = nullptr;
@@ -445,21 +608,17 @@ int free_matrix(hpccg_hip_matrix* M)
                     M->d_Ap,         M->d_x,      M->d_b,         M->d_tickets,  M->d_scal,
                     M->d_kst,        M->d_hist,   M->d_stamps,    M->d_gen_b,   M->d_gen_x0,   M->d_gen_xexact,
                     M->d_send_idx,   M->d_send_buf,  M->d_emul,  M->d_tl};
-    for (void* p : ptrs)
-        if (p) (void)hipFree(p);
+    for (void* p : ptrs) big_free(p);
     for (void* p : M->ipc_opened) (void)hipIpcCloseMemHandle(p);
     for (void* p : M->ipc_r_opened) (void)hipIpcCloseMemHandle(p);
     if (M->h_rb) (void)hipHostFree(M->h_rb);
-    for (void* p : M->graveyard) (void)hipFree(p);
+    for (void* p : M->graveyard) big_free(p);
     for (const auto& v : M->vmm) {
         (void)hipMemUnmap(v.va, v.bytes);
         (void)hipMemRelease(v.h);
         (void)hipMemAddressFree(v.res, v.res_bytes);
     }
-    if (M->d_mbox) (void)hipFree(M->d_mbox);
-    if (M->d_gtab) (void)hipFree(M->d_gtab);
-    if (M->d_pseg) (void)hipFree(M->d_pseg);
-    if (M->d_peers) (void)hipFree(M->d_peers);
+    for (void* p : {(void*)M->d_mbox, (void*)M->d_gtab, (void*)M->d_pseg, (void*)M->d_peers}) big_free(p);
     for (hipEvent_t e : M->ev) (void)hipEventDestroy(e);
     if (M->ev_flush) (void)hipEventDestroy(M->ev_flush);
     if (M->ev_mid) (void)hipEventDestroy(M->ev_mid);
@@ -689,20 +848,18 @@ int exchange_plan(hpccg_hip_matrix* M, int* mode = nullptr, std::vector<int>* al
             return set_err(HPCCG_HIP_EPLAN, "columns outside the local rows on a single rank");
         return 0;
     }
-    int* d = nullptr;
-    HIP_TRY(hipMalloc(&d, sizeof(int) * 4 * (g_comm.nranks + 1)));
     int mine[4] = {M->nrow, M->ghost_lo, M->ghost_hi, M->start_row};
-    TRY(h2d(M, d, mine, sizeof mine));
-    NCCL_TRY(ncclAllGather(d, d + 4, 4, ncclInt32, g_comm.comm, M->stream));
     std::vector<int> all(4 * g_comm.nranks);
-    TRY(d2h(M->stream, all.data(), d + 4, sizeof(int) * 4 * g_comm.nranks));
-    HIP_TRY(hipStreamSynchronize(M->stream));
-    (void)hipFree(d);
+    TRY(comm_allgather(mine, all.data(), sizeof mine));
     const int md = choose_halo_mode(all.data(), g_comm.nranks);
     if (md < 0) return set_err(HPCCG_HIP_EPLAN, "the z-slab halo plan cannot serve this partition");
     if (all_out) *all_out = all;
     if (md == 2) {
         if (!mode) return set_err(HPCCG_HIP_EPLAN, "gather halo plan needs the matrix rows");
+        // (every rank decides this from the same all-gathered rows)
+        if (comm_host())
+            return set_err(HPCCG_HIP_EPLAN, "the gather halo plan moves p through RCCL; a host-bootstrapped "
+                                            "communicator serves z-slab partitions only");
         *mode = 2;
         return 0;
     }
@@ -1115,7 +1272,7 @@ int alloc_ring(hpccg_hip_matrix* M, int nbuf)
     double* buf = nullptr;
     HIP_TRY(big_malloc(reinterpret_cast<void**>(&buf), sizeof(double) * ptotal));
     if (hipMemsetAsync(buf, 0, sizeof(double) * ptotal, M->stream) != hipSuccess) {
-        (void)hipFree(buf);
+        big_free(buf);
         return set_err(HPCCG_HIP_EHIP, "hipMemset of the p ring failed");
     }
     dev_free(M, &M->d_pbuf, (size_t)M->pstride * M->ring_alloc);
@@ -1376,6 +1533,14 @@ CgArgs unit_range(const CgArgs& a, int s0, int n0, int s1, int n1)
 // Halo exchange of p (exchange_externals.cpp:51-131): the z-slab ghosts are
 // contiguous, so no pack: rank r sends its first send_lo rows down and its
 // last send_hi rows up, and receives straight into the ghost regions.
+// The RCCL data path asked for on a host-bootstrapped communicator (solve_ranks
+// refuses such an iteration up front; this guards every other caller).
+int need_rccl(const char* what)
+{
+    return set_err(HPCCG_HIP_EINVAL, "%s needs RCCL: the host-bootstrapped communicator runs the peer all-reduce "
+                                     "and the halo pull only", what);
+}
+
 int enqueue_halo(hpccg_hip_matrix* M, double* p, hipStream_t st, double* dst = nullptr)
 {
     // dst: where the ghost planes land (local row 0 of that buffer; p's own by default)
@@ -1393,6 +1558,7 @@ int enqueue_halo(hpccg_hip_matrix* M, double* p, hipStream_t st, double* dst = n
         NCCL_TRY(ncclGroupEnd());
         return 0;
     }
+    if (!g_comm.comm) return need_rccl("the p halo exchange");
     const int r = g_comm.rank;
     NCCL_TRY(ncclGroupStart());
     if (r > 0) {
@@ -1407,12 +1573,44 @@ int enqueue_halo(hpccg_hip_matrix* M, double* p, hipStream_t st, double* dst = n
     return 0;
 }
 
+// The z-slab halo of p through the host bootstrap (the kernel-level sparsemv
+// of a host-bootstrapped job; its solver pulls r's planes in the kernels):
+// every rank contributes its first send_lo and last send_hi rows and takes its
+// ghost planes from its neighbours' contributions (exchange_externals.cpp
+// :87-126, staged through the host). Local failures are recorded, not
+// returned, until both all-gathers are done.
+int host_halo(hpccg_hip_matrix* M, double* p)
+{
+    const int P = g_comm.nranks, r = g_comm.rank;
+    const int mine[2] = {M->send_lo, M->send_hi};
+    std::vector<int> sz(2 * P);
+    TRY(comm_allgather(mine, sz.data(), sizeof mine));
+    int S = 1;
+    for (int q = 0; q < P; q++) S = std::max(S, sz[2 * q] + sz[2 * q + 1]);
+    std::vector<double> out(S, 0.0), all((size_t)S * P);
+    int rc = 0;
+    if (M->send_lo) rc = d2h(M->stream, out.data(), p, sizeof(double) * M->send_lo);
+    if (!rc && M->send_hi) rc = d2h(M->stream, out.data() + M->send_lo, p + M->nrow - M->send_hi, sizeof(double) * M->send_hi);
+    TRY(comm_allgather(out.data(), all.data(), sizeof(double) * S));
+    if (rc) return rc;
+    if (r > 0 && M->ghost_lo) {  // rank r-1's last rows: its contribution after its first send_lo
+        if (sz[2 * (r - 1) + 1] != M->ghost_lo) return set_err(HPCCG_HIP_EPLAN, "host halo: rank %d sends %d rows, %d needed", r - 1, sz[2 * (r - 1) + 1], M->ghost_lo);
+        TRY(h2d(M, p - M->ghost_lo, all.data() + (size_t)S * (r - 1) + sz[2 * (r - 1)], sizeof(double) * M->ghost_lo));
+    }
+    if (r < P - 1 && M->ghost_hi) {  // rank r+1's first rows
+        if (sz[2 * (r + 1)] != M->ghost_hi) return set_err(HPCCG_HIP_EPLAN, "host halo: rank %d sends %d rows, %d needed", r + 1, sz[2 * (r + 1)], M->ghost_hi);
+        TRY(h2d(M, p + M->nrow, all.data() + (size_t)S * (r + 1), sizeof(double) * M->ghost_hi));
+    }
+    return 0;
+}
+
 // Gather plan over RCCL (exchange_externals.cpp:51-131): pack what each
 // requester needs, then one grouped send/recv per neighbour; the externals
 // arrive contiguously after the local rows.
 int enqueue_halo_gather(hpccg_hip_matrix* M, const CgArgs& a, double* p, bool prologue)
 {
     if (g_comm.nranks == 1) return 0;
+    if (!g_comm.comm) return need_rccl("the gather halo exchange");
     launch_cg_pack(a, M->d_send_idx, M->nsend, M->d_send_buf, prologue, M->stream);
     NCCL_TRY(ncclGroupStart());
     for (size_t i = 0; i < M->recv_rank.size(); i++)
@@ -1428,7 +1626,8 @@ int enqueue_halo_gather(hpccg_hip_matrix* M, const CgArgs& a, double* p, bool pr
 // MPI_Allreduce of one scalar (ddot.cpp:79-80): loc[which] -> g[which].
 int enqueue_allreduce(hpccg_hip_matrix* M, const CgArgs& a, int which)
 {
-    if (!a.allreduce || !g_comm.comm) return 0;
+    if (!a.allreduce) return 0;
+    if (!g_comm.comm) return comm_host() ? need_rccl("the scalar all-reduce") : 0;
     NCCL_TRY(ncclAllReduce(a.loc + which, a.g + which, 1, ncclFloat64, ncclSum, g_comm.comm, M->stream));
     return 0;
 }
@@ -1664,7 +1863,7 @@ int exch_rr_rhalo(const Ranks& R)
     }
     hpccg_hip_matrix* M = R.M[0];
     const CgArgs& a = R.a[0];
-    if (!g_comm.comm) return 0;
+    if (!g_comm.comm) return comm_host() ? need_rccl("r's plane exchange") : 0;
     // rhalo_group 1: the all-reduce and the planes in one RCCL group; 0: the
     // all-reduce, then the planes' group
     if (!M->rhalo_group) TRY(enqueue_allreduce(M, a, kRR));
@@ -2093,18 +2292,18 @@ int alloc_mbox(hpccg_hip_matrix* M)
     return 0;
 }
 
-// Collective over an RCCL job: every rank exports its mailbox (IPC handle),
-// all-gathers the handles and maps the others'. Every rank makes the same
-// RCCL calls whatever fails locally; *all_ok is the minimum over the ranks
-// (0: some rank could not take part, nothing is mapped).
+// Collective over the ranks of a job (RCCL or the host bootstrap): every rank
+// exports its mailbox (IPC handle), all-gathers the handles and maps the
+// others'. A local failure only clears this rank's flag -- every rank makes
+// the same collective calls whatever fails locally -- and
+// *all_ok is the minimum over the ranks (0: nothing is mapped).
 int map_peer_mailboxes(hpccg_hip_matrix* M, std::vector<double*>& table, int* all_ok)
 {
     const int nr = M->nranks;
     int ok = 1;
     if (!M->d_mbox) {
-        const int rc = alloc_mbox(M);
-        if (rc > 1 || rc < 0) return rc;
-        ok = rc == 0;
+        ok = alloc_mbox(M) == 0;
+        (void)hipGetLastError();
     }
     hipIpcMemHandle_t h;
     std::memset(&h, 0, sizeof h);
@@ -2113,19 +2312,12 @@ int map_peer_mailboxes(hpccg_hip_matrix* M, std::vector<double*>& table, int* al
         ok = 0;
     }
     const size_t hb = sizeof(h), rec = hb + 8;  // handle | ok flag (padded)
-    std::vector<unsigned char> mine(rec, 0);
+    std::vector<unsigned char> mine(rec, 0), all(rec * nr);
     std::memcpy(mine.data(), &h, hb);
     mine[hb] = (unsigned char)ok;
-    unsigned char* d = nullptr;
-    HIP_TRY(hipMalloc(&d, rec * (nr + 1)));
-    TRY(h2d(M, d + rec * nr, mine.data(), rec));
-    NCCL_TRY(ncclAllGather(d + rec * nr, d, rec, ncclUint8, g_comm.comm, M->stream));
-    std::vector<unsigned char> all(rec * nr);
-    TRY(d2h(M->stream, all.data(), d, rec * nr));
-    (void)hipFree(d);
-    int every = 1;
-    for (int q = 0; q < nr; q++) every = every && all[rec * q + hb] != 0;
-    int mapped = every;
+    TRY(comm_allgather(mine.data(), all.data(), rec));
+    int mapped = 1;
+    for (int q = 0; q < nr; q++) mapped = mapped && all[rec * q + hb] != 0;
     for (int q = 0; q < nr && mapped; q++) {
         if (q == M->rank) {
             table[q] = M->d_mbox;
@@ -2142,13 +2334,7 @@ int map_peer_mailboxes(hpccg_hip_matrix* M, std::vector<double*>& table, int* al
         M->ipc_opened.push_back(ptr);
         table[q] = static_cast<double*>(ptr);
     }
-    // every rank learns whether every rank mapped every mailbox
-    int* f = nullptr;
-    HIP_TRY(hipMalloc(&f, 2 * sizeof(int)));
-    TRY(h2d(M, f, &mapped, sizeof(int)));
-    NCCL_TRY(ncclAllReduce(f, f + 1, 1, ncclInt32, ncclMin, g_comm.comm, M->stream));
-    TRY(d2h(M->stream, all_ok, f + 1, sizeof(int)));
-    (void)hipFree(f);
+    TRY(comm_min(mapped, all_ok));  // every rank learns whether every rank mapped every mailbox
     if (!*all_ok) {
         for (void* ptr : M->ipc_opened) (void)hipIpcCloseMemHandle(ptr);
         M->ipc_opened.clear();
@@ -2158,8 +2344,8 @@ int map_peer_mailboxes(hpccg_hip_matrix* M, std::vector<double*>& table, int* al
 
 // The peer all-reduce's mailboxes and each rank's table of them (once per
 // rank count): an in-process group's members address each other's directly;
-// the ranks of an RCCL job exchange IPC handles of their mailboxes (one
-// all-gather over RCCL) and map them (hipIpcOpenMemHandle); the 1-rank
+// the ranks of a job exchange IPC handles of their mailboxes (one all-gather
+// over RCCL or the host bootstrap) and map them (hipIpcOpenMemHandle); the 1-rank
 // emulation addresses its own.
 int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
 {
@@ -2180,7 +2366,7 @@ int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
         for (int r = 0; r < P; r++)
             for (int q = 0; q < P; q++) tables[r][q] = Ms[q]->d_mbox;
     } else {  // one process per GPU: IPC handles through RCCL
-        if (!g_comm.comm) return set_err(HPCCG_HIP_EINVAL, "peer_allreduce: no communicator");
+        if (!comm_up()) return set_err(HPCCG_HIP_EINVAL, "peer_allreduce: no communicator");
         int all_ok = 0;
         TRY(map_peer_mailboxes(M, tables[0], &all_ok));
         if (!all_ok)
@@ -2199,25 +2385,26 @@ int ensure_peers(hpccg_hip_matrix* const* Ms, int P)
     return 0;
 }
 
-// Option peer_allreduce auto (-1, the default): at creation, every rank of an
-// RCCL job maps the others' mailboxes and runs kPeerTestRounds peer
-// all-reduces of both scalars through the kernels' own code (k_peer_selftest,
-// bounded waits), each checked bitwise on the host against the rank-ordered
-// sum; when every rank passes (RCCL min), the scalars are summed in the
-// kernels from then on and the iteration is one launch (fused update) plus
-// r's planes; otherwise RCCL's all-reduces stay. Collective: every rank
+// Option peer_allreduce auto (-1, the default): at creation, every rank of a
+// job maps the others' mailboxes and runs kPeerTestRounds peer all-reduces of
+// both scalars through the kernels' own code (k_peer_selftest, bounded waits),
+// each checked bitwise on the host against the rank-ordered sum; when every
+// rank passes, protocol_autotest runs the real iteration once more before the
+// scalars are summed in the kernels from then on (the iteration is one launch
+// with the fused update); otherwise RCCL's all-reduces stay (a host-bootstrapped
+// job has no such fallback: its matrices are refused). Collective: every rank
 // creates its matrix.
 constexpr int kPeerTestRounds = 64;
 
 int reset_dot_state(hpccg_hip_matrix* M);
 
-// Option halo_pull auto in an RCCL job (collective, at creation): every rank
-// exports its r buffer (IPC handle, the offset of local row 0, its row
-// count), maps its two neighbours', and tests a pull: each rank stores
+// Option halo_pull auto (collective, at creation): every rank exports its r
+// buffer (IPC handle of the allocation, the offset of local row 0 in it, its
+// row count), maps its two neighbours', and tests a pull: each rank stores
 // 0.5 g + 1 at every global row g of its first send_lo and last send_hi rows,
-// the ranks meet (an RCCL all-reduce), each pulls its ghost planes with the
-// kernels' own k_pull and checks them on the host. Used only when every rank
-// passes (RCCL min); otherwise r's planes stay on RCCL.
+// the ranks meet, each pulls its ghost planes with the kernels' own k_pull and
+// checks them on the host. Then protocol_autotest. Used only when every rank
+// passes; otherwise r's planes stay on RCCL.
 int pull_autotest(hpccg_hip_matrix* M)
 {
     M->pull_auto_ok = 0;
@@ -2225,24 +2412,20 @@ int pull_autotest(hpccg_hip_matrix* M)
     hipIpcMemHandle_t h;
     std::memset(&h, 0, sizeof h);
     int ok = M->d_rbuf != nullptr;
-    if (ok && hipIpcGetMemHandle(&h, M->d_rbuf) != hipSuccess) {
+    void* base = nullptr;  // the allocation the handle maps (canary mode: before d_rbuf)
+    size_t range = 0;
+    if (ok && (hipMemGetAddressRange(&base, &range, M->d_r) != hipSuccess || hipIpcGetMemHandle(&h, base) != hipSuccess)) {
         (void)hipGetLastError();
         ok = 0;
     }
     const size_t hb = sizeof h, rec = hb + 16;  // handle | offset of row 0 (B) | nrow | ok
-    std::vector<unsigned char> mine(rec, 0);
+    std::vector<unsigned char> mine(rec, 0), all(rec * nr);
     std::memcpy(mine.data(), &h, hb);
-    const long long off = (long long)((char*)M->d_r - (char*)M->d_rbuf);
+    const long long off = ok ? (long long)((char*)M->d_r - (char*)base) : 0;
     std::memcpy(mine.data() + hb, &off, 8);
     std::memcpy(mine.data() + hb + 8, &M->nrow, 4);
     std::memcpy(mine.data() + hb + 12, &ok, 4);
-    unsigned char* d = nullptr;
-    HIP_TRY(hipMalloc(&d, rec * (nr + 1)));
-    TRY(h2d(M, d + rec * nr, mine.data(), rec));
-    NCCL_TRY(ncclAllGather(d + rec * nr, d, rec, ncclUint8, g_comm.comm, M->stream));
-    std::vector<unsigned char> all(rec * nr);
-    TRY(d2h(M->stream, all.data(), d, rec * nr));
-    (void)hipFree(d);
+    TRY(comm_allgather(mine.data(), all.data(), rec));
     auto field = [&](int q, size_t at, void* out, size_t n) { std::memcpy(out, all.data() + rec * q + at, n); };
     int mapped = 1;
     for (int side = 0; side < 2 && mapped; side++) {
@@ -2263,52 +2446,45 @@ int pull_autotest(hpccg_hip_matrix* M)
             break;
         }
         M->ipc_r_opened.push_back(ptr);
-        double* base = reinterpret_cast<double*>(static_cast<char*>(ptr) + qoff);
+        double* rbase = reinterpret_cast<double*>(static_cast<char*>(ptr) + qoff);
         if (side == 0) {
-            M->d_pull_lo = base;
+            M->d_pull_lo = rbase;
             M->pull_lo_n = qn;
         } else {
-            M->d_pull_hi = base;
+            M->d_pull_hi = rbase;
         }
     }
-    int* f = nullptr;
-    HIP_TRY(hipMalloc(&f, 2 * sizeof(int)));
-    auto all_min = [&](int v, int* out) -> int {
-        TRY(h2d(M, f, &v, sizeof(int)));
-        NCCL_TRY(ncclAllReduce(f, f + 1, 1, ncclInt32, ncclMin, g_comm.comm, M->stream));
-        TRY(d2h(M->stream, out, f + 1, sizeof(int)));
-        return 0;
-    };
     int all_ok = 0;
-    TRY(all_min(mapped, &all_ok));
+    TRY(comm_min(mapped, &all_ok));
     if (all_ok) {
         // the test pattern in this rank's sent rows, then every rank pulls
         auto pattern = [&](long long g) { return 0.5 * (double)g + 1.0; };
+        int good = 1;
         std::vector<double> v;
         for (int i = 0; i < M->send_lo; i++) v.push_back(pattern((long long)M->start_row + i));
-        if (M->send_lo) TRY(h2d(M, M->d_r, v.data(), sizeof(double) * v.size()));
+        if (M->send_lo && h2d(M, M->d_r, v.data(), sizeof(double) * v.size())) good = 0;
         v.clear();
         for (int i = M->nrow - M->send_hi; i < M->nrow; i++) v.push_back(pattern((long long)M->start_row + i));
-        if (M->send_hi) TRY(h2d(M, M->d_r + M->nrow - M->send_hi, v.data(), sizeof(double) * v.size()));
+        if (M->send_hi && h2d(M, M->d_r + M->nrow - M->send_hi, v.data(), sizeof(double) * v.size())) good = 0;
         int dummy = 0;
-        TRY(all_min(1, &dummy));  // every rank's rows are in place
-        CgArgs a = make_args(M, M->d_b, M->d_x, 2, 0.0);
+        TRY(comm_min(1, &dummy));  // every rank's rows are in place
         const int lo = M->d_pull_lo ? M->ghost_lo : 0, hi = M->d_pull_hi ? M->ghost_hi : 0;
-        launch_pull(a, M->d_pull_lo ? M->d_pull_lo + M->pull_lo_n - lo : nullptr, M->d_r - M->ghost_lo, lo,
-                    M->d_pull_hi, M->d_r + M->nrow, hi, M->stream, true);
-        HIP_TRY(hipGetLastError());
         std::vector<double> gl(lo), gh(hi);
-        if (lo) TRY(d2h(M->stream, gl.data(), M->d_r - lo, sizeof(double) * lo));
-        if (hi) TRY(d2h(M->stream, gh.data(), M->d_r + M->nrow, sizeof(double) * hi));
-        int good = 1;
+        if (good) {
+            CgArgs a = make_args(M, M->d_b, M->d_x, 2, 0.0);
+            launch_pull(a, M->d_pull_lo ? M->d_pull_lo + M->pull_lo_n - lo : nullptr, M->d_r - M->ghost_lo, lo,
+                        M->d_pull_hi, M->d_r + M->nrow, hi, M->stream, true);
+            good = hipGetLastError() == hipSuccess;
+        }
+        if (good && lo && d2h(M->stream, gl.data(), M->d_r - lo, sizeof(double) * lo)) good = 0;
+        if (good && hi && d2h(M->stream, gh.data(), M->d_r + M->nrow, sizeof(double) * hi)) good = 0;
         for (int i = 0; i < lo && good; i++) good = gl[i] == pattern((long long)M->start_row - lo + i);
         for (int i = 0; i < hi && good; i++) good = gh[i] == pattern((long long)M->start_row + M->nrow + i);
-        TRY(all_min(good, &all_ok));
-        TRY(all_min(1, &dummy));  // no rank clears its rows while another still pulls
+        TRY(comm_min(good, &all_ok));
+        TRY(comm_min(1, &dummy));  // no rank clears its rows while another still pulls
         HIP_TRY(hipMemsetAsync(M->d_rbuf, 0, sizeof(double) * (size_t)M->pstride, M->stream));
         TRY(flush_stream(M));
     }
-    (void)hipFree(f);
     if (!all_ok) {
         for (void* ptr : M->ipc_r_opened) (void)hipIpcCloseMemHandle(ptr);
         M->ipc_r_opened.clear();
@@ -2328,44 +2504,120 @@ int peer_autotest(hpccg_hip_matrix* M)
     int all_ok = 0;
     TRY(map_peer_mailboxes(M, table, &all_ok));
     if (!all_ok) return 0;
-    if (!M->d_peers) HIP_TRY(hipMalloc(&M->d_peers, sizeof(double*) * kMaxGroupRanks));
-    TRY(h2d(M, M->d_peers, table.data(), sizeof(double*) * kMaxGroupRanks));
-    M->peers_for = nr;
-    CgArgs a = make_args(M, M->d_b, M->d_x, 2, 0.0);
-    a.peer_ar = 1;
-    a.prank = M->rank;
-    a.pranks = nr;
-    a.mbox = M->d_mbox;
-    a.peers = M->d_peers;
-    const long long budget = std::min<long long>(200000000LL, M->spin_us * 100);  // at most 2 s
-    launch_rearm(M->d_kst, M->d_partial, (int)M->npartial, M->d_tickets, M->ntickets, (int)budget, M->stream);
+    int ok = 1;
+    if (!M->d_peers && hipMalloc(&M->d_peers, sizeof(double*) * kMaxGroupRanks) != hipSuccess) ok = 0;
+    if (ok && h2d(M, M->d_peers, table.data(), sizeof(double*) * kMaxGroupRanks)) ok = 0;
     double* out = nullptr;
-    HIP_TRY(hipMalloc(&out, sizeof(double) * 2 * kPeerTestRounds));
-    launch_peer_selftest(a, kPeerTestRounds, out, M->stream);
-    HIP_TRY(hipGetLastError());
+    if (ok && hipMalloc(&out, sizeof(double) * 2 * kPeerTestRounds) != hipSuccess) ok = 0;
     std::vector<double> got(2 * kPeerTestRounds);
-    int err[kErrWords];
-    TRY(d2h(M->stream, got.data(), out, sizeof(double) * got.size()));
-    TRY(d2h(M->stream, err, M->d_kst + kErrBase, sizeof err));
-    (void)hipFree(out);
-    int ok = err[0] == kErrNone;
+    int err[kErrWords] = {kErrNone};
+    if (ok) {  // (a rank that cannot run it leaves the others' waits to expire: they fail too)
+        M->peers_for = nr;
+        CgArgs a = make_args(M, M->d_b, M->d_x, 2, 0.0);
+        a.peer_ar = 1;
+        a.prank = M->rank;
+        a.pranks = nr;
+        a.mbox = M->d_mbox;
+        a.peers = M->d_peers;
+        const long long budget = std::min<long long>(200000000LL, M->spin_us * 100);  // at most 2 s
+        launch_rearm(M->d_kst, M->d_partial, (int)M->npartial, M->d_tickets, M->ntickets, (int)budget, M->stream);
+        launch_peer_selftest(a, kPeerTestRounds, out, M->stream);
+        ok = hipGetLastError() == hipSuccess;
+        if (ok && d2h(M->stream, got.data(), out, sizeof(double) * got.size())) ok = 0;
+        if (ok && d2h(M->stream, err, M->d_kst + kErrBase, sizeof err)) ok = 0;
+    }
+    (void)hipGetLastError();
+    if (out) (void)hipFree(out);
+    ok = ok && err[0] == kErrNone;
     for (int k = 0; k < kPeerTestRounds && ok; k++)
         for (int which = 0; which < 2; which++) {
             double want = 0.0;  // k_peer_selftest's contributions, summed in rank order
             for (int q = 0; q < nr; q++) want += (double)(q + 1) + 0.5 * k + 0.25 * which;
             if (std::memcmp(&want, &got[2 * k + which], sizeof want) != 0) ok = 0;
         }
-    int* f = nullptr;
-    HIP_TRY(hipMalloc(&f, 2 * sizeof(int)));
-    TRY(h2d(M, f, &ok, sizeof(int)));
-    NCCL_TRY(ncclAllReduce(f, f + 1, 1, ncclInt32, ncclMin, g_comm.comm, M->stream));
-    TRY(d2h(M->stream, &all_ok, f + 1, sizeof(int)));
-    (void)hipFree(f);
-    if (!all_ok) {  // a rank's waits may have given up: every mailbox empty again
-        TRY(reset_dot_state(M));
-        return 0;
+    TRY(comm_min(ok, &all_ok));
+    TRY(reset_dot_state(M));  // the test's slots, and a rank's waits may have given up: every mailbox empty
+    TRY(comm_min(1, &ok));    // no rank's next kernel stores into a mailbox before its owner has reset it
+    M->peer_auto_ok = all_ok;
+    return 0;
+}
+
+int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, double* const* x_dev, int max_iter,
+                double tol, int* niters_out, double* normr_out, double* times, int print);
+
+// The production protocol itself, after the peer and pull tests
+// passed on every rank: a short solve of this matrix (kProtoIters iterations,
+// a synthetic b) launch for launch as the solves will run it -- the peer
+// all-reduce inside the kernels, r's boundary rows stored write-through and
+// drained before the r.r partial, the neighbours' rows pulled by the
+// iteration's last launch -- against the same solve with r's planes moved by
+// RCCL (a host-bootstrapped job: by k_pull launches before each SpMV). Both
+// must give the same bits (the scalars are summed the same way in both, only
+// the plane transport differs), and every rank's trace must be every other
+// rank's (all sum the same global dots). The auto modes stay on only if every
+// rank passes; otherwise both fall back to RCCL.
+constexpr int kProtoIters = 12;
+
+int protocol_autotest(hpccg_hip_matrix* M, int* all_ok)
+{
+    *all_ok = 0;
+    int ok = 1;
+    const size_t np = M->npad;
+    double* scratch = nullptr;  // b | x, padded like the solver's own vectors
+    if (hipMalloc(&scratch, 2 * sizeof(double) * np) != hipSuccess) {
+        (void)hipGetLastError();
+        scratch = nullptr;
+        ok = 0;
     }
-    M->peer_auto_ok = 1;
+    std::vector<double> hb(np, 0.0);
+    for (int i = 0; i < M->nrow; i++) hb[i] = 1.0 + (double)(((long long)M->start_row + i) % 13) * 0.125;
+    if (ok && h2d(M, scratch, hb.data(), sizeof(double) * np)) ok = 0;
+    struct Run {
+        int it = -1;
+        double nr = 0.0;
+        std::vector<double> trace, x;
+    } run[2];
+    const int hp0 = M->halo_pull, ug0 = M->use_graph;
+    for (int v = 0; v < 2; v++) {  // every rank runs both solves: their RCCL calls and error exchanges are collective
+        M->halo_pull = v == 0 ? 2 : (comm_host() ? 1 : 0);
+        M->use_graph = 0;
+        const double* b = scratch;
+        double* x = scratch ? scratch + np : nullptr;
+        int rc = 0;
+        if (!scratch) {
+            // no buffers: still take part in the collective steps of a solve
+            // with the matrix's own vectors (its result is not compared)
+            b = M->d_b;
+            x = M->d_x;
+        }
+        if (hipMemsetAsync(x, 0, sizeof(double) * np, M->stream) != hipSuccess) ok = 0;
+        rc = solve_ranks(&M, 1, &b, &x, kProtoIters + 1, 0.0, &run[v].it, &run[v].nr, nullptr, 0);
+        if (rc) ok = 0;
+        run[v].trace = M->trace;
+        run[v].x.assign(M->nrow, 0.0);
+        if (rc == 0 && d2h(M->stream, run[v].x.data(), x, sizeof(double) * M->nrow)) ok = 0;
+    }
+    (void)hipGetLastError();
+    M->halo_pull = hp0;
+    M->use_graph = ug0;
+    M->trace.clear();
+    M->last_niters = 0;
+    if (scratch) (void)hipFree(scratch);
+    ok = ok && run[0].it == kProtoIters && run[1].it == run[0].it &&
+         std::memcmp(&run[0].nr, &run[1].nr, sizeof(double)) == 0 && run[0].trace.size() == run[1].trace.size() &&
+         std::memcmp(run[0].trace.data(), run[1].trace.data(), sizeof(double) * run[0].trace.size()) == 0 &&
+         std::memcmp(run[0].x.data(), run[1].x.data(), sizeof(double) * M->nrow) == 0;
+    // every rank's trace is every other rank's
+    unsigned long long hsh = 0x9e3779b97f4a7c15ULL;
+    for (double t : run[0].trace) {
+        unsigned long long bits;
+        std::memcpy(&bits, &t, 8);
+        hsh = (hsh ^ bits) * 0x100000001b3ULL;
+    }
+    std::vector<unsigned long long> hs(M->nranks);
+    TRY(comm_allgather(&hsh, hs.data(), sizeof hsh));
+    for (unsigned long long q : hs) ok = ok && q == hsh;
+    TRY(comm_min(ok, all_ok));
     return 0;
 }
 
@@ -2406,7 +2658,18 @@ int check_device_error(hpccg_hip_matrix* const* Ms, int P, const int* err0)
         if (e[0] != kErrNone || (P == 1 && e[kErrAllRanks] != kErrNone)) bad_rank = r;
     }
     if (bad_rank < 0) return 0;
-    for (int r = 0; r < P; r++) TRY(reset_dot_state(Ms[r]));
+    for (int r = 0; r < P; r++) {
+        TRY(reset_dot_state(Ms[r]));
+        Ms[r]->solve_dirty = 0;  // reset here (a second reset at the next solve's start could empty a slot a
+                                 // faster rank has already filled for it)
+    }
+    // a job's ranks all come here (the code is all-reduced): none starts its
+    // next solve -- whose first contributions land in the others' mailboxes --
+    // before every rank has emptied its own
+    if (P == 1 && Ms[0]->nranks > 1 && !Ms[0]->in_group && comm_up()) {
+        int dummy = 0;
+        TRY(comm_min(1, &dummy));
+    }
     HIP_TRY(hipSetDevice(Ms[0]->device));
     const int rank = Ms[bad_rank]->rank;
     if (e[0] == kErrNone)
@@ -2483,6 +2746,14 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     }
     if (multi_of(M) && pull_of(M))
         for (int r = 0; r < P; r++) TRY(pull_plan(Ms, av.data(), P, r));
+    // a host-bootstrapped job has no RCCL: the iteration must make no collective
+    // call (the scalars summed in the kernels, r's planes pulled). Every rank
+    // holds the same options unless the caller set them differently
+    if (P == 1 && M->nranks > 1 && comm_host() && (av[0].allreduce || !av[0].rhalo || !pull_of(M)))
+        return set_err(HPCCG_HIP_EINVAL,
+                       "host-bootstrapped communicator: this solve would need RCCL (peer_allreduce %d, rhalo %d, "
+                       "halo_pull %d): leave peer_allreduce, halo_pull, fuse_p and the kernel on auto",
+                       av[0].peer_ar, av[0].rhalo, pull_of(M) ? 1 : 0);
     // group fold: RCCL-style group sums (no peer all-reduce), both dots folded,
     // no overlapped halo (its SpMV runs as two launches)
     if (P > 1 && Ms[0]->group_fold != 0 && av[0].allreduce && fold_of(av[0], kPAP) && fold_of(av[0], kRR) &&
@@ -2625,6 +2896,14 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
                                M->stream));
     TRY(wait_matrix(M));
     const auto t_end = std::chrono::steady_clock::now();
+    // a host-bootstrapped job: every rank learns whether any rank gave up a wait
+    // (after the wait: no rank starts its next solve before every rank's last
+    // kernels have ended, so no mailbox slot of this solve is written late)
+    if (P == 1 && M->nranks > 1 && !M->in_group && comm_host()) {
+        std::vector<int> codes(M->nranks);
+        TRY(comm_allgather(kst + kErrBase, codes.data(), sizeof(int)));
+        kst[kErrBase + kErrAllRanks] = *std::max_element(codes.begin(), codes.end());
+    }
     TRY(check_device_error(Ms, P, kst + kErrBase));
     // (the fused update keeps k in kst[0] / kst[2] by parity: the later one is the count)
     const int niters = std::max(0, (av[0].fupd ? std::max(kst[0], kst[2]) : kst[0]) - 1);
@@ -2672,6 +2951,14 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     *niters_out = niters;
     *normr_out = normr;
     for (int r = 0; r < P; r++) Ms[r]->solve_dirty = 0;
+    if (canary_on()) {  // debug mode: no store of this solve ran past a buffer
+        std::string rep;
+        const int bad = canary_check(&rep);
+        if (bad) {
+            std::fprintf(stderr, "hpccg_hip canary: %d tripped after a solve\n%s", bad, rep.c_str());
+            return set_err(HPCCG_HIP_EHIP, "canary: %d tripped after a solve: %s", bad, rep.c_str());
+        }
+    }
     return 0;
 }
 
@@ -2698,11 +2985,41 @@ int finish_matrix(hpccg_hip_matrix* M)
             g_place_tries > 0 ? g_place_tries : ((double)M->a_slots * 8.0 >= kPlaceMinBytes ? kPlaceAuto : 0);
         if (tries) TRY(hpccg_hip_probe_placement(M, tries));
     }
-    // an RCCL job's ranks (collective, after the probe: it may move r): the
-    // peer all-reduce and the halo pull self-tests
-    if (M->nranks > 1 && !M->in_group && g_comm.comm) {
-        if (M->peer_ar < 0 && !std::getenv("HPCCG_NO_PEER_AUTO")) TRY(peer_autotest(M));
-        if (M->halo_pull != 0 && !M->general && !std::getenv("HPCCG_NO_PULL_AUTO")) TRY(pull_autotest(M));
+    // a job's ranks (collective, after the probe: it may move r): the peer
+    // all-reduce and the halo pull self-tests, then the production protocol
+    // (protocol_autotest); every rank reaches the same verdicts
+    if (M->nranks > 1 && !M->in_group && comm_up()) {
+        const bool host = comm_host();
+        // a host-bootstrapped job has no RCCL to fall back to: the r-halo
+        // iteration (z-slab plan, SELL-512-A kernel with the p update fused) on
+        // every rank, or the matrix is refused on every rank
+        int can = 1;
+        if (host) TRY(comm_min(rhalo_of(M) ? 1 : 0, &can));
+        if (host && !can)
+            return set_err(HPCCG_HIP_EPLAN, "host-bootstrapped communicator: a rank's matrix cannot run the r-halo "
+                                            "iteration (z-slab plan and a SELL-512-A image are needed; RCCL serves "
+                                            "the others)");
+        const bool peer = M->peer_ar < 0 && (host || !std::getenv("HPCCG_NO_PEER_AUTO"));
+        const bool pull = M->halo_pull != 0 && !M->general && (host || !std::getenv("HPCCG_NO_PULL_AUTO"));
+        if (peer) TRY(peer_autotest(M));
+        if (pull) TRY(pull_autotest(M));
+        M->proto_auto_ok = 0;
+        if (peer && pull && M->peer_auto_ok && M->pull_auto_ok) {  // (the verdicts are every rank's)
+            int ok = 0;
+            TRY(protocol_autotest(M, &ok));
+            M->proto_auto_ok = ok;
+            if (!ok) {  // both fall back to RCCL
+                M->peer_auto_ok = M->pull_auto_ok = 0;
+                for (void* ptr : M->ipc_r_opened) (void)hipIpcCloseMemHandle(ptr);
+                M->ipc_r_opened.clear();
+                M->d_pull_lo = M->d_pull_hi = nullptr;
+            }
+        }
+        if (host && !(M->peer_auto_ok && M->pull_auto_ok))
+            return set_err(HPCCG_HIP_EPLAN, "host-bootstrapped communicator: the %s self-test failed on some rank "
+                                            "(peer %d, pull %d, protocol %d); this transport needs all three",
+                           !M->peer_auto_ok ? "peer all-reduce" : !M->pull_auto_ok ? "halo pull" : "protocol",
+                           M->peer_auto_ok, M->pull_auto_ok, M->proto_auto_ok);
     }
     return 0;
 }
@@ -2988,10 +3305,7 @@ int hpccg_hip_comm_unique_id(unsigned char id_out[128])
 int hpccg_hip_comm_init(const unsigned char id[128], int nranks, int rank)
 {
     if (nranks < 1 || rank < 0 || rank >= nranks) return set_err(HPCCG_HIP_EINVAL, "bad nranks/rank");
-    if (g_comm.comm) {
-        ncclCommDestroy(g_comm.comm);
-        g_comm = Comm();
-    }
+    comm_reset();
     // a 1-rank communicator is created too (bootstrap + RCCL check on one GPU);
     // the solver still takes its single-rank path when nranks == 1
     ncclUniqueId uid;
@@ -3002,10 +3316,34 @@ int hpccg_hip_comm_init(const unsigned char id[128], int nranks, int rank)
     return 0;
 }
 
+int hpccg_hip_comm_init_host(int nranks, int rank, hpccg_hip_allgather_fn allgather, void* ctx)
+{
+    if (nranks < 1 || rank < 0 || rank >= nranks || !allgather)
+        return set_err(HPCCG_HIP_EINVAL, "bad nranks/rank or no all-gather callback");
+    comm_reset();
+    g_comm.nranks = nranks;
+    g_comm.rank = rank;
+    g_comm.ag = allgather;
+    g_comm.ag_ctx = ctx;
+    // the callback is collective: every rank must see every rank in order
+    std::vector<int> all(nranks, -1);
+    int rc = comm_allgather(&rank, all.data(), sizeof rank);
+    for (int q = 0; q < nranks && rc == 0; q++)
+        if (all[q] != q) rc = set_err(HPCCG_HIP_EINVAL, "host all-gather: slot %d holds rank %d", q, all[q]);
+    if (rc) comm_reset();
+    return rc;
+}
+
 int hpccg_hip_comm_destroy(void)
 {
-    if (g_comm.comm) ncclCommDestroy(g_comm.comm);
-    g_comm = Comm();
+    comm_reset();
+    return 0;
+}
+
+int hpccg_hip_comm_mode(int* mode)
+{
+    if (!mode) return set_err(HPCCG_HIP_EINVAL, "mode is NULL");
+    *mode = g_comm.comm ? 1 : (g_comm.ag ? 2 : 0);
     return 0;
 }
 
@@ -3019,6 +3357,19 @@ int hpccg_hip_comm_size(int* nranks, int* rank)
 int hpccg_hip_comm_allreduce_host(double* vals, int n, int op)
 {
     if (!vals || n < 0 || op < 0 || op > 2) return set_err(HPCCG_HIP_EINVAL, "bad argument");
+    if (comm_host() && n > 0) {  // every rank's values, reduced in rank order
+        std::vector<double> all((size_t)n * g_comm.nranks);
+        TRY(comm_allgather(vals, all.data(), sizeof(double) * n));
+        for (int i = 0; i < n; i++) {
+            double v = op == 0 ? 0.0 : all[i];
+            for (int q = 0; q < g_comm.nranks; q++) {
+                const double w = all[(size_t)q * n + i];
+                v = op == 0 ? v + w : op == 1 ? std::min(v, w) : std::max(v, w);
+            }
+            vals[i] = v;
+        }
+        return 0;
+    }
     if (!g_comm.comm || n == 0) return 0;
     double* d = nullptr;
     hipStream_t s = nullptr;
@@ -3495,6 +3846,9 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "nt")) *value = image_big(M) ? 1 : 0;
     else if (!std::strcmp(key, "device_bytes")) *value = M->bytes;
     else if (!std::strcmp(key, "placement_pick")) *value = M->place_pick;
+    else if (!std::strcmp(key, "peer_auto_ok")) *value = M->peer_auto_ok;
+    else if (!std::strcmp(key, "pull_auto_ok")) *value = M->pull_auto_ok;
+    else if (!std::strcmp(key, "proto_auto_ok")) *value = M->proto_auto_ok;
     else return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
     return 0;
 }
@@ -3611,15 +3965,20 @@ int probe_time(hpccg_hip_matrix* M, const double* b, double* x, double* us)
     return 0;
 }
 
-// The probe's candidates are plain allocations (big_malloc's reason). The
-// diagnostics of its side effects (tools/diag_carry.py) can ask for others:
+// The probe's candidates are plain allocations (big_malloc's reason). Only
+// the diagnostics variant of the library (-DHPCCG_DIAG_CONTIG,
+// tools/build_variant.sh) lets tools/diag_carry.py ask for others:
 // HPCCG_PROBE_ALLOC = hipExtMallocWithFlags flags (4: contiguous -- this
-// corrupts other buffers, diagnostics only), HPCCG_PROBE_KEEP=1 holds the
-// dropped candidates for the life of the process instead of freeing them.
+// corrupted other buffers). HPCCG_PROBE_KEEP=1 holds the dropped candidates
+// for the life of the process instead of freeing them.
 static unsigned probe_alloc_flags()
 {
+#ifdef HPCCG_DIAG_CONTIG
     const char* e = std::getenv("HPCCG_PROBE_ALLOC");
     return e && *e ? (unsigned)std::atoi(e) : hipDeviceMallocDefault;
+#else
+    return hipDeviceMallocDefault;
+#endif
 }
 static bool probe_keep()
 {
@@ -3681,7 +4040,7 @@ int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
             size_t fr = 0, tot = 0;
             if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < bytes + (size_t(8) << 30)) break;  // headroom
             double* q = nullptr;
-            if (hipExtMallocWithFlags(reinterpret_cast<void**>(&q), bytes, probe_alloc_flags()) != hipSuccess)
+            if (big_malloc(reinterpret_cast<void**>(&q), bytes, probe_alloc_flags()) != hipSuccess)
                 break;
             cand.push_back(q);
             const hipError_t e = phase == 0 ? hipMemcpyAsync(q, cand[0], bytes, hipMemcpyDeviceToDevice, M->stream)
@@ -3707,7 +4066,7 @@ int hpccg_hip_probe_placement(hpccg_hip_matrix* M, int tries)
                 if (probe_keep())
                     g_probe_held.push_back(cand[i]);  // diagnostics: never handed out again
                 else
-                    (void)hipFree(cand[i]);
+                    big_free(cand[i]);
             }
         if (phase > 0 && hipMemsetAsync(cand[best], 0, bytes, M->stream) != hipSuccess && !rc)
             rc = set_err(HPCCG_HIP_EHIP, "placement probe: hipMemsetAsync failed");  // the solves' values
@@ -3772,17 +4131,28 @@ int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which, unsigned long long* v
     default: return set_err(HPCCG_HIP_EINVAL, "which must be 0..4");
     }
     if (mode < 0 || mode > 6) return set_err(HPCCG_HIP_EINVAL, "mode must be 0..6");
+#ifndef HPCCG_DIAG_CONTIG
+    if (mode == 1)
+        return set_err(HPCCG_HIP_EINVAL, "mode 1 (physically contiguous memory) exists only in the diagnostics "
+                                         "variant of the library (-DHPCCG_DIAG_CONTIG): it corrupted other buffers");
+#endif
     if (!*buf) return set_err(HPCCG_HIP_EINVAL, "buffer %d not allocated", which);
+    // the neighbours pull from this r through their IPC mappings of it (halo_pull):
+    // a moved r would leave them reading the old buffer
+    if (which == 2 && M->pull_auto_ok)
+        return set_err(HPCCG_HIP_EINVAL, "r cannot move: the neighbours have it mapped (halo_pull)");
     double* nb = nullptr;
     const size_t bytes = sizeof(double) * n;
     if (mode == 0) {
         HIP_TRY(big_malloc(reinterpret_cast<void**>(&nb), bytes));
+#ifdef HPCCG_DIAG_CONTIG
     } else if (mode == 1) {
-        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocContiguous));
+        HIP_TRY(big_malloc(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocContiguous));
+#endif
     } else if (mode == 5) {  // fine-grained (coherent) device memory
-        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocFinegrained));
+        HIP_TRY(big_malloc(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocFinegrained));
     } else if (mode == 6) {
-        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocUncached));
+        HIP_TRY(big_malloc(reinterpret_cast<void**>(&nb), bytes, hipDeviceMallocUncached));
     } else {  // VMM at 2 MB, 64 MB or 1 GB virtual alignment
         const size_t align = mode == 2 ? (size_t(1) << 21) : mode == 3 ? (size_t(1) << 26) : (size_t(1) << 30);
         TRY(vmm_alloc(M, bytes, align, &nb));
@@ -3798,6 +4168,15 @@ int hpccg_hip_diag_realloc(hpccg_hip_matrix* M, int which, unsigned long long* v
     if (which == 2) M->d_r = M->d_rbuf + roff;
     if (va_out) *va_out = reinterpret_cast<unsigned long long>(nb);
     return 0;  // the graph cache compares kernel arguments: the next solve re-captures
+}
+
+int hpccg_hip_diag_canary_check(int* enabled, char* report, int cap)
+{
+    if (enabled) *enabled = canary_on() ? 1 : 0;
+    std::string rep;
+    const int bad = canary_check(&rep);
+    if (report && cap > 0) std::snprintf(report, (size_t)cap, "%s", rep.c_str());
+    return bad;
 }
 
 int hpccg_hip_diag_timeline(const hpccg_hip_matrix* M, unsigned long long* out, int cap)
@@ -3855,6 +4234,8 @@ int hpccg_hip_sparsemv(hpccg_hip_matrix* M, const double* x_dev, double* y_dev)
     CgArgs a = make_args(M, nullptr, nullptr, 1, 0.0);
     if (M->general)
         TRY(enqueue_halo_gather(M, a, M->d_p, true));
+    else if (comm_host() && g_comm.nranks > 1)
+        TRY(host_halo(M, M->d_p));
     else
         TRY(enqueue_halo(M, M->d_p, M->stream));
     if (M->has_sell && (M->kernel == kSpmvSell || !M->has_a)) {
@@ -3880,6 +4261,16 @@ int hpccg_hip_ddot(int n, const double* x_dev, const double* y_dev, double* resu
     TRY(scratch_for(nparts));
     launch_ddot(n, x_dev, y_dev, g_scratch.partial, nparts, g_scratch.out, g_scratch.s);
     HIP_TRY(hipGetLastError());
+    if (comm_host() && g_comm.nranks > 1) {  // every rank's local sum, added in rank order from 0.0
+        double loc = 0.0;
+        TRY(d2h(g_scratch.s, &loc, g_scratch.out, sizeof(double)));
+        std::vector<double> all(g_comm.nranks);
+        TRY(comm_allgather(&loc, all.data(), sizeof loc));
+        double v = 0.0;
+        for (double w : all) v += w;
+        *result = v;
+        return 0;
+    }
     if (g_comm.nranks > 1)
         NCCL_TRY(ncclAllReduce(g_scratch.out, g_scratch.out + 1, 1, ncclFloat64, ncclSum, g_comm.comm, g_scratch.s));
     return d2h(g_scratch.s, result, g_scratch.out + (g_comm.nranks > 1 ? 1 : 0), sizeof(double));

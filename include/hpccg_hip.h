@@ -51,8 +51,27 @@ int hpccg_hip_set_device(int device);       /* one GPU per rank/process */
  *      library runs single-GPU (nranks = 1). ---------------------------- */
 int hpccg_hip_comm_unique_id(unsigned char id_out[128]);
 int hpccg_hip_comm_init(const unsigned char id[128], int nranks, int rank);
+/* Host-bootstrapped communicator (replaces MPI_Init / MPI_COMM_WORLD's setup
+ * role, main.cpp:131-132 and make_local_matrix.cpp:185-201; no RCCL): the
+ * ranks' setup exchanges (the halo plan's all-gather, the IPC handles of the
+ * peer mailboxes and of r, the self-tests' verdicts) go through the caller's
+ * all-gather -- allgather(send, recv, bytes, ctx) must place every rank's
+ * `bytes` bytes into recv in rank order and return 0 -- e.g. gloo from
+ * torch.distributed. The CG iteration then makes no collective call at all:
+ * the two scalars are summed inside the kernels through IPC-mapped mailboxes
+ * (ddot.cpp:75-85) and each rank pulls its z-slab ghost planes of r from its
+ * neighbours' memory (exchange_externals.cpp:51-131). Several ranks may share
+ * one GPU (RCCL refuses that). Matrix creation is collective and fails on
+ * every rank (HPCCG_HIP_EPLAN) when that transport is not available: the
+ * gather halo plan, a matrix without a SELL-512-A image, or a self-test that
+ * failed on any rank. The kernel-level sparsemv and ddot exchange through the
+ * callback. hpccg_hip_comm_destroy ends it. */
+typedef int (*hpccg_hip_allgather_fn)(const void* send, void* recv, unsigned long long bytes, void* ctx);
+int hpccg_hip_comm_init_host(int nranks, int rank, hpccg_hip_allgather_fn allgather, void* ctx);
 int hpccg_hip_comm_destroy(void);
 int hpccg_hip_comm_size(int* nranks, int* rank);
+/* The communicator in use: 0 none (one rank), 1 RCCL, 2 host-bootstrapped. */
+int hpccg_hip_comm_mode(int* mode);
 /* Host-value all-reduce over the communicator (main.cpp:206-208,
  * compute_residual.cpp:73): op 0 = sum, 1 = min, 2 = max. In place. */
 int hpccg_hip_comm_allreduce_host(double* vals, int n, int op);
@@ -286,6 +305,15 @@ int hpccg_hip_diag_placement(const hpccg_hip_matrix* M, double* us_out, int cap)
  * rows (cap x 8 words); returns the row count. Replaces nothing in the
  * reference (its TICK/TOCK classes are per kernel). */
 int hpccg_hip_diag_timeline(const hpccg_hip_matrix* M, unsigned long long* out, int cap);
+/* Debug (canary mode: HPCCG_CANARY=1 in the environment when the library
+ * first allocates): every matrix buffer is allocated with a 64 KB canary of
+ * a NaN pattern no kernel stores before and after it, and every solve checks
+ * every canary of the process when it ends (HPCCG_HIP_EHIP naming the buffer
+ * and the byte range on a trip). This checks them now (device-wide sync
+ * first): returns the number of tripped canaries and describes up to 8 in
+ * report; *enabled = whether canary mode is on. Replaces nothing in the
+ * reference (its solver touches only its own work vectors, HPCCG.cpp:327-329). */
+int hpccg_hip_diag_canary_check(int* enabled, char* report, int cap);
 /* Diagnostic (host only, no GPU): the folded dot completion's plan for a
  * launch of `units` units (spu = 1 slice or 2 slices each) on `grid` blocks
  * dealt over the 8 XCDs (rev: the update's reversed order): for each group of

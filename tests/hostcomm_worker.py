@@ -1,0 +1,157 @@
+"""One rank of the host-bootstrapped 2-process job (tests/test_gpu_hostcomm.py):
+two processes share GPU 0, torch.distributed (gloo) carries the setup
+exchanges through hpccg_hip_comm_init_host, and the CG iteration runs the
+default multi-rank transport for real between the processes -- IPC-mapped
+peer mailboxes (the in-kernel all-reduce of ddot.cpp:75-85) and r's ghost
+planes pulled from the other process's memory (exchange_externals.cpp:
+51-131). Writes <out>/rank<r>.json (+ .npy vectors) for the test to check.
+
+    python -m torch.distributed.run --nproc-per-node 2 tests/hostcomm_worker.py <out_dir>
+"""
+import json
+import os
+import sys
+import time
+import traceback
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from conftest import RTRANS_RTOL_MULTI, check_final, check_trace, kat2_rr0, load_pkg, solve_case, unhex  # noqa: E402
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+    out_dir = sys.argv[1]
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    hp = load_pkg()
+    dev = int(os.environ.get("LOCAL_RANK", rank)) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    hp.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    hp.comm_init_host(world, rank)
+    res = {"rank": rank, "device": dev, "comm_mode": hp.comm_mode(), "pci": hp.runtime_info()["pci_bus_id"]}
+    with open(os.path.join(HERE, "golden", "golden.json")) as f:
+        golden = json.load(f)
+
+    def solve(M, b, max_iter=500, tol=0.0):
+        n = M.info()["nrow"]
+        x = torch.zeros(n, dtype=torch.float64, device=f"cuda:{dev}")
+        _, it, nr, times = hp.HPCCG(M, b, x, max_iter=max_iter, tolerance=tol, device=True)
+        return it, nr, M.last_trace().copy(), x.cpu().numpy(), times
+
+    def transport(M):
+        return {k: M.get_option(k) for k in ("peer_allreduce", "halo_pull", "rhalo", "fuse_update", "spmv_kernel",
+                                             "peer_auto_ok", "pull_auto_ok", "proto_auto_ok", "graph_used")}
+
+    def case(name, fn):
+        t0 = time.time()
+        try:
+            r = fn()
+            r["ok"] = True
+        except Exception as e:
+            r = {"ok": False, "error": f"{type(e).__name__}: {e}", "tb": traceback.format_exc()[-3000:]}
+        r["seconds"] = round(time.time() - t0, 3)
+        res[name] = r
+        dist.barrier()
+
+    # 1-2: the reference's 2-rank goldens (the z-stacked global problem solved by
+    # the unmodified reference HPCCG(), tests/golden/make_golden.py)
+    def golden_case(gname):
+        c = solve_case(golden, gname)
+        assert c["ranks"] == world
+        M = hp.Matrix.generate(c["nx"], c["ny"], c["nz"], use_7pt=c["use_7pt"])
+        b, _, _ = M.vectors()
+        it, nr, tr, x, times = solve(M, b)
+        out = {"transport": transport(M), "niters": it, "normr": nr.hex(), "trace0": tr[0].hex()}
+        ref_tr = [unhex(t) for t in c["trace_normr"]]
+        rr = c["runs"]["500"]
+        assert tr[0] == ref_tr[0]
+        out["checked"] = check_trace(tr, ref_tr, RTRANS_RTOL_MULTI)
+        assert out["checked"] >= 5
+        check_final(it, nr, tr, rr["niters"], unhex(rr["normr"]), ref_tr, 500)
+        out["x_err"] = float(np.max(np.abs(x - 1.0)))
+        assert out["x_err"] <= 1e-12
+        out["halo_s"], out["allreduce_s"] = times[5], times[4]
+        # the same solve with k_pull launches, and eagerly: the same bits
+        same = (it, nr, tr.tobytes(), x.tobytes())
+        M.set_option("halo_pull", 1)
+        it1, nr1, tr1, x1, _ = solve(M, b)
+        out["kpull_same"] = (it1, nr1, tr1.tobytes(), x1.tobytes()) == same
+        M.set_option("halo_pull", -1)
+        M.set_option("use_graph", 0)
+        it2, nr2, tr2, x2, _ = solve(M, b)
+        out["eager_same"] = (it2, nr2, tr2.tobytes(), x2.tobytes()) == same
+        M.close()
+        return out
+
+    case("golden27", lambda: golden_case("27pt_8x8x8_x2ranks"))
+    case("golden7", lambda: golden_case("7pt_12x10x8_x2ranks"))
+
+    # 3-4: 2 x 64^3, bits for the in-process group comparison; then one rank
+    # withholds a p.Ap partial: both ranks must give up within the spin budget
+    # (the other one waits for the missing peer contribution), and the next
+    # solve must be bitwise the first
+    state = {}
+
+    def bits64():
+        M = hp.Matrix.generate(64, 64, 64)
+        b, _, _ = M.vectors()
+        it, nr, tr, x, _ = solve(M, b)
+        np.save(os.path.join(out_dir, f"x64_rank{rank}.npy"), x)
+        np.save(os.path.join(out_dir, f"tr64_rank{rank}.npy"), tr)
+        state["M"], state["b"], state["first"] = M, b, (it, nr, tr.tobytes(), x.tobytes())
+        return {"transport": transport(M), "niters": it, "normr": nr.hex()}
+
+    def withhold():
+        M, b = state["M"], state["b"]
+        budget_us = 200000
+        M.set_option("spin_budget_us", budget_us)
+        if rank == 0:
+            M.set_option("dbg_withhold", 1)
+        t0 = time.time()
+        err = None
+        try:
+            solve(M, b)
+        except hp.HPCCGError as e:
+            err = str(e)
+        dt = time.time() - t0
+        M.set_option("dbg_withhold", 0)
+        M.set_option("spin_budget_us", 1000000)
+        it, nr, tr, x, _ = solve(M, b)
+        return {"error": err, "seconds_failed": dt, "budget_s": budget_us * 1e-6,
+                "after_same": (it, nr, tr.tobytes(), x.tobytes()) == state["first"]}
+
+    case("bits64", bits64)
+    case("withhold", withhold)
+    if "M" in state:
+        state["M"].close()
+
+    # 5: the kernel-level entry points across the processes: HPC_sparsemv with
+    # the host-staged halo (KAT-1: A 1 = b bitwise), ddot all-reduced (KAT-2)
+    def kernel_level():
+        nx, ny, nz = 12, 10, 8
+        M = hp.Matrix.generate(nx, ny, nz)
+        n = nx * ny * nz
+        ones = torch.ones(n, dtype=torch.float64, device=f"cuda:{dev}")
+        y = torch.zeros(n, dtype=torch.float64, device=f"cuda:{dev}")
+        hp.HPC_sparsemv(M, ones, y)
+        prob = hp.generate_matrix(nx, ny, nz, rank, world)  # the host generator's b of this rank
+        kat1 = y.cpu().numpy().tobytes() == prob.b.tobytes()
+        prob.close()
+        rr = hp.ddot(n, y, y)
+        M.close()
+        return {"kat1": kat1, "rr": rr, "kat2": float(kat2_rr0(nx, ny, nz * world))}
+
+    case("kernel_level", kernel_level)
+    with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    hp.comm_destroy()
+    dist.destroy_process_group()
+    print(f"HOSTCOMM-WORKER-DONE rank {rank}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
