@@ -170,7 +170,11 @@ struct CgArgs {
 // (after the barrier), [4] slot loop done, [5] epilogue + dot hand-off done
 // (s_memrealtime, 100 MHz), [6] XCC id, [7] iteration k.
 constexpr int kTlWords = 8;
-constexpr int kMboxSlots = 2 * 2 * 16;  // [dot][k & 1][rank], up to kMaxGroupRanks ranks
+// Peer mailbox: [kind][k & 1][rank], kind = kRR / kPAP (the two CG scalars) or
+// kMboxBarrier (the prologue's barrier before the x pull), up to kMboxRanks ranks
+constexpr int kMboxRanks = 16;
+constexpr int kMboxBarrier = 2;
+constexpr int kMboxSlots = 3 * 2 * kMboxRanks;
 
 // Bounded in-kernel waits: a wait that outlives the spin budget (s_memrealtime
 // ticks, 100 MHz) records itself in the device error record and ends the
@@ -246,9 +250,14 @@ void launch_cg_end(const CgArgs& a, hipStream_t s);
 // peer all-reduce self-test: rounds x both scalars through peer_allreduce, results to out[2 * rounds]
 void launch_peer_selftest(const CgArgs& a, int rounds, double* out, hipStream_t s);
 // r-halo by pull: ghost planes of r read from the neighbours' boundary rows
-// (system-scope loads) before the SpMV launch; lo_cnt rows lo_src -> lo_dst, hi likewise
+// (system-scope loads) before the SpMV launch; lo_cnt rows lo_src -> lo_dst, hi likewise.
+// force: outside a solve's iteration test (the creation-time test, the prologue);
+// pexpr: store v + 0.0 v (the prologue's p = x, HPCCG.cpp:347) instead of v
 void launch_pull(const CgArgs& a, const double* lo_src, double* lo_dst, int lo_cnt, const double* hi_src, double* hi_dst,
-                 int hi_cnt, hipStream_t s, bool force = false);
+                 int hi_cnt, hipStream_t s, bool force = false, bool pexpr = false);
+// the prologue's barrier (one lane, peer_allreduce on the kMboxBarrier slots):
+// every rank's p = x (and its x) is in place before any rank pulls x's rows
+void launch_peer_barrier(const CgArgs& a, hipStream_t s);
 // solve start: state zeroed (spin budget set), every dot slot empty, tickets zero
 void launch_rearm(int* kst, double* partial, int np, unsigned int* tickets, int nt, int budget, hipStream_t s);
 void launch_cg_xflush(const CgArgs& a, hipStream_t s);  // pending deferred x updates
@@ -256,6 +265,7 @@ void launch_cg_xflush(const CgArgs& a, hipStream_t s);  // pending deferred x up
 // In-process rank group all-reduce of one CG scalar: g[which] of every rank =
 // sum of loc[which] over ranks, in rank order.
 constexpr int kMaxGroupRanks = 16;
+static_assert(kMaxGroupRanks == kMboxRanks, "mailbox rows");
 struct GroupSum {
     int nranks;
     int which;

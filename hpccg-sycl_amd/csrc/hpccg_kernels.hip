@@ -472,7 +472,7 @@ __device__ __forceinline__ double top_sum_wave(Ld ld, int ng, int lane)
 // Returns NaN when the wait gave up (the solve is void then).
 __device__ __forceinline__ double peer_allreduce(const CgArgs& a, double s, int which, int k, bool drain = false)
 {
-    const int base = (which * 2 + (k & 1)) * (kMboxSlots / 4);
+    const int base = (which * 2 + (k & 1)) * kMboxRanks;
     for (int q = 0; q < a.pranks; q++)
         __hip_atomic_store(a.peers[q] + base + a.prank, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     double* const mb = a.mbox + base;
@@ -2006,9 +2006,10 @@ __global__ void k_end(CgArgs a) { mark_end(a); }
 // has ended leaves them alone.
 __global__ __launch_bounds__(256) void k_pull(CgArgs a, const double* __restrict__ lo_src, double* __restrict__ lo_dst,
                                               int lo_cnt, const double* __restrict__ hi_src,
-                                              double* __restrict__ hi_dst, int hi_cnt, int force)
+                                              double* __restrict__ hi_dst, int hi_cnt, int mode)
 {
-    if (!force) {  // (force: the creation-time test, outside a solve)
+    const bool force = mode & 1, pexpr = mode & 2;
+    if (!force) {  // (force: the creation-time test and the prologue, outside the iteration test)
         const int k = a.fupd ? (a.kst[1] ? a.max_iter : a.kst[a.kpar ? 2 : 0]) : a.kst[0];
         const double rr = a.g[a.fupd ? kRRPar + a.kpar : kRR];
         if (k >= a.max_iter || !(sqrt(k == 1 ? rr : a.hist[max(k - 2, 0)]) > a.tol)) return;  // cg_run
@@ -2029,9 +2030,21 @@ __global__ __launch_bounds__(256) void k_pull(CgArgs a, const double* __restrict
 #pragma unroll
         for (int u = 0; u < kU; u++) {
             const int i = i0 + u * (int)(gridDim.x * blockDim.x);
-            if (i < tot) (i < lo_cnt ? lo_dst[i] : hi_dst[i - lo_cnt]) = v[u];
+            // (pexpr: k_prologue_copy's p = x + 0.0 x on the neighbour's x)
+            if (i < tot) (i < lo_cnt ? lo_dst[i] : hi_dst[i - lo_cnt]) = pexpr ? v[u] + 0.0 * v[u] : v[u];
         }
     }
+}
+
+// The prologue's barrier (one lane): a peer all-reduce on the kMboxBarrier
+// slots. Every rank stores into it after its p = x (stream order), so once it
+// returns every rank's x is in place for the x pull that follows; no rank
+// changes its x before this rank's first r.r contribution, which comes after
+// that pull. Used once per solve: each rank empties its slots when all
+// arrived, long before the next solve's barrier refills them.
+__global__ void k_peer_barrier(CgArgs a)
+{
+    if (threadIdx.x == 0) (void)peer_allreduce(a, 1.0, kMboxBarrier, 0, true);
 }
 
 // The peer all-reduce's creation-time self-test (peer_autotest): one lane runs
@@ -2515,13 +2528,18 @@ void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s)
 void launch_cg_end(const CgArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_end, dim3(1), dim3(64), 0, s, a); }
 
 void launch_pull(const CgArgs& a, const double* lo_src, double* lo_dst, int lo_cnt, const double* hi_src, double* hi_dst,
-                 int hi_cnt, hipStream_t s, bool force)
+                 int hi_cnt, hipStream_t s, bool force, bool pexpr)
 {
     const int tot = lo_cnt + hi_cnt;
     if (tot <= 0) return;
     const int grid = (tot + 4 * 256 - 1) / (4 * 256);
     hipLaunchKernelGGL(k_pull, dim3(grid), dim3(256), 0, s, a, lo_src, lo_dst, lo_cnt, hi_src, hi_dst, hi_cnt,
-                       force ? 1 : 0);
+                       (force ? 1 : 0) | (pexpr ? 2 : 0));
+}
+
+void launch_peer_barrier(const CgArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, s, a);
 }
 
 void launch_peer_selftest(const CgArgs& a, int rounds, double* out, hipStream_t s)

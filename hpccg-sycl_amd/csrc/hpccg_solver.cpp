@@ -351,8 +351,11 @@ struct hpccg_hip_matrix {
     int halo_pull = -1;
     int pull_auto_ok = 0;              // RCCL job: the creation-time pull test passed on every rank
     int proto_auto_ok = 0;             // ... and the production-protocol test (protocol_autotest)
+    std::string selftest_note;         // why a creation-time self-test failed on this rank (diagnostics)
     double* d_pull_lo = nullptr;       // rank - 1's r (its local row 0), mapped here (RCCL job)
     double* d_pull_hi = nullptr;       // rank + 1's r
+    double* d_pullx_lo = nullptr;      // rank - 1's x workspace (d_x, its local row 0): the prologue's p = x halo
+    double* d_pullx_hi = nullptr;      // rank + 1's x
     int pull_lo_n = 0;                 // rank - 1's row count
     std::vector<void*> ipc_r_opened;   // the neighbours' r buffers mapped from other processes
     double* d_mbox = nullptr;          // this rank's mailbox (kMboxSlots, uncached / fine-grained)
@@ -2109,6 +2112,27 @@ int enqueue_iteration(const Ranks& R, int slot = -1, int k_host = 1)
     return 0;
 }
 
+// The prologue's p = x halo by pull (exchange_externals.cpp:51-131 at
+// HPCCG.cpp:349) for a process's rank of a job whose pull tests passed, x in
+// the mapped workspace: after a one-lane peer barrier (every rank's x is in
+// place), the neighbours' boundary rows of x are read with system-scope loads
+// into p's ghost rows through k_prologue_copy's expression. With it a solve
+// makes no RCCL call at all (the host-bootstrapped job has none to make).
+bool xpull_of(const hpccg_hip_matrix* M, const CgArgs& a)
+{
+    return M->nranks > 1 && !M->in_group && pull_of(M) && a.peer_ar && a.x == M->d_x &&
+           (!M->ghost_lo || M->d_pullx_lo) && (!M->ghost_hi || M->d_pullx_hi);
+}
+
+void prologue_pull(hpccg_hip_matrix* M, const CgArgs& a)
+{
+    launch_cg_stamp(a, kStampHalo, true, M->stream);
+    launch_peer_barrier(a, M->stream);
+    const int lo = M->ghost_lo, hi = M->ghost_hi;
+    launch_pull(a, lo ? M->d_pullx_lo + M->pull_lo_n - lo : nullptr, a.p - lo, lo, M->d_pullx_hi, a.p + M->nrow, hi,
+                M->stream, true, true);
+}
+
 int enqueue_prologue(const Ranks& R, bool events)
 {
     const bool multi = multi_of(R.M[0]);
@@ -2116,7 +2140,10 @@ int enqueue_prologue(const Ranks& R, bool events)
         TRY(use_device(R, r));
         launch_cg_prologue_copy(R.a[r], R.M[r]->stream);  // p = x
     }
-    if (multi) TRY(exch_halo(R, 0, true));
+    if (multi && R.P == 1 && xpull_of(R.M[0], R.a[0]))
+        prologue_pull(R.M[0], R.a[0]);
+    else if (multi)
+        TRY(exch_halo(R, 0, true));
     for (int r = 0; r < R.P; r++) {
         hpccg_hip_matrix* M = R.M[r];
         const CgArgs& a = R.a[r];
@@ -2303,11 +2330,14 @@ int map_peer_mailboxes(hpccg_hip_matrix* M, std::vector<double*>& table, int* al
     int ok = 1;
     if (!M->d_mbox) {
         ok = alloc_mbox(M) == 0;
+        if (!ok) M->selftest_note += "mailbox: no uncached or fine-grained memory; ";
         (void)hipGetLastError();
     }
     hipIpcMemHandle_t h;
     std::memset(&h, 0, sizeof h);
-    if (ok && hipIpcGetMemHandle(&h, M->d_mbox) != hipSuccess) {
+    hipError_t e;
+    if (ok && (e = hipIpcGetMemHandle(&h, M->d_mbox)) != hipSuccess) {
+        M->selftest_note += std::string("mailbox hipIpcGetMemHandle: ") + hipGetErrorString(e) + "; ";
         (void)hipGetLastError();
         ok = 0;
     }
@@ -2326,7 +2356,9 @@ int map_peer_mailboxes(hpccg_hip_matrix* M, std::vector<double*>& table, int* al
         hipIpcMemHandle_t hq;
         std::memcpy(&hq, all.data() + rec * q, hb);
         void* ptr = nullptr;
-        if (hipIpcOpenMemHandle(&ptr, hq, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+        if ((e = hipIpcOpenMemHandle(&ptr, hq, hipIpcMemLazyEnablePeerAccess)) != hipSuccess) {
+            M->selftest_note += "rank " + std::to_string(q) + "'s mailbox hipIpcOpenMemHandle: " +
+                                hipGetErrorString(e) + "; ";
             (void)hipGetLastError();
             mapped = 0;
             break;
@@ -2409,22 +2441,31 @@ int pull_autotest(hpccg_hip_matrix* M)
 {
     M->pull_auto_ok = 0;
     const int nr = M->nranks, me = M->rank;
-    hipIpcMemHandle_t h;
-    std::memset(&h, 0, sizeof h);
-    int ok = M->d_rbuf != nullptr;
-    void* base = nullptr;  // the allocation the handle maps (canary mode: before d_rbuf)
-    size_t range = 0;
-    if (ok && (hipMemGetAddressRange(&base, &range, M->d_r) != hipSuccess || hipIpcGetMemHandle(&h, base) != hipSuccess)) {
-        (void)hipGetLastError();
-        ok = 0;
+    // r (the iteration's pull) and the x workspace (the prologue's p = x halo):
+    // the IPC handle of each allocation and the offset of local row 0 in it
+    double* const bufs[2] = {M->d_r, M->d_x};
+    hipIpcMemHandle_t h[2];
+    long long off[2] = {0, 0};
+    std::memset(h, 0, sizeof h);
+    int ok = M->d_rbuf != nullptr && M->d_x != nullptr;
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 2 && ok; i++) {
+        void* base = nullptr;  // the allocation the handle maps (canary mode: before the buffer)
+        size_t range = 0;
+        if ((e = hipMemGetAddressRange(&base, &range, bufs[i])) != hipSuccess ||
+            (e = hipIpcGetMemHandle(&h[i], base)) != hipSuccess) {
+            M->selftest_note += std::string(i ? "x" : "r") + " hipIpcGetMemHandle: " + hipGetErrorString(e) + "; ";
+            (void)hipGetLastError();
+            ok = 0;
+        }
+        off[i] = (long long)((char*)bufs[i] - (char*)base);
     }
-    const size_t hb = sizeof h, rec = hb + 16;  // handle | offset of row 0 (B) | nrow | ok
+    const size_t hb = sizeof(hipIpcMemHandle_t), rec = 2 * hb + 24;  // handles | offsets (B) | nrow | ok
     std::vector<unsigned char> mine(rec, 0), all(rec * nr);
-    std::memcpy(mine.data(), &h, hb);
-    const long long off = ok ? (long long)((char*)M->d_r - (char*)base) : 0;
-    std::memcpy(mine.data() + hb, &off, 8);
-    std::memcpy(mine.data() + hb + 8, &M->nrow, 4);
-    std::memcpy(mine.data() + hb + 12, &ok, 4);
+    std::memcpy(mine.data(), h, 2 * hb);
+    std::memcpy(mine.data() + 2 * hb, off, 16);
+    std::memcpy(mine.data() + 2 * hb + 16, &M->nrow, 4);
+    std::memcpy(mine.data() + 2 * hb + 20, &ok, 4);
     TRY(comm_allgather(mine.data(), all.data(), rec));
     auto field = [&](int q, size_t at, void* out, size_t n) { std::memcpy(out, all.data() + rec * q + at, n); };
     int mapped = 1;
@@ -2433,25 +2474,33 @@ int pull_autotest(hpccg_hip_matrix* M)
         const int need = side == 0 ? M->ghost_lo : M->ghost_hi;
         if (q < 0 || q >= nr || need == 0) continue;
         int qok = 0, qn = 0;
-        long long qoff = 0;
-        field(q, hb + 12, &qok, 4);
-        field(q, hb + 8, &qn, 4);
-        field(q, hb, &qoff, 8);
-        hipIpcMemHandle_t hq;
-        field(q, 0, &hq, hb);
-        void* ptr = nullptr;
-        if (!qok || hipIpcOpenMemHandle(&ptr, hq, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-            (void)hipGetLastError();
-            mapped = 0;
-            break;
+        long long qoff[2] = {0, 0};
+        field(q, 2 * hb + 20, &qok, 4);
+        field(q, 2 * hb + 16, &qn, 4);
+        field(q, 2 * hb, qoff, 16);
+        double* got[2] = {nullptr, nullptr};
+        for (int i = 0; i < 2 && mapped; i++) {
+            hipIpcMemHandle_t hq;
+            field(q, i * hb, &hq, hb);
+            void* ptr = nullptr;
+            if (!qok || (e = hipIpcOpenMemHandle(&ptr, hq, hipIpcMemLazyEnablePeerAccess)) != hipSuccess) {
+                M->selftest_note += "rank " + std::to_string(q) + "'s " + (i ? "x " : "r ") +
+                                    (qok ? std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e)
+                                         : std::string("not exported")) + "; ";
+                (void)hipGetLastError();
+                mapped = 0;
+                break;
+            }
+            M->ipc_r_opened.push_back(ptr);
+            got[i] = reinterpret_cast<double*>(static_cast<char*>(ptr) + qoff[i]);
         }
-        M->ipc_r_opened.push_back(ptr);
-        double* rbase = reinterpret_cast<double*>(static_cast<char*>(ptr) + qoff);
         if (side == 0) {
-            M->d_pull_lo = rbase;
+            M->d_pull_lo = got[0];
+            M->d_pullx_lo = got[1];
             M->pull_lo_n = qn;
         } else {
-            M->d_pull_hi = rbase;
+            M->d_pull_hi = got[0];
+            M->d_pullx_hi = got[1];
         }
     }
     int all_ok = 0;
@@ -2480,6 +2529,7 @@ int pull_autotest(hpccg_hip_matrix* M)
         if (good && hi && d2h(M->stream, gh.data(), M->d_r + M->nrow, sizeof(double) * hi)) good = 0;
         for (int i = 0; i < lo && good; i++) good = gl[i] == pattern((long long)M->start_row - lo + i);
         for (int i = 0; i < hi && good; i++) good = gh[i] == pattern((long long)M->start_row + M->nrow + i);
+        if (!good) M->selftest_note += "pull pattern: the pulled ghost rows differ; ";
         TRY(comm_min(good, &all_ok));
         TRY(comm_min(1, &dummy));  // no rank clears its rows while another still pulls
         HIP_TRY(hipMemsetAsync(M->d_rbuf, 0, sizeof(double) * (size_t)M->pstride, M->stream));
@@ -2488,7 +2538,7 @@ int pull_autotest(hpccg_hip_matrix* M)
     if (!all_ok) {
         for (void* ptr : M->ipc_r_opened) (void)hipIpcCloseMemHandle(ptr);
         M->ipc_r_opened.clear();
-        M->d_pull_lo = M->d_pull_hi = nullptr;
+        M->d_pull_lo = M->d_pull_hi = M->d_pullx_lo = M->d_pullx_hi = nullptr;
         return 0;
     }
     M->pull_auto_ok = 1;
@@ -2528,12 +2578,17 @@ int peer_autotest(hpccg_hip_matrix* M)
     }
     (void)hipGetLastError();
     if (out) (void)hipFree(out);
+    if (!ok) M->selftest_note += "peer test: could not run; ";
+    if (ok && err[0] != kErrNone) M->selftest_note += "peer test: a wait gave up (code " + std::to_string(err[0]) + "); ";
     ok = ok && err[0] == kErrNone;
     for (int k = 0; k < kPeerTestRounds && ok; k++)
         for (int which = 0; which < 2; which++) {
             double want = 0.0;  // k_peer_selftest's contributions, summed in rank order
             for (int q = 0; q < nr; q++) want += (double)(q + 1) + 0.5 * k + 0.25 * which;
-            if (std::memcmp(&want, &got[2 * k + which], sizeof want) != 0) ok = 0;
+            if (std::memcmp(&want, &got[2 * k + which], sizeof want) != 0) {
+                if (ok) M->selftest_note += "peer test: round " + std::to_string(k) + " summed wrong; ";
+                ok = 0;
+            }
         }
     TRY(comm_min(ok, &all_ok));
     TRY(reset_dot_state(M));  // the test's slots, and a rank's waits may have given up: every mailbox empty
@@ -2563,15 +2618,11 @@ int protocol_autotest(hpccg_hip_matrix* M, int* all_ok)
     *all_ok = 0;
     int ok = 1;
     const size_t np = M->npad;
-    double* scratch = nullptr;  // b | x, padded like the solver's own vectors
-    if (hipMalloc(&scratch, 2 * sizeof(double) * np) != hipSuccess) {
-        (void)hipGetLastError();
-        scratch = nullptr;
-        ok = 0;
-    }
+    // b and x: the matrix's own workspace (x is the buffer the neighbours have
+    // mapped for the prologue's pull); b = 1 + (global row mod 13) / 8
     std::vector<double> hb(np, 0.0);
     for (int i = 0; i < M->nrow; i++) hb[i] = 1.0 + (double)(((long long)M->start_row + i) % 13) * 0.125;
-    if (ok && h2d(M, scratch, hb.data(), sizeof(double) * np)) ok = 0;
+    if (h2d(M, M->d_b, hb.data(), sizeof(double) * np)) ok = 0;
     struct Run {
         int it = -1;
         double nr = 0.0;
@@ -2581,17 +2632,10 @@ int protocol_autotest(hpccg_hip_matrix* M, int* all_ok)
     for (int v = 0; v < 2; v++) {  // every rank runs both solves: their RCCL calls and error exchanges are collective
         M->halo_pull = v == 0 ? 2 : (comm_host() ? 1 : 0);
         M->use_graph = 0;
-        const double* b = scratch;
-        double* x = scratch ? scratch + np : nullptr;
-        int rc = 0;
-        if (!scratch) {
-            // no buffers: still take part in the collective steps of a solve
-            // with the matrix's own vectors (its result is not compared)
-            b = M->d_b;
-            x = M->d_x;
-        }
+        const double* b = M->d_b;
+        double* x = M->d_x;
         if (hipMemsetAsync(x, 0, sizeof(double) * np, M->stream) != hipSuccess) ok = 0;
-        rc = solve_ranks(&M, 1, &b, &x, kProtoIters + 1, 0.0, &run[v].it, &run[v].nr, nullptr, 0);
+        const int rc = solve_ranks(&M, 1, &b, &x, kProtoIters + 1, 0.0, &run[v].it, &run[v].nr, nullptr, 0);
         if (rc) ok = 0;
         run[v].trace = M->trace;
         run[v].x.assign(M->nrow, 0.0);
@@ -2602,7 +2646,8 @@ int protocol_autotest(hpccg_hip_matrix* M, int* all_ok)
     M->use_graph = ug0;
     M->trace.clear();
     M->last_niters = 0;
-    if (scratch) (void)hipFree(scratch);
+    if (!ok) M->selftest_note += "protocol test: a solve failed (" + g_err + "); ";
+    const bool ran = ok;
     ok = ok && run[0].it == kProtoIters && run[1].it == run[0].it &&
          std::memcmp(&run[0].nr, &run[1].nr, sizeof(double)) == 0 && run[0].trace.size() == run[1].trace.size() &&
          std::memcmp(run[0].trace.data(), run[1].trace.data(), sizeof(double) * run[0].trace.size()) == 0 &&
@@ -2616,7 +2661,12 @@ int protocol_autotest(hpccg_hip_matrix* M, int* all_ok)
     }
     std::vector<unsigned long long> hs(M->nranks);
     TRY(comm_allgather(&hsh, hs.data(), sizeof hsh));
-    for (unsigned long long q : hs) ok = ok && q == hsh;
+    if (ran && !ok) M->selftest_note += "protocol test: the in-launch pull and the reference transport differ; ";
+    for (unsigned long long q : hs)
+        if (q != hsh && ok) {
+            M->selftest_note += "protocol test: the ranks' traces differ; ";
+            ok = 0;
+        }
     TRY(comm_min(ok, all_ok));
     return 0;
 }
@@ -2749,11 +2799,11 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     // a host-bootstrapped job has no RCCL: the iteration must make no collective
     // call (the scalars summed in the kernels, r's planes pulled). Every rank
     // holds the same options unless the caller set them differently
-    if (P == 1 && M->nranks > 1 && comm_host() && (av[0].allreduce || !av[0].rhalo || !pull_of(M)))
+    if (P == 1 && M->nranks > 1 && comm_host() && (av[0].allreduce || !av[0].rhalo || !pull_of(M) || !xpull_of(M, av[0])))
         return set_err(HPCCG_HIP_EINVAL,
                        "host-bootstrapped communicator: this solve would need RCCL (peer_allreduce %d, rhalo %d, "
-                       "halo_pull %d): leave peer_allreduce, halo_pull, fuse_p and the kernel on auto",
-                       av[0].peer_ar, av[0].rhalo, pull_of(M) ? 1 : 0);
+                       "halo_pull %d, x pull %d): leave peer_allreduce, halo_pull, fuse_p and the kernel on auto",
+                       av[0].peer_ar, av[0].rhalo, pull_of(M) ? 1 : 0, xpull_of(M, av[0]) ? 1 : 0);
     // group fold: RCCL-style group sums (no peer all-reduce), both dots folded,
     // no overlapped halo (its SpMV runs as two launches)
     if (P > 1 && Ms[0]->group_fold != 0 && av[0].allreduce && fold_of(av[0], kPAP) && fold_of(av[0], kRR) &&
@@ -3012,14 +3062,20 @@ int finish_matrix(hpccg_hip_matrix* M)
                 M->peer_auto_ok = M->pull_auto_ok = 0;
                 for (void* ptr : M->ipc_r_opened) (void)hipIpcCloseMemHandle(ptr);
                 M->ipc_r_opened.clear();
-                M->d_pull_lo = M->d_pull_hi = nullptr;
+                M->d_pull_lo = M->d_pull_hi = M->d_pullx_lo = M->d_pullx_hi = nullptr;
             }
         }
         if (host && !(M->peer_auto_ok && M->pull_auto_ok))
             return set_err(HPCCG_HIP_EPLAN, "host-bootstrapped communicator: the %s self-test failed on some rank "
-                                            "(peer %d, pull %d, protocol %d); this transport needs all three",
+                                            "(peer %d, pull %d, protocol %d); this transport needs all three. "
+                                            "This rank: %s",
                            !M->peer_auto_ok ? "peer all-reduce" : !M->pull_auto_ok ? "halo pull" : "protocol",
-                           M->peer_auto_ok, M->pull_auto_ok, M->proto_auto_ok);
+                           M->peer_auto_ok, M->pull_auto_ok, M->proto_auto_ok,
+                           M->selftest_note.empty() ? "passed" : M->selftest_note.c_str());
+        if ((peer && !M->peer_auto_ok) || (pull && !M->pull_auto_ok))  // (an RCCL job falls back; say why)
+            std::fprintf(stderr, "hpccg_hip rank %d: in-kernel transport off (peer %d, pull %d, protocol %d): %s\n",
+                         M->rank, M->peer_auto_ok, M->pull_auto_ok, M->proto_auto_ok,
+                         M->selftest_note.empty() ? "another rank failed" : M->selftest_note.c_str());
     }
     return 0;
 }
