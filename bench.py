@@ -8,12 +8,18 @@ x resident in HBM before the timed region (device generator).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 200] [--stencil 27]
 
-N > 1: one process per GPU under torch.distributed.run (the driver's launch;
+N > 1: one process per rank under torch.distributed.run (the driver's launch;
 `python bench.py --gpus N` without WORLD_SIZE starts that launcher itself as a
 child process before touching a GPU); z-stacked slabs (local nz fixed, weak
-scaling), halo + dot all-reduces over RCCL inside libhpccg_hip.so;
-torch.distributed (gloo) carries only the control plane (unique id, barrier,
-max-over-ranks time).
+scaling). One rank per GPU over RCCL (--comm rccl, the default when there are
+at least N GPUs): after the creation-time self-tests the iteration sums its two
+scalars inside the kernels and pulls its ghost planes from the neighbours'
+memory, RCCL being the fallback; with fewer GPUs than ranks (--comm host) the
+ranks share GPUs and bootstrap through the host (hpccg_hip_comm_init_host),
+running the same in-kernel transport between processes. torch.distributed
+(gloo) carries only the control plane (unique id / setup all-gathers, barrier,
+max-over-ranks time). The line carries every rank's transport verdicts, the
+max-over-ranks SpMV launch time, and a CPU leg on the global problem.
 
 value = (CG iterations x ranks x K) / max-over-ranks wall time of the K steps
       = 200^3-slab CG iterations per second summed over GPUs.
@@ -28,12 +34,18 @@ roofline (the SpMV kernel, 84 % of the reference's time):
   rocprofv3 FETCH_SIZE / WRITE_SIZE passes of the same kernel
   (profiles/pmc_spmv_<stencil>pt_<n>.json), or null. credited_frac keeps
   SURVEY 8(d)'s fixed formula (12 nnz + 20 n SpMV + ddot/waxpby bytes the
-  fused kernel absorbs), which can pass 1.0 because the format moves less.
+  fused kernel absorbs) is reported as bytes only.
 cpu_baseline: the reference compiled from its own sources (oracle/_ref) on
-  a bounded sample of the same problem, rank 0, N = 1 only, three legs: the
+  a bounded sample of the same problem, rank 0. N = 1: three legs, the
   OpenMP build with one thread per physical core of this process's CPU mask
-  (the full-host bar, the headline value), the OpenMP build with the box's
-  thread share (OMP_NUM_THREADS), and the serial build.
+  (the full-host bar), the OpenMP build with the box's thread share
+  (OMP_NUM_THREADS), and the serial build; value = the fastest. N > 1: the
+  reference on the global nx x ny x (N nz) problem with the
+  box's thread share, sampled iterations; value in the same unit as the line's
+  (global-problem iterations/s x N, i.e. per-GPU-slab iterations summed).
+secondary (N = 1): the other single-GPU configs of BASELINE.json (27-pt 100^3,
+  7-pt 256^3) measured in the same run the same way: value, launch time,
+  compulsory-byte fraction, committed PMC traffic ratio; no CPU leg.
 
 Multi-GPU runs describe themselves: every rank logs its stages on stderr
 (comm init, setup, first solve, timed steps), the line carries what RCCL
@@ -282,6 +294,332 @@ def opt_or_none(M, key):
         return None
 
 
+def cpu_baseline_global(nx, ny, nz_global, use_7pt, world, budget_s=15.0):
+    """N > 1: the reference (oracle/_ref, OpenMP, the box's thread share) on the
+    global z-stacked problem the N ranks solve together (the
+    200 x 200 x 1600 problem on the host cores), first iterations of one
+    HPCCG() solve. value is reported as global iterations/s x N: the unit of
+    the line's value (per-slab iterations summed over the N slabs)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
+    import oracle  # test infrastructure: baseline leg only
+    share = int(os.environ["OMP_NUM_THREADS"])
+    if not os.path.exists(oracle.REF_OMP_SO):
+        raise RuntimeError("oracle/_ref is not built (make -C oracle ref)")
+    t0 = time.time()
+    A = oracle.generate(nx, ny, nz_global, use_7pt=use_7pt)
+    gomp = ctypes.CDLL("libgomp.so.1")
+    gomp.omp_set_num_threads(share)
+    saved = os.dup(1)
+    null = os.open(os.devnull, os.O_WRONLY)
+    os.dup2(null, 1)
+    try:
+        M = oracle.ref_from_csr(A, omp=True)
+        b = A.b
+        del A  # the reference holds its own copy
+        setup_s = time.time() - t0
+        probe = 2
+        t = oracle.ref_hpccg(M, b, max_iter=probe + 1)["times"][0]
+        iters = int(max(2, min(500, budget_s / max(t / probe, 1e-6))))
+        res = oracle.ref_hpccg(M, b, max_iter=iters + 1)
+        M.close()
+    finally:
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(saved, 1)
+        os.close(null)
+        os.close(saved)
+    its = res["niters"] / res["times"][0]
+    return {"value": its * world, "unit": "CG iterations/s (global-problem iterations x %d slabs)" % world,
+            "global_iterations_per_s": its, "cores": share, "threads": share, "kind": "reference",
+            "leg": "box_share", "physical_cores": physical_cores(), "host": host_cpu(),
+            "setup_s": round(setup_s, 1),
+            "sample": f"global {nx}x{ny}x{nz_global} {'7' if use_7pt else '27'}-pt (the {world} slabs together), "
+                      f"first {res['niters']} CG iterations of one reference HPCCG() solve "
+                      f"({res['times'][0]:.1f} s), OpenMP {share} threads "
+                      f"(OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, OMP_PLACES={os.environ.get('OMP_PLACES')})"}
+
+
+def measure(hp, torch, M, dev, max_iter, steps, warmup, event_steps, world, dist=None, stage=None):
+    """Warmup, then `steps` timed solves bracketed by a barrier and a device
+    sync on both sides; the first `event_steps` of them eager with hipEvents
+    around every SpMV launch (the roofline's kernel time), the rest graph
+    replays. Returns the raw numbers (elapsed is the max over ranks)."""
+    b, _, _ = M.vectors()
+    nrow = M.info()["nrow"]
+    x = torch.zeros(nrow, dtype=torch.float64, device=f"cuda:{dev}")
+    torch.cuda.synchronize()
+
+    def step(events):
+        M.set_option("event_timing", 1 if events else 0)
+        x.zero_()
+        return hp.HPCCG(M, b, x, max_iter=max_iter, device=True)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    cold_s = None
+    for i in range(warmup):
+        t0 = time.perf_counter()
+        step(i == 0)
+        if i == 0:
+            cold_s = time.perf_counter() - t0  # first solve: graph build, cold caches
+            if stage:
+                stage("first_solve", seconds=f"{cold_s:.3f}")
+    barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    niters_total = 0
+    spmv_ms = spmv_n = upd_ms = upd_n = 0.0
+    times_acc = [0.0] * 7
+    step_s = []
+    graph_used = 1
+    it, nr = 0, 0.0
+    for i in range(steps):
+        ev = i < event_steps
+        t0 = time.perf_counter()
+        _, it, nr, times = step(ev)
+        step_s.append(time.perf_counter() - t0)
+        niters_total += it
+        if ev:
+            kt = M.kernel_times()
+            spmv_ms += kt["spmv_ms"]
+            spmv_n += kt["spmv_launches"]
+            upd_ms += kt["update_ms"]
+            upd_n += kt["update_launches"]
+        else:
+            graph_used = min(graph_used, M.get_option("graph_used"))
+        for j in range(7):
+            times_acc[j] += times[j]
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    local_elapsed = elapsed
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    # outside the timed region: the last solve's answer (xexact = 1, generate_matrix.cpp:286)
+    # and residual reduction, max over ranks -- a wrong multi-rank exchange shows here
+    tr = M.last_trace()
+    chk = torch.tensor([(x - 1.0).abs().max().item(), float(nr / tr[0]) if tr[0] > 0 else 0.0],
+                       dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(chk, op=dist.ReduceOp.MAX)
+    if spmv_n > 0:
+        spmv_avg_s = spmv_ms / spmv_n * 1e-3
+        timing_src = ("hipEvent pairs around every SpMV launch on the solver stream, %d of the %d timed steps "
+                      "(eager; the others replay hipGraphs)" % (event_steps, steps))
+    else:  # graph mode only: device-clock stamps (SPARSEMV class time / calls)
+        spmv_avg_s = times_acc[3] / max(1, niters_total + steps)
+        timing_src = "s_memrealtime stamps (graph mode)"
+    return {"elapsed": elapsed, "local_elapsed": local_elapsed, "niters_total": niters_total, "it": it,
+            "spmv_avg_s": spmv_avg_s, "timing_src": timing_src, "upd_ms": upd_ms, "upd_n": upd_n,
+            "times_acc": times_acc, "step_s": step_s, "cold_s": cold_s, "graph_used": graph_used,
+            "chk": [chk[0].item(), chk[1].item()], "steps": steps, "event_steps": event_steps}
+
+
+def roofline_of(M, n, stencil, spmv_avg_s):
+    """The SpMV launch against the HBM roofline: format-compulsory bytes
+     over the launch time, the committed PMC traffic of the same
+    kernel configuration, SURVEY 8(d)'s credited bytes beside them."""
+    info = M.info()
+    nrow = info["nrow"]
+    kernel = M.get_option("spmv_kernel")
+    kfmt = 3 if (kernel == 2 and M.get_option("a2_ring") > 0) else kernel  # 3: the pair kernel's LDS-DMA ring form
+    fused = M.get_option("fuse_p")
+    slots = info["slots"]
+    # bytes the SpMV must move in its format: the stored slots (8 B; SELL-512
+    # also 4 B of column), p or (r, p_{k-1}) once, p_k and Ap written
+    slot_bytes = 12.0 if kernel == 0 else 8.0
+    vec_bytes = (32.0 if fused else 16.0) * nrow
+    # x_defer 2: the launch's trailing blocks apply the deferred x terms of
+    # 1/q of the rows (q = x_ring - 1): x read and written, q p's read
+    xside = M.get_option("x_defer") == 2
+    q = M.get_option("x_ring") - 1
+    side_bytes = (16.0 + 8.0 * q) / q * nrow if xside else 0.0
+    # fused update: the launch's trailing blocks also run the update (r, Ap read; r written)
+    fupd = M.get_option("fuse_update") == 1
+    upd_bytes = 24.0 * nrow if fupd else 0.0
+    format_bytes = slot_bytes * slots + vec_bytes + side_bytes + upd_bytes
+    # SURVEY 8(d) credited bytes: HPC_sparsemv 12 nnz + 20 n, ddot(p, Ap) 16 n,
+    # with the fused p update the waxpby p = r + beta p, 24 n
+    credited = 12.0 * info["nnz"] + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fused else 0.0)
+    achieved = format_bytes / spmv_avg_s / 1e9
+    traffic, traffic_src = pmc_traffic(f"spmv_{stencil}pt_{n}", kfmt, fused, M.get_option("x_defer"),
+                                       M.get_option("fuse_update"))
+    roof = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        # FETCH_SIZE / WRITE_SIZE count the L2 <-> fabric bytes: Infinity
+        # Cache (MALL) hits are in them. An image under 256 MB (100^3)
+        # may be served partly by the MALL, so "hbm" is its upper bound.
+        "traffic_note": "L2-fabric bytes (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE), Infinity Cache hits included",
+        "traffic_over_compulsory": round(traffic / format_bytes, 4) if traffic else None,
+        "image_fits_infinity_cache": not bool(M.get_option("nt")),
+        "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
+        "kernel": "%s: %s + p.Ap%s" % (KERNEL_NAMES[kfmt], FORMAT_NAMES[kfmt], " + p = r + beta p" if fused else ""),
+        "bytes_per_launch": format_bytes,
+        "bytes_formula": ("%g B per stored slot x %d slots + %d B per row (r, p_{k-1} read; p_k, Ap "
+                          "written)" % (slot_bytes, slots, 32) if fused else
+                          "%g B per stored slot x %d slots + 16 B per row (p read, Ap written)" % (slot_bytes, slots)) +
+                         (" + (16 + 8 q) / q B per row, q = %d (side blocks: x read and written, q p's read "
+                          "for 1/q of the rows)" % q if xside else "") +
+                         (" + 24 B per row (fused update blocks: r and Ap read, r written)" if fupd else ""),
+        # SURVEY 8(d)'s fixed byte formula for the unfused reference sequence
+        # this launch replaces (more bytes than this format moves; no rate is
+        # derived from it: `frac` above is the roofline fraction)
+        "credited_bytes_per_launch": credited,
+        "avg_launch_us": round(spmv_avg_s * 1e6, 2),
+    }
+    if traffic:
+        roof["traffic_gbs"] = round(traffic / spmv_avg_s / 1e9, 1)
+        roof["traffic_frac"] = round(traffic / spmv_avg_s / 1e9 / HBM_PEAK_GBS, 4)
+    return roof, kernel, kfmt, fused, fupd
+
+
+TRANSPORT_KEYS = ("peer_allreduce", "halo_pull", "rhalo", "fuse_update", "peer_auto_ok", "pull_auto_ok",
+                  "proto_auto_ok")
+
+
+def rank_record(hp, M, rank, dev, comm_mode, rt, meas):
+    """What every rank contributes to the line (gathered to rank 0)."""
+    return {"rank": rank, "device": dev, "pci_bus_id": rt.get("pci_bus_id"), "comm": comm_mode,
+            "rccl_nranks": rt.get("rccl_nranks"),
+            "transport": {k: opt_or_none(M, k) for k in TRANSPORT_KEYS},
+            "spmv_avg_us": round(meas["spmv_avg_s"] * 1e6, 3), "local_elapsed_s": round(meas["local_elapsed"], 6),
+            "halo_us_per_iteration": round(meas["times_acc"][5] / max(1, meas["niters_total"]) * 1e6, 3),
+            "allreduce_us_per_iteration": round(meas["times_acc"][4] / max(1, meas["niters_total"]) * 1e6, 3)}
+
+
+def gather_ranks(dist, world, rec):
+    """Every rank's record, in rank order (gloo)."""
+    if world == 1:
+        return [rec]
+    out = [None] * world
+    dist.all_gather_object(out, rec)
+    return out
+
+
+def multirank_summary(ranks, bytes_per_launch):
+    """N > 1: the slowest rank's SpMV launch (hipEvents) against the roofline,
+    and the transport every rank actually ran."""
+    worst = max(ranks, key=lambda r: r["spmv_avg_us"])
+    ach = bytes_per_launch / (worst["spmv_avg_us"] * 1e-6) / 1e9
+    tr = [r["transport"] for r in ranks]
+    in_kernel = all(t.get("peer_allreduce") == 1 and t.get("halo_pull") in (1, 2) for t in tr)
+    return {"spmv_avg_us_max_over_ranks": worst["spmv_avg_us"], "slowest_rank": worst["rank"],
+            "frac_max_over_ranks": round(ach / HBM_PEAK_GBS, 4),
+            "spmv_avg_us_per_rank": [r["spmv_avg_us"] for r in ranks],
+            "transport_used": ("in-kernel: peer all-reduce + halo pull (no collective call per iteration)"
+                               if in_kernel else "RCCL (all-reduce and/or send/recv per iteration) on some rank"),
+            "verdicts_per_rank": [{k: t.get(k) for k in ("peer_auto_ok", "pull_auto_ok", "proto_auto_ok")}
+                                  for t in tr],
+            "halo_us_per_iteration_per_rank": [r["halo_us_per_iteration"] for r in ranks],
+            "allreduce_us_per_iteration_per_rank": [r["allreduce_us_per_iteration"] for r in ranks]}
+
+
+def secondary_config(hp, torch, n, stencil, dev, args):
+    """One other single-GPU config of BASELINE.json, measured like the headline."""
+    M = hp.Matrix.generate(n, n, n, use_7pt=stencil == 7)
+    try:
+        meas = measure(hp, torch, M, dev, args.max_iter, args.secondary_steps, 2, 1, 1)
+        roof, kernel, kfmt, fused, fupd = roofline_of(M, n, stencil, meas["spmv_avg_s"])
+        value = meas["niters_total"] / meas["elapsed"]
+        return {"metric": f"CG iterations/sec + effective SpMV GB/s (% HBM peak), {stencil}-pt nx=ny=nz={n}",
+                "workload": f"HPCCG solve, {stencil}-pt {n}x{n}x{n}, max_iter={args.max_iter}, tolerance 0",
+                "value": round(value, 3), "unit": "CG iterations/s", "steps": meas["steps"],
+                "ms_per_step": round(meas["elapsed"] / meas["steps"] * 1e3, 3),
+                "avg_launch_us": roof["avg_launch_us"], "frac": roof["frac"],
+                "traffic_over_compulsory": roof["traffic_over_compulsory"], "roofline": roof,
+                "spmv_kernel": kernel, "graph_replay": bool(meas["graph_used"]),
+                "check": {"x_minus_xexact_inf": meas["chk"][0], "final_normr_over_initial": meas["chk"][1],
+                          "niters_per_solve": meas["it"]},
+                "cpu_baseline": None,
+                "cpu_note": "no CPU leg for secondary configs (the headline line carries the reference's)"}
+    finally:
+        M.close()
+
+
+def build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt, ranks, cpu, secondary,
+               probe_report):
+    """The one JSON line (pure: the CPU suite checks its schema for N > 1)."""
+    it_per_s = meas["niters_total"] / meas["elapsed"]  # per rank: every rank runs the same iterations
+    value = it_per_s * world
+    nrow = info["nrow"]
+    iter_bytes = 12.0 * info["nnz"] + 116.0 * nrow  # unfused reference sequence, SURVEY 8(d)
+    step_s = meas["step_s"]
+    es = meas["event_steps"]
+    times_acc, niters_total = meas["times_acc"], meas["niters_total"]
+    fupd = M_opts.get("fuse_update") == 1
+    comm = ranks[0]["comm"]
+    out = {
+        "metric": f"CG iterations/sec + effective SpMV GB/s (% HBM peak), {args.stencil}-pt nx=ny=nz={n}",
+        "value": round(value, 3),
+        "unit": "CG iterations/s (per-GPU %d^3 slab iterations, summed over GPUs)" % n,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(meas["elapsed"] / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (generate_matrix stencil on the device; deterministic, no RNG)",
+        "config": {
+            "workload": f"HPCCG solve, {args.stencil}-pt {n}x{n}x{n} per GPU, z-stacked, "
+                        f"max_iter={args.max_iter} ({args.max_iter - 1} CG iterations), tolerance 0",
+            "nx": n, "ny": n, "nz_per_gpu": n, "stencil": args.stencil,
+            "max_iter": args.max_iter,
+            "parallelism": f"z-slab x{world}" + ("" if world == 1 else f" ({comm})"),
+            "nnz_per_gpu": info["nnz"], "matrix_slots_per_gpu": info["slots"],
+            "spmv_kernel": kernel, "matrix_format": FORMAT_NAMES[kfmt],
+            "device_bytes_per_gpu": M_opts.get("device_bytes"),
+            "graph_replay": bool(meas["graph_used"]),
+            "placement_probe": probe_report,
+            "options": {k: M_opts.get(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update", "overlap",
+                                                   "graph_chunk", "nt", "a2_ring", "nt_store", "fuse_update", "rhalo",
+                                                   "peer_allreduce", "halo_pull")},
+        },
+        "cg_iterations_per_s_global": round(it_per_s, 3),
+        "spmv_effective_gbs": roof["achieved"],
+        "spmv_frac_hbm_peak": roof["frac"],
+        "iteration_effective_gbs_credited": round(iter_bytes * it_per_s / 1e9, 1),
+        "roofline": dict(roof, timing=meas["timing_src"]),
+        # fused update: no update launch (its work is inside the SpMV launch above)
+        "update_kernel_avg_us": round(meas["upd_ms"] / meas["upd_n"] * 1e3, 2) if (meas["upd_n"] and not fupd)
+        else None,
+        "check": {"x_minus_xexact_inf": meas["chk"][0], "final_normr_over_initial": meas["chk"][1],
+                  "niters_per_solve": meas["it"]},
+        # per-solve wall times on rank 0 (SURVEY 8(d): first/cold and median of the solves);
+        # event steps launch eagerly with hipEvents and are slower than the graph replays
+        "solve_ms": {"cold": round(meas["cold_s"] * 1e3, 3) if meas["cold_s"] is not None else None,
+                     "median": round(sorted(step_s)[len(step_s) // 2] * 1e3, 3),
+                     "min": round(min(step_s) * 1e3, 3), "max": round(max(step_s) * 1e3, 3),
+                     "median_graph_replay": round(sorted(step_s[es:])[len(step_s[es:]) // 2] * 1e3, 3)
+                     if len(step_s) > es else None},
+        "times_per_step_s": {"total": times_acc[0] / args.steps, "ddot": times_acc[1] / args.steps,
+                             "waxpby": times_acc[2] / args.steps, "sparsemv": times_acc[3] / args.steps,
+                             "allreduce": times_acc[4] / args.steps, "halo": times_acc[5] / args.steps},
+        # rank 0's device stamps (HPCCG.cpp:71-72 classes t4, t5) per CG iteration
+        "per_iteration_us": {"allreduce": round(times_acc[4] / max(1, niters_total) * 1e6, 3),
+                             "halo": round(times_acc[5] / max(1, niters_total) * 1e6, 3),
+                             "total": round(meas["elapsed"] / max(1, niters_total) * 1e6, 3)},
+        "runtime": dict(rt, comm=comm, ranks=ranks),
+        "cpu_baseline": cpu,
+    }
+    if world > 1:
+        out["multirank"] = multirank_summary(ranks, roof["bytes_per_launch"])
+    if secondary is not None:
+        out["secondary"] = secondary
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -291,6 +629,12 @@ def main():
     ap.add_argument("--stencil", type=int, default=27, choices=[27, 7])
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="N = 1: skip the other single-GPU configs (27-pt 100^3, 7-pt 256^3)")
+    ap.add_argument("--secondary-steps", type=int, default=10)
+    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "host"],
+                    help="N > 1: rccl (one rank per GPU), host (hpccg_hip_comm_init_host: ranks may share a GPU); "
+                         "auto = rccl when there are at least N GPUs")
     ap.add_argument("--kernel", type=int, default=-1, help="SpMV kernel: 0 SELL-512, 1 A direct, 2 A pairs")
     ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1 auto, 0 off)")
     ap.add_argument("--fold", type=int, default=-1, help="dot completion in the producer (-1 auto, 0..3)")
@@ -327,30 +671,27 @@ def main():
     import torch
     import torch.distributed as dist
     hp = load_pkg()
-    torch.cuda.set_device(local_rank)
-    hp.set_device(local_rank)
+    ndev = max(1, torch.cuda.device_count())
+    comm = args.comm if args.comm != "auto" else ("rccl" if ndev >= world else "host")
+    dev = local_rank % ndev
+    torch.cuda.set_device(dev)
+    hp.set_device(dev)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        obj = [hp.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        hp.comm_init(obj[0], world, rank)
+        if comm == "rccl":
+            obj = [hp.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            hp.comm_init(obj[0], world, rank)
+        else:
+            hp.comm_init_host(world, rank)
+    else:
+        comm = "none"
     try:
         rt = hp.runtime_info()
     except AttributeError:  # an older library under A/B (HPCCG_HIP_LIB)
         rt = {"rccl_nranks": None, "pci_bus_id": None, "rccl_version": None, "rccl_rank": rank}
-    stage("comm_init", rccl_nranks=rt["rccl_nranks"], pci=rt["pci_bus_id"], rccl=rt["rccl_version"])
-    if world > 1:
-        gathered = [None] * world
-        dist.all_gather_object(gathered, (rt["pci_bus_id"], rt["rccl_nranks"], rt["rccl_rank"]))
-        rt["pci_bus_ids"] = [g[0] for g in gathered]
-        rt["rccl_ranks_seen"] = [g[2] for g in gathered]
-        rt["distinct_devices"] = len(set(rt["pci_bus_ids"]))
-        if rt["rccl_nranks"] != world or rt["distinct_devices"] != world:
-            log(f"[rank {rank}] WARNING: RCCL counts {rt['rccl_nranks']} ranks on {rt['distinct_devices']} distinct "
-                f"devices for WORLD_SIZE={world}")
-    else:
-        rt["pci_bus_ids"] = [rt["pci_bus_id"]]
-        rt["distinct_devices"] = 1
+    stage("comm_init", comm=comm, device=dev, rccl_nranks=rt["rccl_nranks"], pci=rt["pci_bus_id"],
+          rccl=rt["rccl_version"])
 
     n = args.n
     use_7pt = args.stencil == 7
@@ -375,203 +716,53 @@ def main():
     for kv in args.set:
         key, _, val = kv.partition("=")
         M.set_option(key.strip(), int(val))
-    b, x0, _ = M.vectors()
-    nrow = n * n * n
-    x = torch.zeros(nrow, dtype=torch.float64, device=f"cuda:{local_rank}")
-    torch.cuda.synchronize()
-    kernel = M.get_option("spmv_kernel")
-    kfmt = 3 if (kernel == 2 and M.get_option("a2_ring") > 0) else kernel  # 3: the pair kernel's LDS-DMA ring form
-    stage("setup", seconds=f"{time.time() - t0:.2f}", nnz=info["nnz"], slots=info["slots"], kernel=kernel,
-          device_gb=f"{M.get_option('device_bytes') / 1e9:.2f}")
+    stage("setup", seconds=f"{time.time() - t0:.2f}", nnz=info["nnz"], slots=info["slots"],
+          kernel=M.get_option("spmv_kernel"), device_gb=f"{M.get_option('device_bytes') / 1e9:.2f}",
+          transport={k: opt_or_none(M, k) for k in ("peer_allreduce", "halo_pull", "proto_auto_ok")})
 
-    def step(events):
-        M.set_option("event_timing", 1 if events else 0)
-        x.zero_()
-        return hp.HPCCG(M, b, x, max_iter=args.max_iter, device=True)
-
-    cold_s = None
-    for i in range(args.warmup):
-        t0 = time.perf_counter()
-        step(i == 0)
-        if i == 0:
-            cold_s = time.perf_counter() - t0  # first solve: graph build, cold caches
-            stage("first_solve", seconds=f"{cold_s:.3f}")
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    niters_total = 0
-    spmv_ms = spmv_n = upd_ms = upd_n = 0.0
-    times_acc = [0.0] * 7
-    step_s = []
-    graph_used = 1
-    for i in range(args.steps):
-        ev = i < args.event_steps
-        t0 = time.perf_counter()
-        _, it, nr, times = step(ev)
-        step_s.append(time.perf_counter() - t0)
-        niters_total += it
-        if ev:
-            kt = M.kernel_times()
-            spmv_ms += kt["spmv_ms"]
-            spmv_n += kt["spmv_launches"]
-            upd_ms += kt["update_ms"]
-            upd_n += kt["update_launches"]
-        else:
-            graph_used = min(graph_used, M.get_option("graph_used"))
-        for j in range(7):
-            times_acc[j] += times[j]
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    stage("timed", steps=args.steps, seconds=f"{elapsed:.3f}")
+    meas = measure(hp, torch, M, dev, args.max_iter, args.steps, args.warmup, args.event_steps, world, dist, stage)
+    stage("timed", steps=args.steps, seconds=f"{meas['elapsed']:.3f}")
+    roof, kernel, kfmt, fused, fupd = roofline_of(M, n, args.stencil, meas["spmv_avg_s"])
+    M_opts = {k: opt_or_none(M, k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update", "overlap",
+                                             "graph_chunk", "nt", "a2_ring", "nt_store", "fuse_update", "rhalo",
+                                             "peer_allreduce", "halo_pull", "device_bytes")}
+    ranks = gather_ranks(dist, world, rank_record(hp, M, rank, dev, comm, rt, meas))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    # outside the timed region: the last solve's answer (xexact = 1, generate_matrix.cpp:286)
-    # and residual reduction, max over ranks -- a wrong multi-rank exchange shows here
-    tr = M.last_trace()
-    chk = torch.tensor([(x - 1.0).abs().max().item(), float(nr / tr[0]) if tr[0] > 0 else 0.0],
-                       dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(chk, op=dist.ReduceOp.MAX)
+        rt["pci_bus_ids"] = [r["pci_bus_id"] for r in ranks]
+        rt["distinct_devices"] = len(set(rt["pci_bus_ids"]))
+        if comm == "rccl" and (rt["rccl_nranks"] != world or rt["distinct_devices"] != world):
+            log(f"[rank {rank}] WARNING: RCCL counts {rt['rccl_nranks']} ranks on {rt['distinct_devices']} distinct "
+                f"devices for WORLD_SIZE={world}")
+    else:
+        rt["pci_bus_ids"] = [rt["pci_bus_id"]]
+        rt["distinct_devices"] = 1
+    M.close()
 
-    fused = M.get_option("fuse_p")
-    slots = info["slots"]
-    # bytes the SpMV must move in its format: the stored slots (8 B; SELL-512
-    # also 4 B of column), p or (r, p_{k-1}) once, p_k and Ap written
-    slot_bytes = 12.0 if kernel == 0 else 8.0
-    vec_bytes = (32.0 if fused else 16.0) * nrow
-    # x_defer 2: the launch's trailing blocks apply the deferred x terms of
-    # 1/q of the rows (q = x_ring - 1): x read and written, q p's read
-    xside = M.get_option("x_defer") == 2
-    q = M.get_option("x_ring") - 1
-    side_bytes = (16.0 + 8.0 * q) / q * nrow if xside else 0.0
-    # fused update: the launch's trailing blocks also run the update (r, Ap read; r written)
-    fupd = M.get_option("fuse_update") == 1
-    upd_bytes = 24.0 * nrow if fupd else 0.0
-    format_bytes = slot_bytes * slots + vec_bytes + side_bytes + upd_bytes
-    # SURVEY 8(d) credited bytes: HPC_sparsemv 12 nnz + 20 n, ddot(p, Ap) 16 n,
-    # with the fused p update the waxpby p = r + beta p, 24 n
-    credited = 12.0 * info["nnz"] + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fused else 0.0)
-    if spmv_n > 0:
-        spmv_avg_s = spmv_ms / spmv_n * 1e-3
-        timing_src = ("hipEvent pairs around every SpMV launch on the solver stream, %d of the %d timed steps "
-                      "(eager; the others replay hipGraphs)" % (args.event_steps, args.steps))
-    else:  # graph mode only: device-clock stamps (SPARSEMV class time / calls)
-        spmv_avg_s = times_acc[3] / max(1, niters_total + args.steps)
-        timing_src = "s_memrealtime stamps (graph mode)"
-    achieved = format_bytes / spmv_avg_s / 1e9
-    it_per_s = niters_total / elapsed  # per rank: every rank runs the same iterations
-    value = it_per_s * world
-    ms_per_step = elapsed / args.steps * 1e3
-    iter_bytes = 12.0 * info["nnz"] + 116.0 * nrow  # unfused reference sequence, SURVEY 8(d)
-    traffic, traffic_src = pmc_traffic(f"spmv_{args.stencil}pt_{n}", kfmt, fused, M.get_option("x_defer"),
-                                       M.get_option("fuse_update"))
+    secondary = None
+    if world == 1 and not args.no_secondary:
+        secondary = []
+        for n2, st2 in ((100, 27), (256, 7)):
+            if (n2, st2) == (n, args.stencil):
+                continue
+            try:
+                secondary.append(secondary_config(hp, torch, n2, st2, dev, args))
+                stage("secondary", config=f"{st2}pt_{n2}", value=secondary[-1]["value"])
+            except Exception as e:  # reported, never silently dropped
+                secondary.append({"workload": f"{st2}-pt {n2}^3", "error": repr(e)})
 
     if rank == 0:
-        out = {
-            "metric": f"CG iterations/sec + effective SpMV GB/s (% HBM peak), {args.stencil}-pt nx=ny=nz={n}",
-            "value": round(value, 3),
-            "unit": "CG iterations/s (per-GPU %d^3 slab iterations, summed over GPUs)" % n,
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (generate_matrix stencil on the device; deterministic, no RNG)",
-            "config": {
-                "workload": f"HPCCG solve, {args.stencil}-pt {n}x{n}x{n} per GPU, z-stacked, "
-                            f"max_iter={args.max_iter} ({args.max_iter - 1} CG iterations), tolerance 0",
-                "nx": n, "ny": n, "nz_per_gpu": n, "stencil": args.stencil,
-                "max_iter": args.max_iter, "parallelism": f"z-slab x{world} (RCCL)",
-                "nnz_per_gpu": info["nnz"], "matrix_slots_per_gpu": slots,
-                "spmv_kernel": kernel, "matrix_format": FORMAT_NAMES[kfmt],
-                "device_bytes_per_gpu": M.get_option("device_bytes"),
-                "graph_replay": bool(graph_used),
-                "placement_probe": placement_report(args.placement, probe_us, pick),
-                "options": {k: opt_or_none(M, k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update",
-                                                           "overlap", "graph_chunk", "nt", "a2_ring", "nt_store",
-                                                           "fuse_update", "rhalo", "peer_allreduce", "halo_pull")},
-            },
-            "cg_iterations_per_s_global": round(it_per_s, 3),
-            "spmv_effective_gbs": round(achieved, 1),
-            "spmv_frac_hbm_peak": round(achieved / HBM_PEAK_GBS, 4),
-            "iteration_effective_gbs_credited": round(iter_bytes * it_per_s / 1e9, 1),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                # FETCH_SIZE / WRITE_SIZE count the L2 <-> fabric bytes: Infinity
-                # Cache (MALL) hits are in them. An image under 256 MB (100^3)
-                # may be served partly by the MALL, so "hbm" is its upper bound.
-                "traffic_note": "L2-fabric bytes (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE), Infinity Cache hits "
-                                "included",
-                "image_fits_infinity_cache": not bool(M.get_option("nt")),
-                "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
-                "kernel": "%s: %s + p.Ap%s" % (KERNEL_NAMES[kfmt], FORMAT_NAMES[kfmt],
-                                              " + p = r + beta p" if fused else ""),
-                "bytes_per_launch": format_bytes,
-                "bytes_formula": ("%g B per stored slot x %d slots + %d B per row (r, p_{k-1} read; p_k, Ap "
-                                  "written)" % (slot_bytes, slots, 32) if fused else
-                                  "%g B per stored slot x %d slots + 16 B per row (p read, Ap written)" %
-                                  (slot_bytes, slots)) +
-                                 (" + (16 + 8 q) / q B per row, q = %d (side blocks: x read and written, q p's read "
-                                  "for 1/q of the rows)" % q if xside else "") +
-                                 (" + 24 B per row (fused update blocks: r and Ap read, r written)" if fupd else ""),
-                "credited_bytes_per_launch": credited,
-                "credited_frac": round(credited / spmv_avg_s / 1e9 / HBM_PEAK_GBS, 4),
-                "credited_formula": "SURVEY 8(d): 12 nnz + 20 n (SpMV) + 16 n (ddot p.Ap)" +
-                                    (" + 24 n (waxpby p)" if fused else ""),
-                "avg_launch_us": round(spmv_avg_s * 1e6, 2),
-                "timing": timing_src,
-            },
-            # fused update: no update launch (its work is inside the SpMV launch above)
-            "update_kernel_avg_us": round(upd_ms / upd_n * 1e3, 2) if (upd_n and not fupd) else None,
-            "check": {"x_minus_xexact_inf": chk[0].item(), "final_normr_over_initial": chk[1].item(),
-                      "niters_per_solve": it},
-            # per-solve wall times on rank 0 (first/cold and median of the solves);
-            # event steps launch eagerly with hipEvents and are slower than the graph replays
-            "solve_ms": {"cold": round(cold_s * 1e3, 3) if cold_s is not None else None,
-                         "median": round(sorted(step_s)[len(step_s) // 2] * 1e3, 3),
-                         "min": round(min(step_s) * 1e3, 3), "max": round(max(step_s) * 1e3, 3),
-                         "median_graph_replay": round(sorted(step_s[args.event_steps:])[
-                             len(step_s[args.event_steps:]) // 2] * 1e3, 3)
-                         if len(step_s) > args.event_steps else None},
-            "times_per_step_s": {"total": times_acc[0] / args.steps, "ddot": times_acc[1] / args.steps,
-                                 "waxpby": times_acc[2] / args.steps, "sparsemv": times_acc[3] / args.steps,
-                                 "allreduce": times_acc[4] / args.steps, "halo": times_acc[5] / args.steps},
-            # rank 0's device stamps (HPCCG.cpp:71-72 classes t4, t5) per CG iteration
-            "per_iteration_us": {"allreduce": round(times_acc[4] / max(1, niters_total) * 1e6, 3),
-                                 "halo": round(times_acc[5] / max(1, niters_total) * 1e6, 3),
-                                 "total": round(elapsed / max(1, niters_total) * 1e6, 3)},
-            "runtime": rt,
-            "cpu_baseline": None,
-        }
-        if traffic:
-            out["roofline"]["traffic_gbs"] = round(traffic / spmv_avg_s / 1e9, 1)
-            out["roofline"]["traffic_frac"] = round(traffic / spmv_avg_s / 1e9 / HBM_PEAK_GBS, 4)
-        if world == 1 and not args.no_cpu_baseline:
+        cpu = None
+        if not args.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = cpu_baseline(n, n, n, use_7pt)
+                cpu = cpu_baseline(n, n, n, use_7pt) if world == 1 else \
+                    cpu_baseline_global(n, n, n * world, use_7pt, world)
             except Exception as e:  # reported, never silently replaced
-                out["cpu_baseline"] = {"error": repr(e)}
+                cpu = {"error": repr(e)}
+        out = build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt, ranks, cpu, secondary,
+                         placement_report(args.placement, probe_us, pick))
         print(json.dumps(out), flush=True)
-
-    M.close()
     if world > 1:
+        dist.barrier()  # rank 0's CPU leg runs while the others wait here
         hp.comm_destroy()
         dist.destroy_process_group()
     stage.done.set()

@@ -1,0 +1,108 @@
+"""bench.py's N > 1 line on CPU (gloo, world_size 2): the
+per-rank records travel to rank 0 through the same all-gather the GPU run
+uses (bench.gather_ranks), and the line assembled from them (bench.build_line)
+carries the driver's contract keys, the roofline and CPU-baseline objects,
+every rank's transport verdicts (peer_auto_ok / pull_auto_ok / proto_auto_ok,
+the transport actually used) and the max-over-ranks SpMV launch time with its
+compulsory fraction. The measured numbers are synthetic here; the GPU run
+fills the same fields."""
+import json
+import multiprocessing as mp
+import os
+import socket
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _FakeM:
+    def __init__(self, opts):
+        self.opts = opts
+
+    def get_option(self, k):
+        return self.opts[k]
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, ROOT)
+        import bench
+        transport = {"peer_allreduce": 1, "halo_pull": 2, "rhalo": 1, "fuse_update": 0, "peer_auto_ok": 1,
+                     "pull_auto_ok": 1, "proto_auto_ok": 1}
+        M = _FakeM(transport)
+        meas = {"spmv_avg_s": (340.0 + 10.0 * rank) * 1e-6, "local_elapsed": 3.5 + 0.01 * rank,
+                "times_acc": [3.5, 0.01, 0.2, 3.0, 0.004, 0.002, 0.0], "niters_total": 499 * 20}
+        rt = {"pci_bus_id": "0000:05:00.0", "rccl_nranks": 0}
+        ranks = bench.gather_ranks(dist, world, bench.rank_record(None, M, rank, 0, "host", rt, meas))
+        if rank == 0:
+            class A:
+                steps, warmup, max_iter, stencil = 20, 2, 500, 27
+            n = 200
+            info = {"nrow": n ** 3, "nnz": 213847192, "slots": 216006144}
+            full = dict(meas, elapsed=3.52, it=499, step_s=[0.176] * 20, cold_s=0.5, graph_used=1, upd_ms=31.0,
+                        upd_n=500, chk=[4e-15, 1e-70], steps=20, event_steps=1, timing_src="synthetic")
+            roof = {"bound": "hbm", "achieved": 6000.0, "peak": 8000.0, "unit": "GB/s", "frac": 0.75,
+                    "traffic": 2.04e9, "bytes_per_launch": 2.05e9, "avg_launch_us": 340.0}
+            cpu = {"value": 12.0, "unit": "CG iterations/s (global-problem iterations x 2 slabs)", "cores": 16,
+                   "kind": "reference", "sample": "synthetic"}
+            opts = dict(transport, device_bytes=4.2e9, fuse_p=1, fold=1, x_defer=2, x_ring=32, rev_update=1,
+                        overlap=0, graph_chunk=32, nt=1, a2_ring=3, nt_store=0)
+            line = bench.build_line(A, world, n, full, roof, 2, 3, 1, info, opts, dict(rt), ranks, cpu, None,
+                                    {"ran": False})
+            q.put(json.dumps(line))
+        else:
+            q.put(None)
+    except Exception as e:  # reported to the test
+        q.put(json.dumps({"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_multirank_line_schema():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    lines = [json.loads(g) for g in got if g is not None]
+    assert len(lines) == 1
+    d = lines[0]
+    assert "error" not in d, d
+    # the driver's contract
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["dtype"] == "f64" and d["higher_is_better"] is True
+    assert d["value"] == pytest.approx(499 * 20 / 3.52 * 2, rel=1e-6)
+    assert d["config"]["workload"].startswith("HPCCG solve, 27-pt 200x200x200 per GPU")
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in d["roofline"], k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in d["cpu_baseline"], k
+    # every rank's record, the transport verdicts and the slowest rank's launch
+    rk = d["runtime"]["ranks"]
+    assert [r["rank"] for r in rk] == [0, 1]
+    for r in rk:
+        assert r["transport"]["peer_auto_ok"] == 1 and r["transport"]["proto_auto_ok"] == 1
+    mr = d["multirank"]
+    assert mr["spmv_avg_us_max_over_ranks"] == pytest.approx(350.0) and mr["slowest_rank"] == 1
+    assert mr["frac_max_over_ranks"] == pytest.approx(2.05e9 / 350e-6 / 1e9 / 8000.0, rel=1e-3)
+    assert mr["transport_used"].startswith("in-kernel")
+    assert len(mr["verdicts_per_rank"]) == 2
