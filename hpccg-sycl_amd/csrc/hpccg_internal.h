@@ -112,6 +112,7 @@ struct CgArgs {
                                   // direct kernel); k lives in kst[0] / kst[2] by parity (kpar)
     int kpar;                     // fused update: parity of the iteration this launch runs
     int fu2;                      // fused update: two slices per update block (four rows per thread)
+    int resident;                 // fused update run by the resident pair kernel (k_spmv_ar, option resident_update)
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
@@ -244,6 +245,8 @@ constexpr int kA2RingDefault = 3;
 size_t a2_lds_bytes(int lds_doubles, int ring);
 int a2_ring_prepare();
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s);
+// k_spmv_ar blocks the whole chip holds at once (0: unknown)
+int resident_capacity(bool nt);
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);
 void launch_cg_end(const CgArgs& a, hipStream_t s);

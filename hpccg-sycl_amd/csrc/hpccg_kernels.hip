@@ -1405,6 +1405,180 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 }
 
 // ---------------------------------------------------------------------------
+// Resident fused update (option resident_update; one rank, direct kernel,
+// width 27): one 256-thread block per slice PAIR, four
+// rows per thread -- rows 2t, 2t + 1 of each slice, the direct kernel's rows,
+// both slices' loads interleaved in one slot loop -- and every unit block
+// resident at once (the host sizes the launch to the chip: hipOccupancy x
+// CUs >= units, else this kernel is not used). A block keeps its rows' Ap
+// and the r it read for p_k in registers, publishes its two p.Ap partials,
+// waits for the launch's p.Ap total (the pready slots the dot completion
+// fills) and applies the update itself: no Ap stream (stored, then read back
+// by update blocks) and no second read of r -- 24 B per row less than the
+// unit + update-block launch. Same expressions in the same order as the
+// direct kernel and fused_update (HPCCG.cpp:377-385): the same bits. The side
+// blocks (deferred x) trail the units as in every direct launch.
+// Co-residency is not promised by HIP: a launch that could not fit (another
+// process on the GPU) ends in the bounded pready wait, an error, not a hang.
+// ---------------------------------------------------------------------------
+// 4 blocks per CU (4 waves per SIMD, <= 128 VGPRs): 1024 resident blocks, the
+// 977 pair units of 100^3 fit at once.
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_spmv_ar(CgArgs a,
+                                                                                                  bool prologue)
+{
+    constexpr int kW = 27, kPre = 3, kStep = 2;  // kW - kPre slots in steps of kStep, loads of a step issued first
+    static_assert((kW - kPre) % kStep == 0, "slot steps");
+    if (side_flush<1, 4, true>(a, prologue)) return;
+    const int P = unit_of(a);
+    IterState st;
+    if (!spmv_begin<true, true, true>(a, prologue, st)) return;
+    if (P < 0) return;
+    const int s0 = 2 * P;
+    const int nsl = min(2, a.nslices - s0);
+    const int s1 = nsl > 1 ? s0 + 1 : s0;  // (an odd last slice: its twin repeats it, masked below)
+    const int lr = threadIdx.x * kRpt;     // row within each slice
+    const int row0 = s0 * kSliceRows + lr, row1 = s1 * kSliceRows + lr;
+    const double* __restrict__ vp0 = a.aval + (size_t)s0 * kW * kSliceRows + lr;
+    const double* __restrict__ vp1 = a.aval + (size_t)s1 * kW * kSliceRows + lr;
+    Rows pre0[kPre], pre1[kPre];
+#pragma unroll
+    for (int j = 0; j < kPre; j++) {
+        pre0[j] = ld_m<kNT>(vp0 + (size_t)j * kSliceRows);
+        pre1[j] = ld_m<kNT>(vp1 + (size_t)j * kSliceRows);
+    }
+    const int* __restrict__ off0 = a.aoff + (size_t)s0 * kAMax;
+    const int* __restrict__ off1 = a.aoff + (size_t)s1 * kAMax;
+    const double* __restrict__ r0 = a.r + row0;
+    const double* __restrict__ r1 = a.r + row1;
+    const double* __restrict__ pold = (st.k == 1) ? a.r : cur_p(a, st.k - 1);
+    const double* __restrict__ y0 = pold + row0;
+    const double* __restrict__ y1 = pold + row1;
+    double sum0[kRpt] = {0.0, 0.0}, sum1[kRpt] = {0.0, 0.0};
+    // one slot of both slices: x = r + beta p_{k-1} at the offset, in slot order
+    auto slot = [&](const Rows& v0, const Rows& v1, const Rows& ra, const Rows& ya, const Rows& rb, const Rows& yb) {
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            sum0[i] = sum0[i] + v0.v[i] * (ra.v[i] + st.beta * ya.v[i]);
+            sum1[i] = sum1[i] + v1.v[i] * (rb.v[i] + st.beta * yb.v[i]);
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < kPre; j++) {
+        const int o0 = sld(off0 + j), o1 = sld(off1 + j);
+        slot(pre0[j], pre1[j], ld_u(r0 + o0), ld_u(y0 + o0), ld_u(r1 + o1), ld_u(y1 + o1));
+    }
+#pragma unroll 1
+    for (int j0 = kPre; j0 < kW; j0 += kStep) {
+        Rows v0[kStep], v1[kStep], ra[kStep], ya[kStep], rb[kStep], yb[kStep];
+#pragma unroll
+        for (int u = 0; u < kStep; u++) {
+            const int o0 = sld(off0 + j0 + u), o1 = sld(off1 + j0 + u);
+            v0[u] = ld_m<kNT>(vp0 + (size_t)(j0 + u) * kSliceRows);
+            v1[u] = ld_m<kNT>(vp1 + (size_t)(j0 + u) * kSliceRows);
+            ra[u] = ld_u(r0 + o0);
+            ya[u] = ld_u(y0 + o0);
+            rb[u] = ld_u(r1 + o1);
+            yb[u] = ld_u(y1 + o1);
+        }
+#pragma unroll
+        for (int u = 0; u < kStep; u++) slot(v0[u], v1[u], ra[u], ya[u], rb[u], yb[u]);
+    }
+    // p_k at the rows (k_p_update's expression), kept with r for the update
+    const Rows rv0 = ld(a.r + row0), rv1 = ld(a.r + row1);
+    const Rows yv0 = ld(pold + row0), yv1 = ld(pold + row1);
+    Rows pk0, pk1;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) {
+        pk0.v[i] = rv0.v[i] + st.beta * yv0.v[i];
+        pk1.v[i] = rv1.v[i] + st.beta * yv1.v[i];
+    }
+    double* __restrict__ p = cur_p(a, st.k);
+    st_vec(a, p, row0, pk0);
+    if (nsl > 1) st_vec(a, p, row1, pk1);
+    double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) {
+        if (row0 + i < a.n) d0 += pk0.v[i] * sum0[i];
+        if (nsl > 1 && row1 + i < a.n) d1 += pk1.v[i] * sum1[i];
+    }
+    // the two slices' p.Ap partials with block_sum<256>'s shape
+    __shared__ double ws2[2][kBlock / kWave];
+    __shared__ double pap_s;
+    __shared__ int gave_up;
+    const int lane = threadIdx.x & (kWave - 1);
+    const double w0 = wave_sum(d0), w1 = wave_sum(d1);
+    if (lane == 0) {
+        ws2[0][threadIdx.x / kWave] = w0;
+        ws2[1][threadIdx.x / kWave] = w1;
+    }
+    __syncthreads();
+    if (threadIdx.x < kWave) {
+        double bsj = 0.0;  // lane j: slice s0 + j's partial
+        if (lane < 2) {
+#pragma unroll
+            for (int i = 0; i < kBlock / kWave; i++) bsj += ws2[lane][i];
+        }
+        complete_dot_lanes(a, spmv_units(a, 2), P, s0, nsl, bsj, kPAP, st.k);
+    }
+    // the launch's p.Ap total (every unit block is resident: no wait depends
+    // on a block that has not started)
+    if (threadIdx.x == 0) {
+        double v;
+        const double* slot = a.pready + kReadyStride * (blockIdx.x % kNumXcd);
+        unsigned t0 = 0, polls = 0;
+        int bail = 0;
+        while (!slot_full(v = ld_sc1(slot))) {
+            if ((++polls & 15) == 0 && wait_expired(a, t0)) {
+                abort_solve(a, kErrReadyWait, blockIdx.x % kNumXcd, st.k, kPAP);
+                bail = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+        pap_s = v;
+        gave_up = bail;
+    }
+    __syncthreads();
+    if (gave_up) return;
+    const double alpha = st.rr / pap_s;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.ahist[st.k] = alpha;
+        stamp(a, st.k, kStampUpdate);
+    }
+    // r = r - alpha Ap (fused_update's expression) and the r.r partials
+    Rows rn0, rn1;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) {
+        rn0.v[i] = rv0.v[i] + (-alpha) * sum0[i];
+        rn1.v[i] = rv1.v[i] + (-alpha) * sum1[i];
+    }
+    st_vec(a, a.r, row0, rn0);
+    if (nsl > 1) st_vec(a, a.r, row1, rn1);
+    double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRpt; i++) {
+        if (row0 + i < a.n) e0 += rn0.v[i] * rn0.v[i];
+        if (nsl > 1 && row1 + i < a.n) e1 += rn1.v[i] * rn1.v[i];
+    }
+    const double x0 = wave_sum(e0), x1 = wave_sum(e1);
+    __syncthreads();  // (ws2 reused)
+    if (lane == 0) {
+        ws2[0][threadIdx.x / kWave] = x0;
+        ws2[1][threadIdx.x / kWave] = x1;
+    }
+    __syncthreads();
+    if (threadIdx.x >= kWave) return;
+    double bsj = 0.0;
+    if (lane < 2) {
+#pragma unroll
+        for (int i = 0; i < kBlock / kWave; i++) bsj += ws2[lane][i];
+    }
+    complete_dot_lanes(a, spmv_units(a, 2), P, s0, nsl, bsj, kRR, st.k);
+}
+
+
+// ---------------------------------------------------------------------------
 // SELL-512-A with x from LDS windows shared by slice pairs: block P owns
 // slices 2P and 2P + 1 with 512 threads (waves 0-3 slice 2P, 4-7 slice
 // 2P + 1, two rows per thread). The pair's windows (one per offset cluster:
@@ -2387,6 +2561,21 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
     const int nghost = (fuse && a.rhalo && gmax > 0) ? (gmax + 4 * gthreads - 1) / (4 * gthreads) : 0;
     CgArgs b = a;
     b.send = a.sgrid + nside;
+    // resident fused update (k_spmv_ar, width 27): [pair units | side blocks]
+    if (fu && a.resident && a.a_width == 27 && kernel == kSpmvDirect) {
+        const int pairs = (a.nslices + 1) / 2;
+        b.s0 = 0;
+        b.sn0 = pairs;
+        b.s1 = b.sn1 = 0;
+        b.sgrid = (pairs + kNumXcd - 1) / kNumXcd * kNumXcd;
+        b.send = b.sgrid + nside;
+        b.ubase = b.gbase = INT_MAX;
+        if (a.nt)
+            hipLaunchKernelGGL(k_spmv_ar<true>, dim3(b.send), dim3(kBlock), 0, s, b, prologue);
+        else
+            hipLaunchKernelGGL(k_spmv_ar<false>, dim3(b.send), dim3(kBlock), 0, s, b, prologue);
+        return;
+    }
     // update units: one slice per block, or two (a.fu2: four rows per thread)
     const int ugrid = a.fu2 ? (((a.nslices + 1) / 2 + kNumXcd - 1) / kNumXcd * kNumXcd) : a.grid;
     // fused update: [units | side | pad to kNumXcd | update | ghost]; else [units | side | ghost]
@@ -2502,6 +2691,18 @@ int slot_plan(int units, int grid, int spu, int rev, int* last_unit, int* top)
 void launch_stream_a(const CgArgs& a, hipStream_t s)
 {
     hipLaunchKernelGGL(k_stream_a, dim3(a.grid), dim3(kBlock), 0, s, a);
+}
+
+// Blocks of k_spmv_ar the whole chip holds at once (the host's residency check).
+int resident_capacity(bool nt)
+{
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    const hipError_t e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spmv_ar<true>, kBlock, 0)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spmv_ar<false>, kBlock, 0);
+    return e == hipSuccess ? per_cu * cus : 0;
 }
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)

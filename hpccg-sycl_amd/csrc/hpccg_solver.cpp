@@ -289,6 +289,7 @@ struct hpccg_hip_matrix {
     int fuse_p = -1;      // -1 auto: on where the kernel forms p_k itself
     int fuse_update = -1; // the update as trailing blocks of the SpMV launch; -1 auto (fuse_update_effective)
     int fused_update_slices = 2;  // slices per update block of the fused update (1 or 2)
+    int resident_update = 0;      // the fused update by the resident pair kernel (k_spmv_ar; resident_of)
     size_t npartial = 0;  // dot slots (the last one: the fused update's p.Ap total)
     int a_pre = -1;       // direct kernel prefetch depth (-1 auto: 4 at width 27, 7 at width 7)
     int lds_ep = 1;       // pair kernel: own p_k from the staged window
@@ -414,8 +415,8 @@ namespace {
 constexpr size_t kCanaryBytes = size_t(64) << 10;
 constexpr unsigned kCanaryWord = 0x7FF5C0DEu;
 struct CanaryRec {
-    char* base;    // the allocation: [canary | user bytes | canary]
-    size_t bytes;  // user bytes
+    char* base;    // the allocation: [canary | user bytes, rounded up to 256 B | canary]
+    size_t bytes;  // user bytes rounded up to 256 (the tail canary's offset: dword-aligned for its fill)
 };
 std::mutex g_canary_mu;
 std::unordered_map<void*, CanaryRec> g_canary;  // user pointer -> allocation
@@ -439,6 +440,7 @@ hipError_t big_malloc(void** p, size_t b, unsigned flags = hipDeviceMallocDefaul
 {
     if (!canary_on()) return flags == hipDeviceMallocDefault ? hipMalloc(p, b) : hipExtMallocWithFlags(p, b, flags);
     void* base = nullptr;
+    b = (b + 255) & ~size_t(255);  // (a byte-sized buffer would leave the tail canary unaligned)
     const size_t tot = b + 2 * kCanaryBytes;
     hipError_t e = flags == hipDeviceMallocDefault ? hipMalloc(&base, tot) : hipExtMallocWithFlags(&base, tot, flags);
     if (e != hipSuccess) return e;
@@ -1430,6 +1432,19 @@ bool fuse_update_effective(const hpccg_hip_matrix* M)
            x_defer_effective(M) == 2;
 }
 
+// Option resident_update (opt-in): one rank, the direct
+// kernel at width 27 with the fused update, and the chip holds every pair
+// unit of the launch at once (hipOccupancy x CUs), else the unit +
+// update-block launch stays.
+bool resident_of(const hpccg_hip_matrix* M)
+{
+    if (!M->resident_update || M->nranks != 1 || M->force_comm || M->in_group || M->kernel != kSpmvDirect ||
+        M->a_width != 27 || !fuse_update_effective(M))
+        return false;
+    const int pairs = (M->nslices + 1) / 2;
+    return resident_capacity(image_big(M)) >= grid_of(pairs);
+}
+
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
 {
     CgArgs a;
@@ -1452,6 +1467,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.xside = 1;
     a.fupd = fuse_update_effective(M) ? 1 : 0;
     a.fu2 = M->fused_update_slices == 2 ? 1 : 0;
+    a.resident = a.fupd && resident_of(M) ? 1 : 0;
     a.pready = M->d_partial + (M->npartial - kNumXcd * kReadyStride);
     a.rev = M->rev_update ? 1 : 0;
     a.nring = a.xdefer ? x_ring_effective(M) : (a.fuse_p ? 2 : 1);
@@ -3768,6 +3784,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
         M->fused_update_slices = (int)value;
     } else if (!std::strcmp(key, "fuse_update")) {
         M->fuse_update = value < 0 ? -1 : (value > 2 ? 2 : (int)value);
+    } else if (!std::strcmp(key, "resident_update")) {
+        M->resident_update = value ? 1 : 0;
     } else if (!std::strcmp(key, "rev_update")) {
         M->rev_update = (int)value;
     } else if (!std::strcmp(key, "overlap")) {
@@ -3857,6 +3875,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "fuse_update")) *value = fuse_update_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "fused_update_slices")) *value = M->fused_update_slices;
+    else if (!std::strcmp(key, "resident_update")) *value = resident_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
     else if (!std::strcmp(key, "graph_chunk")) {  // effective: see graph_chunk_of
         long long c = std::max(1, M->graph_iters);

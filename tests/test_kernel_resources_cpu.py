@@ -31,6 +31,10 @@ BUDGETS = {
     "k_spmv_a<27, false, true, 4, false, false, false>": 72,
     "k_spmv_a<7, true, true, 7, true, false, false>": 80,
     "k_update<false>": 64,
+    # option resident_update: 4 waves per SIMD, so 1024 resident blocks hold
+    # the 977 pair units of 100^3 at once (the host also checks occupancy)
+    "k_spmv_ar<false>": 128,
+    "k_spmv_ar<true>": 128,
 }
 
 
