@@ -78,13 +78,15 @@ os.environ.setdefault("OMP_PLACES", "cores")
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 COPY_CEILING_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy, measured
-KERNEL_NAMES = {0: "k_spmv_sell", 1: "k_spmv_a", 2: "k_spmv_a2", 3: "k_spmv_a2r"}
+KERNEL_NAMES = {0: "k_spmv_sell", 1: "k_spmv_a", 2: "k_spmv_a2", 3: "k_spmv_a2r", 4: "k_spmv_ar"}
 FORMAT_NAMES = {0: "SELL-512 (8 B value + 4 B int32 column per slot)",
                 1: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets",
                 2: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice "
                    "pairs",
                 3: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice "
-                   "pairs, values streamed HBM -> LDS by per-wave LDS-DMA rings"}
+                   "pairs, values streamed HBM -> LDS by per-wave LDS-DMA rings",
+                4: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets, one "
+                   "block per slice pair, every block resident: the update applied from registers (no Ap stream)"}
 
 
 def load_pkg():
@@ -205,7 +207,7 @@ def cpu_baseline(nx, ny, nz, use_7pt, budget_s=15.0, budget_1t_s=10.0):
     return out
 
 
-def pmc_traffic(tag, kernel, fused, xdefer, fupd):
+def pmc_traffic(tag, kernel, fused, xdefer, fupd, resident=0):
     """HBM bytes per SpMV launch from the committed rocprofv3 FETCH/WRITE
     passes of the same kernel configuration (profiles/pmc_<tag>.json; matched
     by kernel template name, fusion and x deferral), else (None, None)."""
@@ -216,7 +218,7 @@ def pmc_traffic(tag, kernel, fused, xdefer, fupd):
         d = json.load(f)
     name = d.get("kernel", "")
     if KERNEL_NAMES[kernel] + "<" not in name or bool(d.get("fuse_p")) != bool(fused) or \
-            d.get("x_defer", 1) != xdefer or d.get("fuse_update", 0) != fupd:
+            d.get("x_defer", 1) != xdefer or d.get("fuse_update", 0) != fupd or d.get("resident_update", 0) != resident:
         return None, None
     return d.get("spmv_hbm_bytes_per_launch"), f"profiles/pmc_{tag}.json ({d.get('tag', '?')}), matched by kernel name"
 
@@ -427,6 +429,9 @@ def roofline_of(M, n, stencil, spmv_avg_s):
     nrow = info["nrow"]
     kernel = M.get_option("spmv_kernel")
     kfmt = 3 if (kernel == 2 and M.get_option("a2_ring") > 0) else kernel  # 3: the pair kernel's LDS-DMA ring form
+    resident = opt_or_none(M, "resident_update") == 1
+    if resident:
+        kfmt = 4  # the resident pair kernel (k_spmv_ar)
     fused = M.get_option("fuse_p")
     slots = info["slots"]
     # bytes the SpMV must move in its format: the stored slots (8 B; SELL-512
@@ -438,16 +443,17 @@ def roofline_of(M, n, stencil, spmv_avg_s):
     xside = M.get_option("x_defer") == 2
     q = M.get_option("x_ring") - 1
     side_bytes = (16.0 + 8.0 * q) / q * nrow if xside else 0.0
-    # fused update: the launch's trailing blocks also run the update (r, Ap read; r written)
+    # fused update: the launch's trailing blocks also run the update (r, Ap read; r written);
+    # resident: the units apply it from registers -- r written instead of Ap, nothing read back
     fupd = M.get_option("fuse_update") == 1
-    upd_bytes = 24.0 * nrow if fupd else 0.0
+    upd_bytes = 24.0 * nrow if (fupd and not resident) else 0.0
     format_bytes = slot_bytes * slots + vec_bytes + side_bytes + upd_bytes
     # SURVEY 8(d) credited bytes: HPC_sparsemv 12 nnz + 20 n, ddot(p, Ap) 16 n,
     # with the fused p update the waxpby p = r + beta p, 24 n
     credited = 12.0 * info["nnz"] + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fused else 0.0)
     achieved = format_bytes / spmv_avg_s / 1e9
     traffic, traffic_src = pmc_traffic(f"spmv_{stencil}pt_{n}", kfmt, fused, M.get_option("x_defer"),
-                                       M.get_option("fuse_update"))
+                                       M.get_option("fuse_update"), 1 if resident else 0)
     roof = {
         "bound": "hbm",
         "achieved": round(achieved, 1),
@@ -465,12 +471,15 @@ def roofline_of(M, n, stencil, spmv_avg_s):
         "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
         "kernel": "%s: %s + p.Ap%s" % (KERNEL_NAMES[kfmt], FORMAT_NAMES[kfmt], " + p = r + beta p" if fused else ""),
         "bytes_per_launch": format_bytes,
-        "bytes_formula": ("%g B per stored slot x %d slots + %d B per row (r, p_{k-1} read; p_k, Ap "
+        "bytes_formula": ("%g B per stored slot x %d slots + 32 B per row (r, p_{k-1} read; p_k, r "
+                          "written; Ap and the update stay in registers)" % (slot_bytes, slots) if resident else
+                          "%g B per stored slot x %d slots + %d B per row (r, p_{k-1} read; p_k, Ap "
                           "written)" % (slot_bytes, slots, 32) if fused else
                           "%g B per stored slot x %d slots + 16 B per row (p read, Ap written)" % (slot_bytes, slots)) +
                          (" + (16 + 8 q) / q B per row, q = %d (side blocks: x read and written, q p's read "
                           "for 1/q of the rows)" % q if xside else "") +
-                         (" + 24 B per row (fused update blocks: r and Ap read, r written)" if fupd else ""),
+                         (" + 24 B per row (fused update blocks: r and Ap read, r written)"
+                          if (fupd and not resident) else ""),
         # SURVEY 8(d)'s fixed byte formula for the unfused reference sequence
         # this launch replaces (more bytes than this format moves; no rate is
         # derived from it: `frac` above is the roofline fraction)
@@ -584,7 +593,7 @@ def build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt
             "placement_probe": probe_report,
             "options": {k: M_opts.get(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update", "overlap",
                                                    "graph_chunk", "nt", "a2_ring", "nt_store", "fuse_update", "rhalo",
-                                                   "peer_allreduce", "halo_pull")},
+                                                   "peer_allreduce", "halo_pull", "resident_update")},
         },
         "cg_iterations_per_s_global": round(it_per_s, 3),
         "spmv_effective_gbs": roof["achieved"],
@@ -725,7 +734,7 @@ def main():
     roof, kernel, kfmt, fused, fupd = roofline_of(M, n, args.stencil, meas["spmv_avg_s"])
     M_opts = {k: opt_or_none(M, k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update", "overlap",
                                              "graph_chunk", "nt", "a2_ring", "nt_store", "fuse_update", "rhalo",
-                                             "peer_allreduce", "halo_pull", "device_bytes")}
+                                             "peer_allreduce", "halo_pull", "device_bytes", "resident_update")}
     ranks = gather_ranks(dist, world, rank_record(hp, M, rank, dev, comm, rt, meas))
     if world > 1:
         rt["pci_bus_ids"] = [r["pci_bus_id"] for r in ranks]

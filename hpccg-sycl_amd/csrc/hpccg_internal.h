@@ -113,6 +113,7 @@ struct CgArgs {
     int kpar;                     // fused update: parity of the iteration this launch runs
     int fu2;                      // fused update: two slices per update block (four rows per thread)
     int resident;                 // fused update run by the resident pair kernel (k_spmv_ar, option resident_update)
+    int dbg_resident_stall;       // debug (retry test): k_spmv_ar's p.Ap wait never sees the total (it expires)
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off

@@ -1528,7 +1528,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
         const double* slot = a.pready + kReadyStride * (blockIdx.x % kNumXcd);
         unsigned t0 = 0, polls = 0;
         int bail = 0;
-        while (!slot_full(v = ld_sc1(slot))) {
+        // (dbg_resident_stall: the wait of a launch that could not be resident)
+        while (!slot_full(v = ld_sc1(slot)) || a.dbg_resident_stall) {
             if ((++polls & 15) == 0 && wait_expired(a, t0)) {
                 abort_solve(a, kErrReadyWait, blockIdx.x % kNumXcd, st.k, kPAP);
                 bail = 1;

@@ -289,7 +289,10 @@ struct hpccg_hip_matrix {
     int fuse_p = -1;      // -1 auto: on where the kernel forms p_k itself
     int fuse_update = -1; // the update as trailing blocks of the SpMV launch; -1 auto (fuse_update_effective)
     int fused_update_slices = 2;  // slices per update block of the fused update (1 or 2)
-    int resident_update = 0;      // the fused update by the resident pair kernel (k_spmv_ar; resident_of)
+    int resident_update = -1;     // the fused update by the resident pair kernel (k_spmv_ar; resident_of)
+    int resident_failed = 0;      // a resident launch's wait expired (GPU shared): the unit + update launch from then on
+    int resident_used = 0;        // the last solve ran k_spmv_ar
+    int last_dev_err = 0;         // the device error code the last failed solve recorded (DevError)
     size_t npartial = 0;  // dot slots (the last one: the fused update's p.Ap total)
     int a_pre = -1;       // direct kernel prefetch depth (-1 auto: 4 at width 27, 7 at width 7)
     int lds_ep = 1;       // pair kernel: own p_k from the staged window
@@ -341,6 +344,7 @@ struct hpccg_hip_matrix {
     int* d_kst = nullptr;      // [0, kErrBase) iteration state, then the device error record (kErrWords)
     long long spin_us = kSpinTicksDefault / 100;  // bound of every in-kernel wait (option spin_budget_us)
     int dbg_withhold = 0;      // debug: slice + 1 whose p.Ap partial is withheld (guard test)
+    int dbg_resident_stall = 0;  // debug: k_spmv_ar's p.Ap wait expires (the retry test)
     unsigned long long* d_tl = nullptr;  // diagnostics (dbg_timeline): per unit kTlWords block stamps
     int tl_units = 0;
     int solve_dirty = 0;       // a solve started and did not finish cleanly: reset the dot slots first
@@ -1432,14 +1436,19 @@ bool fuse_update_effective(const hpccg_hip_matrix* M)
            x_defer_effective(M) == 2;
 }
 
-// Option resident_update (opt-in): one rank, the direct
-// kernel at width 27 with the fused update, and the chip holds every pair
-// unit of the launch at once (hipOccupancy x CUs), else the unit +
-// update-block launch stays.
+// Option resident_update (-1 auto, the default; 0 off):
+// one rank, the direct kernel at width 27 with the fused update, and the chip
+// holds every pair unit of the launch at once (hipOccupancy x CUs: 27-pt up
+// to ~101^3), else the unit + update-block launch stays. 100^3, alternating
+// processes, 3 rounds: 19.6-19.8k -> 20.8-21.2k CG it/s, SpMV launch 49.3-49.8
+// -> 46.1-46.9 us (profiles/r05_ab/resident_update_ab100.log). A solve whose
+// resident wait expired (another process holding part of the GPU) is re-run
+// without it, and the matrix keeps the other launch (resident_retry). Not
+// with the block-timeline diagnostics (their instantiation is the other launch).
 bool resident_of(const hpccg_hip_matrix* M)
 {
-    if (!M->resident_update || M->nranks != 1 || M->force_comm || M->in_group || M->kernel != kSpmvDirect ||
-        M->a_width != 27 || !fuse_update_effective(M))
+    if (!M->resident_update || M->resident_failed || M->d_tl || M->nranks != 1 || M->force_comm || M->in_group ||
+        M->kernel != kSpmvDirect || M->a_width != 27 || !fuse_update_effective(M))
         return false;
     const int pairs = (M->nslices + 1) / 2;
     return resident_capacity(image_big(M)) >= grid_of(pairs);
@@ -1489,6 +1498,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.hist = M->d_hist;
     a.kst = M->d_kst;
     a.dbg_withhold = M->dbg_withhold;
+    a.dbg_resident_stall = M->dbg_resident_stall;
     a.dbg_tl = M->d_tl;
     a.rhalo = rhalo_of(M) ? 1 : 0;
     a.ghost_hi = M->ghost_hi;
@@ -2724,6 +2734,7 @@ int check_device_error(hpccg_hip_matrix* const* Ms, int P, const int* err0)
         if (e[0] != kErrNone || (P == 1 && e[kErrAllRanks] != kErrNone)) bad_rank = r;
     }
     if (bad_rank < 0) return 0;
+    for (int r = 0; r < P; r++) Ms[r]->last_dev_err = e[0] != kErrNone ? e[0] : e[kErrAllRanks];
     for (int r = 0; r < P; r++) {
         TRY(reset_dot_state(Ms[r]));
         Ms[r]->solve_dirty = 0;  // reset here (a second reset at the next solve's start could empty a slot a
@@ -2882,6 +2893,8 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
         }
     }
     for (int r = 0; r < P; r++) Ms[r]->gfold_used = av[0].gn > 0 ? 1 : 0;
+    M->resident_used = av[0].resident;
+    M->last_dev_err = 0;
     const Ranks R{Ms, av.data(), P, gev.data()};
     if (events) TRY(ensure_events(M, iters + 1));
     TRY(enqueue_prologue(R, events));
@@ -3026,6 +3039,21 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
         }
     }
     return 0;
+}
+
+// The resident fused update waits inside its launch for blocks HIP does not
+// promise to run at the same time: with another process holding part of the
+// GPU its p.Ap wait can expire. Such a solve is re-run from the caller's
+// inputs with the unit + update-block launch, which needs no co-residency
+// (every wait there is on blocks dispatched earlier), and the matrix keeps
+// that launch.
+bool resident_retry(hpccg_hip_matrix* M, int rc)
+{
+    if (rc != HPCCG_HIP_EHIP || !M->resident_used || M->last_dev_err != kErrReadyWait) return false;
+    M->resident_failed = 1;
+    std::fprintf(stderr, "hpccg_hip: the resident update's wait expired (a shared GPU?); the solve is re-run with "
+                         "the unit + update-block launch, which this matrix keeps\n");
+    return true;
 }
 
 int solve_impl(hpccg_hip_matrix* M, const double* b_dev, double* x_dev, int max_iter, double tol, int* niters_out,
@@ -3785,7 +3813,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "fuse_update")) {
         M->fuse_update = value < 0 ? -1 : (value > 2 ? 2 : (int)value);
     } else if (!std::strcmp(key, "resident_update")) {
-        M->resident_update = value ? 1 : 0;
+        M->resident_update = value < 0 ? -1 : (value ? 1 : 0);
+        if (value) M->resident_failed = 0;
     } else if (!std::strcmp(key, "rev_update")) {
         M->rev_update = (int)value;
     } else if (!std::strcmp(key, "overlap")) {
@@ -3844,6 +3873,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
             M->tl_units = 3 * M->nslices + 1024;  // >= the blocks of any SpMV launch (units, side, ghost, update)
             TRY(dev_alloc(M, &M->d_tl, (size_t)M->tl_units * kTlWords, true));
         }  // the graph cache compares the kernel arguments: a changed dbg_tl re-captures
+    } else if (!std::strcmp(key, "dbg_resident_stall")) {
+        M->dbg_resident_stall = value ? 1 : 0;
     } else if (!std::strcmp(key, "dbg_withhold")) {
         if (value < 0 || value > M->nslices) return set_err(HPCCG_HIP_EINVAL, "dbg_withhold must be 0..nslices");
         M->dbg_withhold = (int)value;
@@ -3943,7 +3974,12 @@ int hpccg_hip_solve_device(hpccg_hip_matrix* M, const double* b_dev, double* x_d
         HIP_TRY(hipMemcpyAsync(M->d_b, b_dev, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
         b = M->d_b;
     }
-    TRY(solve_impl(M, b, x, max_iter, tolerance, niters, normr, times, print));
+    int rc = solve_impl(M, b, x, max_iter, tolerance, niters, normr, times, print);
+    if (resident_retry(M, rc)) {  // from x_dev again
+        HIP_TRY(hipMemcpyAsync(x, x_dev, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
+        rc = solve_impl(M, b, x, max_iter, tolerance, niters, normr, times, print);
+    }
+    TRY(rc);
     HIP_TRY(hipMemcpyAsync(x_dev, x, sizeof(double) * M->nrow, hipMemcpyDeviceToDevice, M->stream));
     return wait_matrix(M);
 }
@@ -3958,7 +3994,13 @@ int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_ite
     HIP_TRY(hipMemcpyAsync(M->d_x, x, sizeof(double) * M->nrow, hipMemcpyHostToDevice, M->stream));
     HIP_TRY(hipStreamSynchronize(M->stream));
     const double setup = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    TRY(solve_impl(M, M->d_b, M->d_x, max_iter, tolerance, niters, normr, times, print));
+    int rc = solve_impl(M, M->d_b, M->d_x, max_iter, tolerance, niters, normr, times, print);
+    if (resident_retry(M, rc)) {  // from the caller's x again
+        HIP_TRY(hipMemcpyAsync(M->d_x, x, sizeof(double) * M->nrow, hipMemcpyHostToDevice, M->stream));
+        HIP_TRY(hipStreamSynchronize(M->stream));
+        rc = solve_impl(M, M->d_b, M->d_x, max_iter, tolerance, niters, normr, times, print);
+    }
+    TRY(rc);
     HIP_TRY(hipMemcpy(x, M->d_x, sizeof(double) * M->nrow, hipMemcpyDeviceToHost));
     if (times) times[6] = setup;
     return 0;

@@ -22,7 +22,9 @@ S=${STENCIL:-27}
 # the committed bench line comes from this same process (same allocations as
 # the kernel stats: the per-process placement spread, DESIGN.md 4, cannot
 # separate the two), CPU baseline included
-step stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --stencil $S
+# (the headline config's line carries the secondary configs, as the driver's does)
+SEC=""; [ "$N" = 200 ] && [ "$S" = 27 ] || SEC="--no-secondary"
+step stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -- python bench.py --n $N --stencil $S $SEC
 step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python tools/pmc_workload.py --n $N --stencil $S
 step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -- python tools/pmc_workload.py --n $N --stencil $S
 find $OUT -name "*.csv" | head -20

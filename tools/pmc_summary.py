@@ -29,6 +29,8 @@ FORMATS = {
     "k_spmv_a2": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice pairs",
     "k_spmv_a2r": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice pairs, "
                   "values streamed HBM -> LDS by per-wave LDS-DMA rings",
+    "k_spmv_ar": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets, one block "
+                 "per slice pair, every block resident: the update applied from registers (no Ap stream)",
 }
 
 
@@ -87,7 +89,7 @@ def main():
     f_stream, _ = pick(fetch, "k_stream_a", "FETCH_SIZE")
     w_stream, _ = pick(write, "k_stream_a", "WRITE_SIZE")
     fetch_factor = stream_read / (f_stream * 1024.0)
-    SPMV = ("k_spmv_sell<", "k_spmv_a<", "k_spmv_a2<", "k_spmv_a2r<")
+    SPMV = ("k_spmv_sell<", "k_spmv_a<", "k_spmv_a2<", "k_spmv_a2r<", "k_spmv_ar<")
     f_spmv, kname = pick(fetch, SPMV, "FETCH_SIZE")
     w_spmv, _ = pick(write, SPMV, "WRITE_SIZE")
     spmv_read = f_spmv * 1024.0 * fetch_factor
@@ -101,6 +103,8 @@ def main():
         fuse_p = targs[0].strip() == "true"
     elif "k_spmv_a2<" in kname:
         fuse_p = targs[1].strip() == "true"
+    elif "k_spmv_ar<" in kname:  # k_spmv_ar<kNT>: always fused (p and the update)
+        fuse_p = True
     else:
         fuse_p = False
     algo = 12.0 * nnz + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fuse_p else 0.0)
@@ -120,7 +124,10 @@ def main():
         launches = len(fetch[(kname, "FETCH_SIZE")])
         side = (16.0 + 8.0 * q) / q * nrow * (launches - 1) / launches
         compulsory += side
-    upd = 24.0 * nrow if opts.get("fuse_update") == 1 else 0.0  # fused update blocks: r, Ap read; r written
+    resident = "k_spmv_ar<" in kname
+    # fused update blocks: r, Ap read; r written (resident: applied from registers, r written
+    # instead of Ap -- the same 32 B per row as above, nothing more)
+    upd = 24.0 * nrow if (opts.get("fuse_update") == 1 and not resident) else 0.0
     compulsory += upd
 
     avg_ns = None
@@ -142,6 +149,7 @@ def main():
         "side_flush_bytes_per_launch": side,
         "fuse_update": opts.get("fuse_update", 0),
         "fused_update_bytes_per_launch": upd,
+        "resident_update": 1 if resident else 0,
         "fetch_size_kib_raw": f_spmv,
         "write_size_kib_raw": w_spmv,
         "fetch_calibration": {"kernel": "k_stream_a", "known_read_bytes": stream_read,
