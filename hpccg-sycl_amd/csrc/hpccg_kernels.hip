@@ -1423,11 +1423,11 @@ __global__ __launch_bounds__(kBlock) void k_spmv_a(CgArgs a, bool prologue)
 // ---------------------------------------------------------------------------
 // 4 blocks per CU (4 waves per SIMD, <= 128 VGPRs): 1024 resident blocks, the
 // 977 pair units of 100^3 fit at once.
-template <bool kNT>
+template <bool kNT, int kPre = 3, int kStep = 2>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_spmv_ar(CgArgs a,
                                                                                                   bool prologue)
 {
-    constexpr int kW = 27, kPre = 3, kStep = 2;  // kW - kPre slots in steps of kStep, loads of a step issued first
+    constexpr int kW = 27;  // kPre early slots, then kW - kPre slots in steps of kStep, a step's loads issued first
     static_assert((kW - kPre) % kStep == 0, "slot steps");
     if (side_flush<1, 4, true>(a, prologue)) return;
     const int P = unit_of(a);
@@ -2571,10 +2571,22 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         b.sgrid = (pairs + kNumXcd - 1) / kNumXcd * kNumXcd;
         b.send = b.sgrid + nside;
         b.ubase = b.gbase = INT_MAX;
-        if (a.nt)
-            hipLaunchKernelGGL(k_spmv_ar<true>, dim3(b.send), dim3(kBlock), 0, s, b, prologue);
-        else
-            hipLaunchKernelGGL(k_spmv_ar<false>, dim3(b.send), dim3(kBlock), 0, s, b, prologue);
+        // (a.resident - 1: the slot-loop shape, option resident_update 1..5; 1 and auto: 3 early, steps of 2)
+#define HPCCG_AR(PRE, STEP)                                                                                      \
+    do {                                                                                                         \
+        if (a.nt)                                                                                                \
+            hipLaunchKernelGGL((k_spmv_ar<true, PRE, STEP>), dim3(b.send), dim3(kBlock), 0, s, b, prologue);   \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_spmv_ar<false, PRE, STEP>), dim3(b.send), dim3(kBlock), 0, s, b, prologue);  \
+    } while (0)
+        switch (a.resident) {
+        case 2: HPCCG_AR(3, 3); break;
+        case 3: HPCCG_AR(3, 4); break;
+        case 4: HPCCG_AR(7, 4); break;
+        case 5: HPCCG_AR(7, 2); break;
+        default: HPCCG_AR(3, 2); break;
+        }
+#undef HPCCG_AR
         return;
     }
     // update units: one slice per block, or two (a.fu2: four rows per thread)

@@ -1476,7 +1476,8 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.xside = 1;
     a.fupd = fuse_update_effective(M) ? 1 : 0;
     a.fu2 = M->fused_update_slices == 2 ? 1 : 0;
-    a.resident = a.fupd && resident_of(M) ? 1 : 0;
+    // (1 + the slot-loop shape: option resident_update 2..5 pick the A/B variants of k_spmv_ar)
+    a.resident = a.fupd && resident_of(M) ? (M->resident_update > 1 ? M->resident_update : 1) : 0;
     a.pready = M->d_partial + (M->npartial - kNumXcd * kReadyStride);
     a.rev = M->rev_update ? 1 : 0;
     a.nring = a.xdefer ? x_ring_effective(M) : (a.fuse_p ? 2 : 1);
@@ -3813,7 +3814,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "fuse_update")) {
         M->fuse_update = value < 0 ? -1 : (value > 2 ? 2 : (int)value);
     } else if (!std::strcmp(key, "resident_update")) {
-        M->resident_update = value < 0 ? -1 : (value ? 1 : 0);
+        if (value < -1 || value > 5) return set_err(HPCCG_HIP_EINVAL, "resident_update: -1 (auto), 0, 1 or 2..5 (shapes)");
+        M->resident_update = (int)value;
         if (value) M->resident_failed = 0;
     } else if (!std::strcmp(key, "rev_update")) {
         M->rev_update = (int)value;

@@ -33,8 +33,8 @@ BUDGETS = {
     "k_update<false>": 64,
     # option resident_update: 4 waves per SIMD, so 1024 resident blocks hold
     # the 977 pair units of 100^3 at once (the host also checks occupancy)
-    "k_spmv_ar<false>": 128,
-    "k_spmv_ar<true>": 128,
+    "k_spmv_ar<false, 3, 2>": 128,
+    "k_spmv_ar<true, 3, 2>": 128,
 }
 
 

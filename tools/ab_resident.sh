@@ -1,0 +1,14 @@
+# Round-robin A/B of k_spmv_ar's slot-loop shapes at 100^3 (option
+# resident_update 0 = the unit + update-block launch, 1 = 3 early slots and
+# steps of 2, 2 = 3/3, 3 = 3/4, 4 = 7/4, 5 = 7/2), fresh process per line.
+export TMPDIR=/tmp; mkdir -p gpurun_out/abr; : > gpurun_out/abr/summary.log
+for rep in $(seq ${REPS:-2}); do
+  for v in ${SHAPES:-0 1 2 3 4 5}; do
+    timeout -k 10 200 python bench.py --n ${N:-100} --no-cpu-baseline --no-secondary --steps ${STEPS:-10} \
+        --set resident_update=$v > gpurun_out/abr/one.json 2>> gpurun_out/abr/err.log || exit 1
+    python3 -c "
+import json; d = json.load(open('gpurun_out/abr/one.json'))
+print('shape $v', d['value'], d['roofline']['avg_launch_us'], d['config']['options'].get('resident_update'))" >> gpurun_out/abr/summary.log
+  done
+done
+cat gpurun_out/abr/summary.log
