@@ -288,6 +288,21 @@ class Stages:
             os._exit(124)
 
 
+def init_gloo(dist, rank, world):
+    """torch.distributed's gloo group for the control plane. Gloo prints its
+    connection banner on fd 1: kept off stdout, which carries one JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.barrier()
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def opt_or_none(M, key):
     """An option's effective value, or None where the library predates it."""
     try:
@@ -686,7 +701,7 @@ def main():
     torch.cuda.set_device(dev)
     hp.set_device(dev)
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_gloo(dist, rank, world)
         if comm == "rccl":
             obj = [hp.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
