@@ -2629,7 +2629,7 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
 
 // The production protocol itself, after the peer and pull tests
 // passed on every rank: a short solve of this matrix (kProtoIters iterations,
-// a synthetic b) launch for launch as the solves will run it -- the peer
+// a synthetic b and a nonzero x0) launch for launch as the solves will run it -- the peer
 // all-reduce inside the kernels, r's boundary rows stored write-through and
 // drained before the r.r partial, the neighbours' rows pulled by the
 // iteration's last launch -- against the same solve with r's planes moved by
@@ -2647,8 +2647,13 @@ int protocol_autotest(hpccg_hip_matrix* M, int* all_ok)
     const size_t np = M->npad;
     // b and x: the matrix's own workspace (x is the buffer the neighbours have
     // mapped for the prologue's pull); b = 1 + (global row mod 13) / 8
-    std::vector<double> hb(np, 0.0);
-    for (int i = 0; i < M->nrow; i++) hb[i] = 1.0 + (double)(((long long)M->start_row + i) % 13) * 0.125;
+    // and x0 = ((global row mod 7) - 3) / 4, not zero: the prologue's p = x halo
+    // carries values (pulled from the neighbours' x in the in-kernel form)
+    std::vector<double> hb(np, 0.0), hx(np, 0.0);
+    for (int i = 0; i < M->nrow; i++) {
+        hb[i] = 1.0 + (double)(((long long)M->start_row + i) % 13) * 0.125;
+        hx[i] = 0.25 * (double)(((long long)M->start_row + i) % 7 - 3);
+    }
     if (h2d(M, M->d_b, hb.data(), sizeof(double) * np)) ok = 0;
     struct Run {
         int it = -1;
@@ -2661,7 +2666,7 @@ int protocol_autotest(hpccg_hip_matrix* M, int* all_ok)
         M->use_graph = 0;
         const double* b = M->d_b;
         double* x = M->d_x;
-        if (hipMemsetAsync(x, 0, sizeof(double) * np, M->stream) != hipSuccess) ok = 0;
+        if (h2d(M, x, hx.data(), sizeof(double) * np)) ok = 0;
         const int rc = solve_ranks(&M, 1, &b, &x, kProtoIters + 1, 0.0, &run[v].it, &run[v].nr, nullptr, 0);
         if (rc) ok = 0;
         run[v].trace = M->trace;

@@ -105,6 +105,18 @@ def main():
         state["M"], state["b"], state["first"] = M, b, (it, nr, tr.tobytes(), x.tobytes())
         return {"transport": transport(M), "niters": it, "normr": nr.hex()}
 
+    def bits64x0():
+        # a nonzero x0: the prologue's p = x halo is pulled from the other
+        # process's x (values, not zeros)
+        M, b = state["M"], state["b"]
+        n = 64 ** 3
+        g = torch.arange(n, dtype=torch.float64, device=f"cuda:{dev}") + rank * n
+        x = 0.25 * (torch.remainder(g, 7.0) - 3.0)
+        _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=500, device=True)
+        np.save(os.path.join(out_dir, f"x64x0_rank{rank}.npy"), x.cpu().numpy())
+        np.save(os.path.join(out_dir, f"tr64x0_rank{rank}.npy"), M.last_trace().copy())
+        return {"niters": it, "normr": nr.hex()}
+
     def withhold():
         M, b = state["M"], state["b"]
         budget_us = 200000
@@ -125,6 +137,7 @@ def main():
                 "after_same": (it, nr, tr.tobytes(), x.tobytes()) == state["first"]}
 
     case("bits64", bits64)
+    case("bits64x0", bits64x0)
     case("withhold", withhold)
     if "M" in state:
         state["M"].close()

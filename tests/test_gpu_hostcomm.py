@@ -105,6 +105,29 @@ def test_hostcomm_bitwise_in_process_group(hostcomm, hp, gpu):
         M.close()
 
 
+def test_hostcomm_nonzero_x0_bitwise_in_process_group(hostcomm, hp, gpu):
+    """The same with x0 = ((global row mod 7) - 3) / 4: the prologue's p = x
+    ghost rows come from the other process's x (pulled after the peer
+    barrier), and the solve is the in-process group's bit for bit."""
+    import torch
+    out, res = hostcomm
+    cs = _case(res, "bits64x0")
+    Ms = hp.group_generate(64, 64, 64, 2)
+    n = 64 ** 3
+    xs = []
+    for r in range(2):
+        g = torch.arange(n, dtype=torch.float64, device="cuda:0") + r * n
+        xs.append(0.25 * (torch.remainder(g, 7.0) - 3.0))
+    _, it, nr, _ = hp.group_HPCCG(Ms, [M.vectors()[0] for M in Ms], xs, max_iter=500)
+    tr = Ms[0].last_trace()
+    assert cs[0]["niters"] == it and float.fromhex(cs[0]["normr"]) == nr
+    for q in range(2):
+        assert np.load(out / f"tr64x0_rank{q}.npy").tobytes() == tr.tobytes()
+        assert np.load(out / f"x64x0_rank{q}.npy").tobytes() == xs[q].cpu().numpy().tobytes()
+    for M in Ms:
+        M.close()
+
+
 def test_hostcomm_withheld_contribution(hostcomm):
     """Rank 0 withholds a p.Ap partial (dbg_withhold): rank 0's group wait and
     rank 1's wait for rank 0's peer contribution both give up within the spin
