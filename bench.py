@@ -78,7 +78,7 @@ os.environ.setdefault("OMP_PLACES", "cores")
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 COPY_CEILING_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy, measured
-KERNEL_NAMES = {0: "k_spmv_sell", 1: "k_spmv_a", 2: "k_spmv_a2", 3: "k_spmv_a2r", 4: "k_spmv_ar"}
+KERNEL_NAMES = {0: "k_spmv_sell", 1: "k_spmv_a", 2: "k_spmv_a2", 3: "k_spmv_a2r", 4: "k_spmv_ar", 5: "k_cg_persist"}
 FORMAT_NAMES = {0: "SELL-512 (8 B value + 4 B int32 column per slot)",
                 1: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets",
                 2: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice "
@@ -86,7 +86,10 @@ FORMAT_NAMES = {0: "SELL-512 (8 B value + 4 B int32 column per slot)",
                 3: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice "
                    "pairs, values streamed HBM -> LDS by per-wave LDS-DMA rings",
                 4: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets, one "
-                   "block per slice pair, every block resident: the update applied from registers (no Ap stream)"}
+                   "block per slice pair, every block resident: the update applied from registers (no Ap stream)",
+                5: "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets, one "
+                   "block per slice pair, every block resident for the whole solve: one launch runs every "
+                   "iteration, x and the update in registers"}
 
 
 def load_pkg():
@@ -444,9 +447,11 @@ def roofline_of(M, n, stencil, spmv_avg_s):
     nrow = info["nrow"]
     kernel = M.get_option("spmv_kernel")
     kfmt = 3 if (kernel == 2 and M.get_option("a2_ring") > 0) else kernel  # 3: the pair kernel's LDS-DMA ring form
-    resident = opt_or_none(M, "resident_update") == 1
+    ru = opt_or_none(M, "resident_update") or 0
+    resident = ru >= 1
+    persist = ru >= 6  # one launch per solve (k_cg_persist): the figures are per iteration of it
     if resident:
-        kfmt = 4  # the resident pair kernel (k_spmv_ar)
+        kfmt = 5 if persist else 4  # the resident pair kernel (k_spmv_ar)
     fused = M.get_option("fuse_p")
     slots = info["slots"]
     # bytes the SpMV must move in its format: the stored slots (8 B; SELL-512
@@ -455,7 +460,7 @@ def roofline_of(M, n, stencil, spmv_avg_s):
     vec_bytes = (32.0 if fused else 16.0) * nrow
     # x_defer 2: the launch's trailing blocks apply the deferred x terms of
     # 1/q of the rows (q = x_ring - 1): x read and written, q p's read
-    xside = M.get_option("x_defer") == 2
+    xside = M.get_option("x_defer") == 2 and not persist  # (persistent: x stays in registers)
     q = M.get_option("x_ring") - 1
     side_bytes = (16.0 + 8.0 * q) / q * nrow if xside else 0.0
     # fused update: the launch's trailing blocks also run the update (r, Ap read; r written);
@@ -468,7 +473,7 @@ def roofline_of(M, n, stencil, spmv_avg_s):
     credited = 12.0 * info["nnz"] + 20.0 * nrow + 16.0 * nrow + (24.0 * nrow if fused else 0.0)
     achieved = format_bytes / spmv_avg_s / 1e9
     traffic, traffic_src = pmc_traffic(f"spmv_{stencil}pt_{n}", kfmt, fused, M.get_option("x_defer"),
-                                       M.get_option("fuse_update"), 1 if resident else 0)
+                                       M.get_option("fuse_update"), ru if resident else 0)
     roof = {
         "bound": "hbm",
         "achieved": round(achieved, 1),
@@ -501,6 +506,9 @@ def roofline_of(M, n, stencil, spmv_avg_s):
         "credited_bytes_per_launch": credited,
         "avg_launch_us": round(spmv_avg_s * 1e6, 2),
     }
+    if persist:
+        roof["launch_note"] = ("one k_cg_persist launch runs every iteration: avg_launch_us is (prologue SpMV + that "
+                               "launch) / (iterations + 1), bytes_per_launch one iteration's")
     if traffic:
         roof["traffic_gbs"] = round(traffic / spmv_avg_s / 1e9, 1)
         roof["traffic_frac"] = round(traffic / spmv_avg_s / 1e9 / HBM_PEAK_GBS, 4)

@@ -116,6 +116,8 @@ struct CgArgs {
     int dbg_resident_stall;       // debug (retry test): k_spmv_ar's p.Ap wait never sees the total (it expires)
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
+    double* pslots;               // persistent CG (resident 6): per iteration pslot_stride slots, emptied before the launch
+    long long pslot_stride;
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
     unsigned long long* dbg_tl;   // diagnostics (option dbg_timeline): per unit 8 words of block clock stamps
                                   // (kTlWords below); null off. Only the timeline instantiation writes it.
@@ -248,6 +250,18 @@ int a2_ring_prepare();
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s);
 // k_spmv_ar blocks the whole chip holds at once (0: unknown)
 int resident_capacity(bool nt);
+// persistent CG (one launch runs every iteration after the prologue): its
+// capacity, the launch, and the slot fill (kSlotEmpty) that precedes it
+constexpr int kResidentPersist = 6;
+constexpr int kResidentAuto = 8;  // resident_update -1: the persistent launch with the 3-slot LDS ring
+int persist_capacity(bool nt);
+void launch_cg_persist(const CgArgs& a, hipStream_t s);
+void launch_fill_empty(double* p, long long n, hipStream_t s);
+// slots per iteration of the persistent launch
+inline long long persist_slot_stride(int nslices)
+{
+    return 2LL * nslices + 2LL * ((nslices + 63) / 64) + 2LL * kNumXcd * kReadyStride;
+}
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);
 void launch_cg_end(const CgArgs& a, hipStream_t s);

@@ -1578,6 +1578,384 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     complete_dot_lanes(a, spmv_units(a, 2), P, s0, nsl, bsj, kRR, st.k);
 }
 
+// ---------------------------------------------------------------------------
+// Persistent CG (option resident_update 6; the k_spmv_ar setting, one launch
+// per solve): after the prologue, ONE launch runs every iteration. Each pair
+// block keeps its rows' x, r_{k-1} and p_{k-1} in registers (x += alpha p_k
+// there: no deferred-x side blocks, x stored once at the end), and the two
+// dots of every iteration complete through slots of their own (a.pslots:
+// iteration k's slice partials, group sums and kNumXcd broadcast copies of the
+// total, all emptied before the launch), so no slot is reused within the
+// launch. Neighbour values of r_{k-1} and p_{k-1} are read with sc1 buffer
+// loads (L1 bypassed: another CU rewrote them during this launch) after the
+// r.r total that orders them; r_k and p_k are stored sc1 and drained by every
+// wave before its block's r.r partial. r_k overwrites r_{k-1} only after the
+// p.Ap total, i.e. after every block's slot loop. Same expressions in the same
+// order as k_spmv_ar / the unfused kernels (HPCCG.cpp:358-385): the same bits.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void vm_wait(int n)  // n: a constant after unrolling
+{
+    switch (n) {
+#define HPCCG_VMW(i) \
+    case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+        HPCCG_VMW(0) HPCCG_VMW(1) HPCCG_VMW(2) HPCCG_VMW(3) HPCCG_VMW(4) HPCCG_VMW(5) HPCCG_VMW(6) HPCCG_VMW(7)
+#undef HPCCG_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr int kCpolSc1 = 16;  // buffer instruction cache policy: sc1
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double* base)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, 0x7FFFFFF0, 0x00020000);
+}
+__device__ __forceinline__ Rows ld_rs(__amdgpu_buffer_rsrc_t rs, int byte)
+{
+    const d2v t = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(rs, byte, 0, kCpolSc1));
+    return Rows{{t.x, t.y}};
+}
+// rows >= n stay untouched (the padding rows hold zeros)
+__device__ __forceinline__ void st_rs(__amdgpu_buffer_rsrc_t rs, int byte, int row, int n, const Rows& o)
+{
+    if (row + kRpt <= n) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
+                                                                  d2v{o.v[0], o.v[1]}),
+                                               rs, byte, 0, kCpolSc1);
+    } else {
+        for (int i = 0; i < kRpt; i++)
+            if (row + i < n)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int,
+                                                                         o.v[i]),
+                                                      rs, byte + 8 * i, 0, kCpolSc1);
+    }
+}
+
+// Iteration k's slots: [which][nslices] partials, [which][ngroups] group sums,
+// [which][kNumXcd x kReadyStride] broadcast copies of the total.
+__device__ __forceinline__ double* pers_slots(const CgArgs& a, int k) { return a.pslots + (size_t)k * a.pslot_stride; }
+__device__ __forceinline__ double* pers_bcast(const CgArgs& a, int k, int which)
+{
+    const int ng = ngroups_of(a);
+    return pers_slots(a, k) + 2 * a.nslices + 2 * ng + which * kNumXcd * kReadyStride;
+}
+
+// complete_dot_lanes' slot protocol on iteration k's own slots (no resets):
+// wave 0, lane j holds slice s0 + j's partial.
+// role: bit 0 this block waits for its group's partials, bit 1 (with bit 0)
+// its group is the top group (group_last_unit / top_group, once per launch)
+__device__ __forceinline__ void pers_dot(const CgArgs& a, int role, int s0, int cnt, double bs, int which, int k)
+{
+    const int lane = threadIdx.x;
+    double* const base = pers_slots(a, k);
+    const int ng = ngroups_of(a);
+    double* const sp = base + which * a.nslices;
+    double* const gp = base + 2 * a.nslices + which * ng;
+    const int g = s0 / kGroup;
+    const int i = g * kGroup + lane;
+    if (lane < cnt && !(which == kPAP && s0 + lane == a.dbg_withhold - 1)) st_sc1(sp + s0 + lane, bs);
+    if (!(role & 1)) return;
+    double v;
+    unsigned t0 = 0, polls = 0;
+    for (;;) {
+        v = i < a.nslices ? ld_sc1(sp + i) : 0.0;
+        if (__all(i >= a.nslices || slot_full(v))) break;
+        if ((++polls & 15) == 0 && wait_expired(a, t0)) {
+            if (lane == 0) abort_solve(a, kErrGroupWait, g, k, which);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    v = wave_sum(v);
+    if (lane == 0) st_sc1(gp + g, v);
+    if (!(role & 2)) return;
+    for (int j0 = 0; j0 < ng; j0 += kWave) {
+        for (;;) {
+            const int j = j0 + lane;
+            const double w = j < ng ? ld_sc1(gp + j) : 0.0;
+            if (__all(j >= ng || slot_full(w))) break;
+            if ((++polls & 15) == 0 && wait_expired(a, t0)) {
+                if (lane == 0) abort_solve(a, kErrTopWait, j0, k, which);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
+    if (lane == 0) {
+        double* const bc = pers_bcast(a, k, which);
+        for (int j = 0; j < kNumXcd; j++) st_sc1(bc + kReadyStride * j, tot);
+        stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
+    }
+}
+
+// One lane per block: iteration k's total of dot `which` (bounded wait).
+// Returns false when the solve was abandoned.
+__device__ __forceinline__ bool pers_wait(const CgArgs& a, int k, int which, double& out, bool stall)
+{
+    const double* slot = pers_bcast(a, k, which) + kReadyStride * (blockIdx.x % kNumXcd);
+    unsigned t0 = 0, polls = 0;
+    double v;
+    while (!slot_full(v = ld_sc1(slot)) || stall) {
+        if ((++polls & 15) == 0 && wait_expired(a, t0)) {
+            abort_solve(a, kErrReadyWait, blockIdx.x % kNumXcd, k, which);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    out = v;
+    return true;
+}
+
+template <bool kNT, int kPre = 2, int kStep = 1, int kL = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cg_persist(CgArgs a)
+{
+    constexpr int kW = 27;
+    // kL > 0: the first kL value slots come through LDS (kPre == kL), loaded by
+    // LDS-DMA during the previous iteration's two waits; else kPre register slots
+    static_assert((kW - kPre) % kStep == 0 && (kL == 0 || kL == kPre), "slot steps");
+    const int P = unit_of(a);
+    if (P < 0) return;
+    const int s0 = 2 * P;
+    const int nsl = min(2, a.nslices - s0);
+    const int s1 = nsl > 1 ? s0 + 1 : s0;
+    const int lr = threadIdx.x * kRpt;
+    const int row0 = s0 * kSliceRows + lr, row1 = s1 * kSliceRows + lr;
+    const double* __restrict__ vp0 = a.aval + (size_t)s0 * kW * kSliceRows + lr;
+    const double* __restrict__ vp1 = a.aval + (size_t)s1 * kW * kSliceRows + lr;
+    const int* __restrict__ off0 = a.aoff + (size_t)s0 * kAMax;
+    const int* __restrict__ off1 = a.aoff + (size_t)s1 * kAMax;
+    constexpr int kR = kL > 0 ? 0 : kPre;  // register slots
+    Rows pre0[kR > 0 ? kR : 1], pre1[kR > 0 ? kR : 1];
+#pragma unroll
+    for (int j = 0; j < kR; j++) {
+        pre0[j] = ld_m<kNT>(vp0 + (size_t)j * kSliceRows);
+        pre1[j] = ld_m<kNT>(vp1 + (size_t)j * kSliceRows);
+    }
+    // LDS value ring: slot j of slice half h, wave w at entry ((j * 2 + h) * 4 +
+    // w) * 128 doubles, lane l's 16 B at + 2 l (written and read by lane l only)
+    __shared__ __attribute__((aligned(16))) double vring[kL > 0 ? kL * 2 * kBlock * kRpt : 2];
+    const int wv = threadIdx.x / kWave;
+    const int lane_ = threadIdx.x & (kWave - 1);
+    auto dma = [&](int j) {
+        __builtin_amdgcn_global_load_lds((const void*)(vp0 + (size_t)j * kSliceRows),
+                                         (lds_void*)(vring + ((j * 2 + 0) * 4 + wv) * (2 * kWave)), 16, 0,
+                                         kNT ? 2 : 0);
+        __builtin_amdgcn_global_load_lds((const void*)(vp1 + (size_t)j * kSliceRows),
+                                         (lds_void*)(vring + ((j * 2 + 1) * 4 + wv) * (2 * kWave)), 16, 0,
+                                         kNT ? 2 : 0);
+    };
+    auto lds_val = [&](int j, int h) -> Rows {
+        const d2v t = *reinterpret_cast<const d2v*>(vring + ((j * 2 + h) * 4 + wv) * (2 * kWave) + 2 * lane_);
+        return Rows{{t.x, t.y}};
+    };
+    constexpr int kA = (kL + 1) / 2;  // ring slots refilled during the p.Ap wait; the rest during the r.r wait
+#pragma unroll
+    for (int j = 0; j < kL; j++) dma(j);
+    // a raw workgroup barrier: __syncthreads() would drain the DMAs (vmcnt(0))
+    auto bar = [&]() {
+        if constexpr (kL > 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        } else {
+            __syncthreads();
+        }
+    };
+    // r and the p ring through buffer resources based at their guard zones
+    const __amdgpu_buffer_rsrc_t rsr = vec_rsrc(a.r - kGuardRows);
+    const __amdgpu_buffer_rsrc_t rsp = vec_rsrc(a.p - kGuardRows);
+    const int b0 = (row0 + (int)kGuardRows) * 8, b1 = (row1 + (int)kGuardRows) * 8;
+    const int pstr = (int)(a.pstride * 8);
+    // the rows' x (in registers for the whole solve)
+    Rows xv0 = ld(a.x + row0), xv1 = ld(a.x + row1);
+    double rr1 = a.g[kRRPar + 1];  // r_{k-1}.r_{k-1}: the prologue's r_0.r_0
+    double rr2 = 0.0;              // r_{k-2}.r_{k-2}
+    int role;
+    {
+        const UnitMap m = spmv_units(a, 2);
+        const int g = s0 / kGroup;
+        role = P == group_last_unit(m, g) ? (g == top_group(m) ? 3 : 1) : 0;
+        role = __builtin_amdgcn_readfirstlane(role);
+    }
+    __shared__ double ws2[2][kBlock / kWave];
+    __shared__ double tot_s;
+    __shared__ int gave_up;
+    const int lane = threadIdx.x & (kWave - 1);
+    int k = 1;
+    for (;; k++) {
+        // HPCCG.cpp:358
+        const bool run = k < a.max_iter && sqrt(k == 1 ? rr1 : rr2) > a.tol;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (k == 1 || run) a.hist[k - 1] = rr1;
+            if (run) stamp(a, k, kStampSpmv);
+        }
+        if (!run) break;
+        const double beta = (k == 1) ? 0.0 : rr1 / rr2;
+        // p_{k-1}: ring buffer (k - 1) & 1 (k = 1: r_0, beta 0)
+        const __amdgpu_buffer_rsrc_t rsy = k == 1 ? rsr : rsp;
+        const int yb = k == 1 ? 0 : ((k - 1) & 1) * pstr;
+        double sum0[kRpt] = {0.0, 0.0}, sum1[kRpt] = {0.0, 0.0};
+        auto slot = [&](const Rows& v0, const Rows& v1, const Rows& ra, const Rows& ya, const Rows& rb, const Rows& yb_) {
+#pragma unroll
+            for (int i = 0; i < kRpt; i++) {
+                sum0[i] = sum0[i] + v0.v[i] * (ra.v[i] + beta * ya.v[i]);
+                sum1[i] = sum1[i] + v1.v[i] * (rb.v[i] + beta * yb_.v[i]);
+            }
+        };
+        if constexpr (kL > 0) vm_wait(0);  // the ring's DMAs (issued during the waits) have landed
+#pragma unroll
+        for (int j = 0; j < kPre; j++) {
+            const int o0 = sld(off0 + j) * 8, o1 = sld(off1 + j) * 8;
+            if constexpr (kL > 0)
+                slot(lds_val(j, 0), lds_val(j, 1), ld_rs(rsr, b0 + o0), ld_rs(rsy, yb + b0 + o0), ld_rs(rsr, b1 + o1),
+                     ld_rs(rsy, yb + b1 + o1));
+            else
+                slot(pre0[j], pre1[j], ld_rs(rsr, b0 + o0), ld_rs(rsy, yb + b0 + o0), ld_rs(rsr, b1 + o1),
+                     ld_rs(rsy, yb + b1 + o1));
+        }
+#pragma unroll 1
+        for (int j0 = kPre; j0 < kW; j0 += kStep) {
+            Rows v0[kStep], v1[kStep], ra[kStep], ya[kStep], rb[kStep], yc[kStep];
+#pragma unroll
+            for (int u = 0; u < kStep; u++) {
+                const int o0 = sld(off0 + j0 + u) * 8, o1 = sld(off1 + j0 + u) * 8;
+                v0[u] = ld_m<kNT>(vp0 + (size_t)(j0 + u) * kSliceRows);
+                v1[u] = ld_m<kNT>(vp1 + (size_t)(j0 + u) * kSliceRows);
+                ra[u] = ld_rs(rsr, b0 + o0);
+                ya[u] = ld_rs(rsy, yb + b0 + o0);
+                rb[u] = ld_rs(rsr, b1 + o1);
+                yc[u] = ld_rs(rsy, yb + b1 + o1);
+            }
+#pragma unroll
+            for (int u = 0; u < kStep; u++) slot(v0[u], v1[u], ra[u], ya[u], rb[u], yc[u]);
+        }
+        // the rows' r_{k-1} and p_k = r + beta p_{k-1} (k_p_update's expression;
+        // read again: the slot loop's centre values came through L2 just now)
+        const Rows rv0 = ld_rs(rsr, b0), rv1 = ld_rs(rsr, b1);
+        const Rows yv0 = ld_rs(rsy, yb + b0), yv1 = ld_rs(rsy, yb + b1);
+        Rows pk0, pk1;
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            pk0.v[i] = rv0.v[i] + beta * yv0.v[i];
+            pk1.v[i] = rv1.v[i] + beta * yv1.v[i];
+        }
+        // p_k at the rows into ring buffer k & 1
+        st_rs(rsp, (k & 1) * pstr + b0, row0, a.n, pk0);
+        if (nsl > 1) st_rs(rsp, (k & 1) * pstr + b1, row1, a.n, pk1);
+        double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            if (row0 + i < a.n) d0 += pk0.v[i] * sum0[i];
+            if (nsl > 1 && row1 + i < a.n) d1 += pk1.v[i] * sum1[i];
+        }
+        {
+            const double w0 = wave_sum(d0), w1 = wave_sum(d1);
+            if (lane == 0) {
+                ws2[0][threadIdx.x / kWave] = w0;
+                ws2[1][threadIdx.x / kWave] = w1;
+            }
+        }
+        bar();
+        if (threadIdx.x < kWave) {
+            double bsj = 0.0;
+            if (lane < 2) {
+#pragma unroll
+                for (int i = 0; i < kBlock / kWave; i++) bsj += ws2[lane][i];
+            }
+            pers_dot(a, role, s0, nsl, bsj, kPAP, k);
+        }
+        // the next iteration's first ring slots, landing during the p.Ap wait
+        // (this lane's reads of those entries are done: lgkmcnt)
+        if constexpr (kL > 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int j = 0; j < kA; j++) dma(j);
+        }
+        if (threadIdx.x == 0) {
+            double v = 0.0;
+            gave_up = pers_wait(a, k, kPAP, v, a.dbg_resident_stall != 0) ? 0 : 1;
+            tot_s = v;
+        }
+        bar();
+        if (gave_up) {
+            vm_wait(0);  // no DMA may land after the block's LDS is released
+            return;
+        }
+        const double alpha = rr1 / tot_s;
+        if (blockIdx.x == 0 && threadIdx.x == 0) stamp(a, k, kStampUpdate);
+        // x += alpha p_k (waxpby, HPCCG.cpp:377), r = r - alpha Ap (:379), r.r (:384)
+        Rows rn0, rn1;
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            xv0.v[i] = xv0.v[i] + alpha * pk0.v[i];
+            xv1.v[i] = xv1.v[i] + alpha * pk1.v[i];
+            rn0.v[i] = rv0.v[i] + (-alpha) * sum0[i];
+            rn1.v[i] = rv1.v[i] + (-alpha) * sum1[i];
+        }
+        st_rs(rsr, b0, row0, a.n, rn0);
+        if (nsl > 1) st_rs(rsr, b1, row1, a.n, rn1);
+        double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < kRpt; i++) {
+            if (row0 + i < a.n) e0 += rn0.v[i] * rn0.v[i];
+            if (nsl > 1 && row1 + i < a.n) e1 += rn1.v[i] * rn1.v[i];
+        }
+        {
+            const double w0 = wave_sum(e0), w1 = wave_sum(e1);
+            // this wave's p_k and r_k have landed before the block's r.r partial
+            // (the next iteration's readers are ordered after the r.r total)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                ws2[0][threadIdx.x / kWave] = w0;
+                ws2[1][threadIdx.x / kWave] = w1;
+            }
+        }
+        bar();
+        if (threadIdx.x < kWave) {
+            double bsj = 0.0;
+            if (lane < 2) {
+#pragma unroll
+                for (int i = 0; i < kBlock / kWave; i++) bsj += ws2[lane][i];
+            }
+            pers_dot(a, role, s0, nsl, bsj, kRR, k);
+        }
+        // the next iteration's early value slots, in flight across the wait
+#pragma unroll
+        for (int j = 0; j < kR; j++) {
+            pre0[j] = ld_m<kNT>(vp0 + (size_t)j * kSliceRows);
+            pre1[j] = ld_m<kNT>(vp1 + (size_t)j * kSliceRows);
+        }
+        if constexpr (kL > 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int j = kA; j < kL; j++) dma(j);
+        }
+        if (threadIdx.x == 0) {
+            double v = 0.0;
+            gave_up = pers_wait(a, k, kRR, v, false) ? 0 : 1;
+            tot_s = v;
+        }
+        bar();
+        if (gave_up) {
+            vm_wait(0);
+            return;
+        }
+        // (tot_s is written again only after the next p.Ap barrier)
+        rr2 = rr1;
+        rr1 = tot_s;
+    }
+    // k: the first iteration not run (niters = k - 1)
+    vm_wait(0);  // (the ring's last refill)
+    st_rows(a.x, row0, a.n, xv0);
+    if (nsl > 1) st_rows(a.x, row1, a.n, xv1);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.kst[0] = k;
+        a.kst[2] = k;
+        mark_end(a);
+    }
+}
+
 
 // ---------------------------------------------------------------------------
 // SELL-512-A with x from LDS windows shared by slice pairs: block P owns
@@ -1793,17 +2171,6 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2(CgArgs a, bool prologue)
 // register pair kernel (2469 it/s); storing Ap and p_k after the p.Ap ticket
 // instead measured 341.8 us. Same products in the same order: same bits.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void vm_wait(int n)  // n: a constant after unrolling
-{
-    switch (n) {
-#define HPCCG_VMW(i) \
-    case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
-        HPCCG_VMW(0) HPCCG_VMW(1) HPCCG_VMW(2) HPCCG_VMW(3) HPCCG_VMW(4) HPCCG_VMW(5) HPCCG_VMW(6) HPCCG_VMW(7)
-#undef HPCCG_VMW
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-}
-typedef __attribute__((address_space(3))) void lds_void;
 constexpr int kA2RingMax = 4;
 
 
@@ -2716,6 +3083,73 @@ int resident_capacity(bool nt)
     const hipError_t e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spmv_ar<true>, kBlock, 0)
                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spmv_ar<false>, kBlock, 0);
     return e == hipSuccess ? per_cu * cus : 0;
+}
+
+int persist_capacity(bool nt)
+{
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    // (the smallest of the shapes' figures)
+    int per_cu2 = 0, per_cu3 = 0, per_cu4 = 0;
+    hipError_t e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<true, 2, 1, 0>, kBlock, 0)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<false, 2, 1, 0>, kBlock, 0);
+    if (e == hipSuccess)
+        e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_cg_persist<true, 1, 2, 0>, kBlock, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_cg_persist<false, 1, 2, 0>, kBlock, 0);
+    if (e == hipSuccess)
+        e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu3, k_cg_persist<true, 3, 2, 3>, kBlock, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu3, k_cg_persist<false, 3, 2, 3>, kBlock, 0);
+    if (e == hipSuccess)
+        e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu4, k_cg_persist<true, 3, 1, 3>, kBlock, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu4, k_cg_persist<false, 3, 1, 3>, kBlock, 0);
+    int per_cu5 = 0;
+    if (e == hipSuccess)
+        e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu5, k_cg_persist<true, 4, 1, 4>, kBlock, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu5, k_cg_persist<false, 4, 1, 4>, kBlock, 0);
+    per_cu = std::min(std::min(std::min(per_cu, per_cu2), std::min(per_cu3, per_cu4)), per_cu5);
+    return e == hipSuccess ? per_cu * cus : 0;
+}
+
+void launch_cg_persist(const CgArgs& a, hipStream_t s)
+{
+    const int pairs = (a.nslices + 1) / 2;
+    CgArgs b = a;
+    b.s0 = 0;
+    b.sn0 = pairs;
+    b.s1 = b.sn1 = 0;
+    b.sgrid = (pairs + kNumXcd - 1) / kNumXcd * kNumXcd;
+    b.send = b.sgrid;
+    b.ubase = b.gbase = INT_MAX;
+    // (resident_update 6: 2 early register slots + steps of 1; 7: 1 + steps of
+    // 2; 8, 9: 3 LDS-ring slots + steps of 2, 1)
+#define HPCCG_PS(PRE, STEP, L)                                                                             \
+    do {                                                                                                   \
+        if (a.nt)                                                                                          \
+            hipLaunchKernelGGL((k_cg_persist<true, PRE, STEP, L>), dim3(b.sgrid), dim3(kBlock), 0, s, b);  \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_cg_persist<false, PRE, STEP, L>), dim3(b.sgrid), dim3(kBlock), 0, s, b); \
+    } while (0)
+    switch (a.resident - kResidentPersist) {
+    case 1: HPCCG_PS(1, 2, 0); break;
+    case 2: HPCCG_PS(3, 2, 3); break;
+    case 3: HPCCG_PS(3, 1, 3); break;
+    case 4: HPCCG_PS(4, 1, 4); break;
+    default: HPCCG_PS(2, 1, 0); break;
+    }
+#undef HPCCG_PS
+}
+
+__global__ __launch_bounds__(256) void k_fill_empty(double* p, long long n)
+{
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = slot_empty();
+}
+
+void launch_fill_empty(double* p, long long n, hipStream_t s)
+{
+    if (n > 0) hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, n);
 }
 
 void launch_cg_finalize(const CgArgs& a, int which, bool prologue, hipStream_t s)

@@ -326,6 +326,8 @@ struct hpccg_hip_matrix {
     double* d_p = nullptr;     // local rows of ring buffer 0
     long long pstride = 0;
     double* d_ahist = nullptr;
+    double* d_pslots = nullptr;   // persistent CG (persist_of): per-iteration dot slots
+    long long pslots_cap = 0;     // doubles
     int x_defer = 2;      // deferred x: beside the SpMV where the kernel carries it, else batched (x_defer_effective)
     int x_ring = -1;
     int rev_update = 1;
@@ -613,7 +615,7 @@ int free_matrix(hpccg_hip_matrix* M)
         for (double** q : {&M->d_aval, &M->d_pbuf, &M->d_rbuf, &M->d_Ap, &M->d_x})
             if (*q == v.va) *q = nullptr;
     void* ptrs[] = {M->d_slice_base, M->d_cols,   M->d_vals,      M->d_aval,    M->d_aoff,     M->d_abase,
-                    M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_adiag2,     M->d_atri,      M->d_pbuf,    M->d_ahist,    M->d_rbuf,
+                    M->d_alds2,      M->d_awin2,  M->d_awn2,      M->d_adiag2,     M->d_atri,      M->d_pbuf,    M->d_ahist,    M->d_pslots,  M->d_rbuf,
                     M->d_Ap,         M->d_x,      M->d_b,         M->d_tickets,  M->d_scal,
                     M->d_kst,        M->d_hist,   M->d_stamps,    M->d_gen_b,   M->d_gen_x0,   M->d_gen_xexact,
                     M->d_send_idx,   M->d_send_buf,  M->d_emul,  M->d_tl};
@@ -1454,6 +1456,43 @@ bool resident_of(const hpccg_hip_matrix* M)
     return resident_capacity(image_big(M)) >= grid_of(pairs);
 }
 
+// The persistent CG launch (k_cg_persist; option resident_update -1 auto or
+// 6..10): every iteration after the prologue in one launch, where resident_of
+// holds and the chip holds every pair block of it at once. Shapes (A/B): 6 two
+// early register slots + steps of 1, 7 one + steps of 2, 8 (auto) three
+// LDS-ring slots + steps of 2, 9 three + steps of 1, 10 four + steps of 1.
+int persist_shape(const hpccg_hip_matrix* M)
+{
+    if (M->resident_update == -1) return kResidentAuto;
+    return M->resident_update >= kResidentPersist ? M->resident_update : 0;
+}
+bool persist_ok(const hpccg_hip_matrix* M)
+{
+    if (!persist_shape(M) || !resident_of(M)) return false;
+    // (byte offsets of the p ring in 32 bits)
+    if ((M->pstride * 2 + kGuardRows) * (long long)sizeof(double) >= (1LL << 31)) return false;
+    return persist_capacity(image_big(M)) >= grid_of((M->nslices + 1) / 2);
+}
+// ... and its per-iteration slots are allocated for max_iter
+bool persist_of(const hpccg_hip_matrix* M, int max_iter)
+{
+    return persist_ok(M) && M->d_pslots &&
+           M->pslots_cap >= (long long)(max_iter + 1) * persist_slot_stride((int)M->nslices);
+}
+// iterations 0 .. max_iter, each with slots of its own
+int ensure_pslots(hpccg_hip_matrix* M, int max_iter)
+{
+    if (!persist_ok(M)) return 0;
+    const long long need = (long long)(max_iter + 1) * persist_slot_stride((int)M->nslices);
+    if (need > M->pslots_cap) {
+        dev_free(M, &M->d_pslots, (size_t)M->pslots_cap);
+        M->pslots_cap = 0;
+        TRY(dev_alloc(M, &M->d_pslots, (size_t)need));
+        M->pslots_cap = need;
+    }
+    return 0;
+}
+
 CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tol)
 {
     CgArgs a;
@@ -1477,10 +1516,21 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.fupd = fuse_update_effective(M) ? 1 : 0;
     a.fu2 = M->fused_update_slices == 2 ? 1 : 0;
     // (1 + the slot-loop shape: option resident_update 2..5 pick the A/B variants of k_spmv_ar)
-    a.resident = a.fupd && resident_of(M) ? (M->resident_update > 1 ? M->resident_update : 1) : 0;
+    a.resident = 0;
+    if (a.fupd && resident_of(M))
+        a.resident = persist_of(M, max_iter) ? persist_shape(M)
+                     : (M->resident_update > 1 && M->resident_update < kResidentPersist) ? M->resident_update : 1;
     a.pready = M->d_partial + (M->npartial - kNumXcd * kReadyStride);
+    if (a.resident >= kResidentPersist) {
+        a.pslots = M->d_pslots;
+        a.pslot_stride = persist_slot_stride((int)M->nslices);
+    }
     a.rev = M->rev_update ? 1 : 0;
     a.nring = a.xdefer ? x_ring_effective(M) : (a.fuse_p ? 2 : 1);
+    if (a.resident >= kResidentPersist) {  // x lives in the persistent blocks' registers: nothing deferred
+        a.xdefer = 0;
+        a.nring = 2;
+    }
     const int units = M->kernel == kSpmvPairs ? (M->nslices + 1) / 2 : M->nslices;
     a.s0 = 0;
     a.sn0 = units;
@@ -2788,6 +2838,7 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
         HIP_TRY(hipSetDevice(Ms[r]->device));
         TRY(ensure_hist(Ms[r], max_iter));
         Ms[r]->kernel = choose_kernel(Ms[r]);
+        if (P == 1) TRY(ensure_pslots(Ms[r], max_iter));
         if (Ms[r]->device != M->device) one_device = false;
     }
     if (P > 1) {
@@ -2906,10 +2957,20 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     TRY(enqueue_prologue(R, events));
     int done = 0;
     M->graph_used = 0;
+    const bool persist = P == 1 && av[0].resident >= kResidentPersist;
+    if (persist) {  // every iteration in one launch (k_cg_persist), its slots emptied first
+        launch_fill_empty(M->d_pslots, (long long)(max_iter + 1) * av[0].pslot_stride, M->stream);
+        if (events && iters > 0) HIP_TRY(hipEventRecord(M->ev[4], M->stream));
+        launch_cg_persist(av[0], M->stream);
+        if (events && iters > 0) HIP_TRY(hipEventRecord(M->ev[5], M->stream));
+        HIP_TRY(hipGetLastError());
+        done = iters;
+    }
     const int chunk = graph_chunk_of(R);
     // (an in-process group with the peer all-reduce: its members' kernels wait
     // for each other, so they are never serialised into one graph)
-    if (!events && M->use_graph && !M->graph_failed && one_device && iters >= chunk && !(P > 1 && av[0].peer_ar)) {
+    if (!persist && !events && M->use_graph && !M->graph_failed && one_device && iters >= chunk &&
+        !(P > 1 && av[0].peer_ar)) {
         // kernel arguments are baked into the graph: rebuild only when they change
         bool same = M->graph_exec && (int)M->graph_args.size() == P && M->graph_kernel == M->kernel &&
                     M->graph_chunk == chunk;
@@ -3002,7 +3063,22 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
         Ms[r]->last_niters = niters;
     }
     const double normr = M->trace[niters];
-    if (events) {
+    if (events && persist) {
+        // the prologue's two launches, then the persistent launch's time spread
+        // evenly over its iterations (one SpMV-to-r.r period each)
+        float ms0 = 0.f, ms1 = 0.f, msp = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms0, M->ev[0], M->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&ms1, M->ev[2], M->ev[3]));
+        if (iters > 0) HIP_TRY(hipEventElapsedTime(&msp, M->ev[4], M->ev[5]));
+        M->kiter.assign(2 * (size_t)(niters + 1), 0.0);
+        M->kiter[0] = ms0;
+        M->kiter[1] = ms1;
+        for (int i = 1; i <= niters; i++) M->kiter[2 * i] = msp / niters;
+        M->ktimes[0] = ms0 + msp;
+        M->ktimes[1] = niters + 1;
+        M->ktimes[2] = ms1;
+        M->ktimes[3] = 1;
+    } else if (events) {
         double sp = 0, up = 0;
         M->kiter.assign(2 * (size_t)(niters + 1), 0.0);
         for (int i = 0; i <= niters; i++) {
@@ -3055,7 +3131,11 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
 // that launch.
 bool resident_retry(hpccg_hip_matrix* M, int rc)
 {
-    if (rc != HPCCG_HIP_EHIP || !M->resident_used || M->last_dev_err != kErrReadyWait) return false;
+    // (the persistent launch waits on every block at each dot: any of its waits)
+    const bool persist_wait = M->resident_used >= kResidentPersist &&
+                              (M->last_dev_err == kErrGroupWait || M->last_dev_err == kErrTopWait);
+    if (rc != HPCCG_HIP_EHIP || !M->resident_used || (M->last_dev_err != kErrReadyWait && !persist_wait))
+        return false;
     M->resident_failed = 1;
     std::fprintf(stderr, "hpccg_hip: the resident update's wait expired (a shared GPU?); the solve is re-run with "
                          "the unit + update-block launch, which this matrix keeps\n");
@@ -3819,7 +3899,8 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
     } else if (!std::strcmp(key, "fuse_update")) {
         M->fuse_update = value < 0 ? -1 : (value > 2 ? 2 : (int)value);
     } else if (!std::strcmp(key, "resident_update")) {
-        if (value < -1 || value > 5) return set_err(HPCCG_HIP_EINVAL, "resident_update: -1 (auto), 0, 1 or 2..5 (shapes)");
+        if (value < -1 || value > 10)
+            return set_err(HPCCG_HIP_EINVAL, "resident_update: -1 (auto), 0, 1, 2..5 (shapes) or 6..10 (persistent)");
         M->resident_update = (int)value;
         if (value) M->resident_failed = 0;
     } else if (!std::strcmp(key, "rev_update")) {
@@ -3913,7 +3994,8 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "rev_update")) *value = M->rev_update;
     else if (!std::strcmp(key, "fuse_update")) *value = fuse_update_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "fused_update_slices")) *value = M->fused_update_slices;
-    else if (!std::strcmp(key, "resident_update")) *value = resident_of(M) ? 1 : 0;
+    else if (!std::strcmp(key, "resident_update"))
+        *value = !resident_of(M) ? 0 : persist_ok(M) ? persist_shape(M) : 1;
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
     else if (!std::strcmp(key, "graph_chunk")) {  // effective: see graph_chunk_of
         long long c = std::max(1, M->graph_iters);

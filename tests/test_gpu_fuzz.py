@@ -52,7 +52,7 @@ def _cases():
         # the resident fused update (default where it fits) against the other
         # launch and a second slot-loop shape; drawn apart so the cases above
         # stay the seed's
-        opts["resident_update"] = (0, -1, 5)[i % 3]
+        opts["resident_update"] = (0, -1, 5, 1, 6, 10)[i % 6]
         out.append((i, (nx, ny, nz), s7, max_iter, early, opts))
     return out
 

@@ -1,5 +1,6 @@
-"""Option resident_update (-1 auto, the default where it
-fits): the fused update run by the resident pair kernel (k_spmv_ar: every pair unit of the launch resident, Ap
+"""Option resident_update 1 (auto, -1, now picks the
+persistent launch where it fits -- tests/test_gpu_persist.py): the fused
+update run by the resident pair kernel (k_spmv_ar: every pair unit of the launch resident, Ap
 and r kept in registers across the p.Ap completion, no Ap stream and no
 second read of r). HPCCG.cpp:377-385 computed with the same expressions in
 the same order as the default fused launch, so every solve must be bitwise
@@ -24,15 +25,18 @@ def _solve(hp, M, it, gpu, b=None):
                                      ((64, 64, 64), 60)])
 def test_resident_update_bitwise(hp, gpu, dims, it):
     M = hp.Matrix.generate(*dims)
-    assert M.get_option("fuse_update") == 1 and M.get_option("resident_update") == 1  # the default here
+    # the default here: the persistent launch (auto)
+    assert M.get_option("fuse_update") == 1 and M.get_option("resident_update") == 8
     M.set_option("resident_update", 0)  # the unit + update-block launch
     assert M.get_option("resident_update") == 0
     ref = _solve(hp, M, it, gpu)
-    M.set_option("resident_update", -1)
+    M.set_option("resident_update", 1)
     assert M.get_option("resident_update") == 1
     for graph in (1, 0):
         M.set_option("use_graph", graph)
         assert _solve(hp, M, it, gpu) == ref, (dims, graph)
+    M.set_option("resident_update", -1)
+    assert _solve(hp, M, it, gpu) == ref, dims
     M.close()
 
 
@@ -51,6 +55,7 @@ def test_resident_update_guard(hp, gpu):
     """A withheld p.Ap partial: the resident blocks' p.Ap wait gives up within
     the spin budget (EHIP) and the next solve is bitwise the first."""
     M = hp.Matrix.generate(40, 36, 30)
+    M.set_option("resident_update", 1)
     assert M.get_option("resident_update") == 1
     ref = _solve(hp, M, 60, gpu)
     M.set_option("spin_budget_us", 100000)
@@ -70,6 +75,7 @@ def test_resident_update_retry_on_expired_wait(hp, gpu):
     the default solve's bits, resident_update then reads 0, and it can be
     switched back on."""
     M = hp.Matrix.generate(40, 36, 30)
+    M.set_option("resident_update", 1)
     ref = _solve(hp, M, 60, gpu)
     M.set_option("spin_budget_us", 50000)
     M.set_option("dbg_resident_stall", 1)
@@ -84,6 +90,7 @@ def test_resident_update_retry_on_expired_wait(hp, gpu):
     import numpy as np
     prob = hp.generate_matrix(40, 36, 30)
     H = hp.Matrix.from_hpc(prob)
+    H.set_option("resident_update", 1)
     x0 = np.zeros(prob.nrow)
     _, n0, nr0, _ = hp.HPCCG(H, prob.b, x0, max_iter=60)
     H.set_option("spin_budget_us", 50000)

@@ -35,6 +35,9 @@ BUDGETS = {
     # the 977 pair units of 100^3 at once (the host also checks occupancy)
     "k_spmv_ar<false, 3, 2>": 128,
     "k_spmv_ar<true, 3, 2>": 128,
+    # the persistent CG launch (4 blocks per CU: every pair block of 100^3 resident)
+    "k_cg_persist<false, 3, 2, 3>": 128,
+    "k_cg_persist<true, 3, 2, 3>": 128,
 }
 
 

@@ -29,6 +29,8 @@ FORMATS = {
     "k_spmv_a2": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice pairs",
     "k_spmv_a2r": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x from LDS windows shared by slice pairs, "
                   "values streamed HBM -> LDS by per-wave LDS-DMA rings",
+    "k_cg_persist": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets, one "
+                    "block per slice pair resident for the whole solve: one launch runs every iteration",
     "k_spmv_ar": "SELL-512-A (8 B value per offset-aligned slot, holes 0.0), x read at the slice's offsets, one block "
                  "per slice pair, every block resident: the update applied from registers (no Ap stream)",
 }
@@ -89,12 +91,18 @@ def main():
     f_stream, _ = pick(fetch, "k_stream_a", "FETCH_SIZE")
     w_stream, _ = pick(write, "k_stream_a", "WRITE_SIZE")
     fetch_factor = stream_read / (f_stream * 1024.0)
-    SPMV = ("k_spmv_sell<", "k_spmv_a<", "k_spmv_a2<", "k_spmv_a2r<", "k_spmv_ar<")
+    SPMV = ("k_spmv_sell<", "k_spmv_a<", "k_spmv_a2<", "k_spmv_a2r<", "k_spmv_ar<", "k_cg_persist<")
     f_spmv, kname = pick(fetch, SPMV, "FETCH_SIZE")
     w_spmv, _ = pick(write, SPMV, "WRITE_SIZE")
-    spmv_read = f_spmv * 1024.0 * fetch_factor
-    spmv_write = w_spmv * 1024.0
-    targs = re.search(r"k_spmv\w*<([^>]*)>", kname).group(1).split(",")
+    # the persistent launch (k_cg_persist) runs every iteration of a solve in
+    # one dispatch: its counters and its duration are divided by the
+    # iterations of that dispatch (pmc_workload: --iters - 1; the bench:
+    # max_iter - 1), so every figure below is per iteration
+    persist = "k_cg_persist<" in kname
+    pmc_iters = int(os.environ.get("PMC_ITERS", "32")) - 1 if persist else 1
+    spmv_read = f_spmv * 1024.0 * fetch_factor / pmc_iters
+    spmv_write = w_spmv * 1024.0 / pmc_iters
+    targs = re.search(r"(?:k_spmv\w*|k_cg_persist)<([^>]*)>", kname).group(1).split(",")
     # k_spmv_a<kW, kNT, kFuse, kPre>, k_spmv_a2<kNT, kFuse, kPre>, k_spmv_a2r<kFuse, kW, kR>,
     # k_spmv_sell<kNT> (never fused)
     if "k_spmv_a<" in kname:
@@ -103,7 +111,7 @@ def main():
         fuse_p = targs[0].strip() == "true"
     elif "k_spmv_a2<" in kname:
         fuse_p = targs[1].strip() == "true"
-    elif "k_spmv_ar<" in kname:  # k_spmv_ar<kNT>: always fused (p and the update)
+    elif "k_spmv_ar<" in kname or persist:  # always fused (p and the update)
         fuse_p = True
     else:
         fuse_p = False
@@ -119,12 +127,12 @@ def main():
         bench = json.loads(lines[-1]) if lines else None
     opts = bench["config"]["options"] if bench else {}
     side = 0.0
-    if opts.get("x_defer") == 2:
+    if opts.get("x_defer") == 2 and not persist:  # (persistent: x in registers)
         q = opts["x_ring"] - 1
         launches = len(fetch[(kname, "FETCH_SIZE")])
         side = (16.0 + 8.0 * q) / q * nrow * (launches - 1) / launches
         compulsory += side
-    resident = "k_spmv_ar<" in kname
+    resident = "k_spmv_ar<" in kname or persist
     # fused update blocks: r, Ap read; r written (resident: applied from registers, r written
     # instead of Ap -- the same 32 B per row as above, nothing more)
     upd = 24.0 * nrow if (opts.get("fuse_update") == 1 and not resident) else 0.0
@@ -137,10 +145,13 @@ def main():
     for row in csv.DictReader(open(stats)):
         if row["Name"] == kname and int(row["Calls"]) > calls:
             avg_ns, calls = float(row["AverageNs"]), int(row["Calls"])
+    if persist and avg_ns:
+        bench_iters = (bench["config"].get("max_iter", 500) - 1) if bench else 499
+        avg_ns /= bench_iters
     out = {
         "tag": tag,
         "problem": f"{stencil}-pt {n}^3, SELL-512 width {width} ({slots} slots, nnz {nnz}); "
-                   + FORMATS.get(re.search(r"(k_spmv\w*)<", kname).group(1), kname),
+                   + FORMATS.get(re.search(r"(k_spmv\w*|k_cg_persist)<", kname).group(1), kname),
         "kernel": kname,
         "fuse_p": fuse_p,
         "bytes_formula": "12 nnz + 20 n + 16 n" + (" + 24 n" if fuse_p else ""),
@@ -149,7 +160,8 @@ def main():
         "side_flush_bytes_per_launch": side,
         "fuse_update": opts.get("fuse_update", 0),
         "fused_update_bytes_per_launch": upd,
-        "resident_update": 1 if resident else 0,
+        "resident_update": opts.get("resident_update", 1 if resident else 0) if resident else 0,
+        "per_iteration_of_one_dispatch": persist,
         "fetch_size_kib_raw": f_spmv,
         "write_size_kib_raw": w_spmv,
         "fetch_calibration": {"kernel": "k_stream_a", "known_read_bytes": stream_read,
