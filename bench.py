@@ -492,7 +492,8 @@ def roofline_of(M, n, stencil, spmv_avg_s):
         "kernel": "%s: %s + p.Ap%s" % (KERNEL_NAMES[kfmt], FORMAT_NAMES[kfmt], " + p = r + beta p" if fused else ""),
         "bytes_per_launch": format_bytes,
         "bytes_formula": ("%g B per stored slot x %d slots + 32 B per row (r, p_{k-1} read; p_k, r "
-                          "written; Ap and the update stay in registers)" % (slot_bytes, slots) if resident else
+                          "written; Ap%s and the update stay in registers)" % (slot_bytes, slots, ", x" if persist else "")
+                          if resident else
                           "%g B per stored slot x %d slots + %d B per row (r, p_{k-1} read; p_k, Ap "
                           "written)" % (slot_bytes, slots, 32) if fused else
                           "%g B per stored slot x %d slots + 16 B per row (p read, Ap written)" % (slot_bytes, slots)) +

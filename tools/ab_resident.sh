@@ -1,6 +1,8 @@
-# Round-robin A/B of k_spmv_ar's slot-loop shapes at 100^3 (option
-# resident_update 0 = the unit + update-block launch, 1 = 3 early slots and
-# steps of 2, 2 = 3/3, 3 = 3/4, 4 = 7/4, 5 = 7/2), fresh process per line.
+# Round-robin A/B of the resident launches at 100^3 (option resident_update
+# 0 = the unit + update-block launch; k_spmv_ar 1 = 3 early slots and steps of
+# 2, 2 = 3/3, 3 = 3/4, 4 = 7/4, 5 = 7/2; the persistent k_cg_persist 6 = 2
+# early register slots + steps of 1, 7 = 1/2, 8 = 3 LDS-ring slots + steps of
+# 2 (auto), 9 = 3 ring/1, 10 = 4 ring/1), fresh process per line.
 export TMPDIR=/tmp; mkdir -p gpurun_out/abr; : > gpurun_out/abr/summary.log
 for rep in $(seq ${REPS:-2}); do
   for v in ${SHAPES:-0 1 2 3 4 5}; do
