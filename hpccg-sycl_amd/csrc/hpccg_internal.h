@@ -116,8 +116,9 @@ struct CgArgs {
     int dbg_resident_stall;       // debug (retry test): k_spmv_ar's p.Ap wait never sees the total (it expires)
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
-    double* pslots;               // persistent CG (resident 6): per iteration pslot_stride slots, emptied before the launch
+    double* pslots;               // persistent CG (resident >= 6): per iteration pslot_stride slots, emptied before the launch
     long long pslot_stride;
+    int pk0, pk1;                 // persistent CG: the launch runs iterations [pk0, pk1) (its window)
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
     unsigned long long* dbg_tl;   // diagnostics (option dbg_timeline): per unit 8 words of block clock stamps
                                   // (kTlWords below); null off. Only the timeline instantiation writes it.
@@ -254,6 +255,7 @@ int resident_capacity(bool nt);
 // capacity, the launch, and the slot fill (kSlotEmpty) that precedes it
 constexpr int kResidentPersist = 6;
 constexpr int kResidentAuto = 8;  // resident_update -1: the persistent launch with the 3-slot LDS ring
+constexpr int kPersistWindow = 512;  // iterations per persistent launch (its slots: 17 MB at 100^3)
 int persist_capacity(bool nt);
 void launch_cg_persist(const CgArgs& a, hipStream_t s);
 void launch_fill_empty(double* p, long long n, hipStream_t s);

@@ -1633,7 +1633,10 @@ __device__ __forceinline__ void st_rs(__amdgpu_buffer_rsrc_t rs, int byte, int r
 
 // Iteration k's slots: [which][nslices] partials, [which][ngroups] group sums,
 // [which][kNumXcd x kReadyStride] broadcast copies of the total.
-__device__ __forceinline__ double* pers_slots(const CgArgs& a, int k) { return a.pslots + (size_t)k * a.pslot_stride; }
+__device__ __forceinline__ double* pers_slots(const CgArgs& a, int k)
+{
+    return a.pslots + (size_t)(k - a.pk0) * a.pslot_stride;  // (the launch's window starts at pk0)
+}
 __device__ __forceinline__ double* pers_bcast(const CgArgs& a, int k, int which)
 {
     const int ng = ngroups_of(a);
@@ -1716,6 +1719,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     static_assert((kW - kPre) % kStep == 0 && (kL == 0 || kL == kPre), "slot steps");
     const int P = unit_of(a);
     if (P < 0) return;
+    if (a.pk0 > 1 && sld(a.kst + 1)) return;  // an earlier window ended the solve
     const int s0 = 2 * P;
     const int nsl = min(2, a.nslices - s0);
     const int s1 = nsl > 1 ? s0 + 1 : s0;
@@ -1769,8 +1773,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     const int pstr = (int)(a.pstride * 8);
     // the rows' x (in registers for the whole solve)
     Rows xv0 = ld(a.x + row0), xv1 = ld(a.x + row1);
-    double rr1 = a.g[kRRPar + 1];  // r_{k-1}.r_{k-1}: the prologue's r_0.r_0
-    double rr2 = 0.0;              // r_{k-2}.r_{k-2}
+    // r_{k-1}.r_{k-1} and r_{k-2}.r_{k-2}: the prologue's r_0.r_0 (k = 1), else
+    // the history the previous window left
+    double rr1 = a.pk0 == 1 ? a.g[kRRPar + 1] : a.hist[a.pk0 - 1];
+    double rr2 = a.pk0 == 1 ? 0.0 : a.hist[a.pk0 - 2];
     int role;
     {
         const UnitMap m = spmv_units(a, 2);
@@ -1782,10 +1788,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     __shared__ double tot_s;
     __shared__ int gave_up;
     const int lane = threadIdx.x & (kWave - 1);
-    int k = 1;
+    int k = a.pk0;
     for (;; k++) {
         // HPCCG.cpp:358
         const bool run = k < a.max_iter && sqrt(k == 1 ? rr1 : rr2) > a.tol;
+        if (run && k >= a.pk1) {  // the end of this launch's window: the next launch goes on from k
+            vm_wait(0);           // (the ring's last refill)
+            st_rows(a.x, row0, a.n, xv0);
+            if (nsl > 1) st_rows(a.x, row1, a.n, xv1);
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                a.hist[k - 1] = rr1;
+                a.kst[0] = k;
+                a.kst[2] = k;
+            }
+            return;
+        }
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             if (k == 1 || run) a.hist[k - 1] = rr1;
             if (run) stamp(a, k, kStampSpmv);

@@ -1473,17 +1473,20 @@ bool persist_ok(const hpccg_hip_matrix* M)
     if ((M->pstride * 2 + kGuardRows) * (long long)sizeof(double) >= (1LL << 31)) return false;
     return persist_capacity(image_big(M)) >= grid_of((M->nslices + 1) / 2);
 }
-// ... and its per-iteration slots are allocated for max_iter
+// ... and its per-iteration slots are allocated: one window of kPersistWindow
+// iterations per launch (a longer solve runs several launches)
+long long persist_slots_needed(const hpccg_hip_matrix* M, int max_iter)
+{
+    return (long long)std::min(std::max(max_iter - 1, 1), kPersistWindow) * persist_slot_stride((int)M->nslices);
+}
 bool persist_of(const hpccg_hip_matrix* M, int max_iter)
 {
-    return persist_ok(M) && M->d_pslots &&
-           M->pslots_cap >= (long long)(max_iter + 1) * persist_slot_stride((int)M->nslices);
+    return persist_ok(M) && M->d_pslots && M->pslots_cap >= persist_slots_needed(M, max_iter);
 }
-// iterations 0 .. max_iter, each with slots of its own
 int ensure_pslots(hpccg_hip_matrix* M, int max_iter)
 {
     if (!persist_ok(M)) return 0;
-    const long long need = (long long)(max_iter + 1) * persist_slot_stride((int)M->nslices);
+    const long long need = persist_slots_needed(M, max_iter);
     if (need > M->pslots_cap) {
         dev_free(M, &M->d_pslots, (size_t)M->pslots_cap);
         M->pslots_cap = 0;
@@ -2958,10 +2961,18 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     int done = 0;
     M->graph_used = 0;
     const bool persist = P == 1 && av[0].resident >= kResidentPersist;
-    if (persist) {  // every iteration in one launch (k_cg_persist), its slots emptied first
-        launch_fill_empty(M->d_pslots, (long long)(max_iter + 1) * av[0].pslot_stride, M->stream);
+    if (persist) {  // every iteration in one launch per window (k_cg_persist), its slots emptied first
         if (events && iters > 0) HIP_TRY(hipEventRecord(M->ev[4], M->stream));
-        launch_cg_persist(av[0], M->stream);
+        for (int k0 = 1; k0 == 1 || k0 <= iters; k0 += kPersistWindow) {
+            CgArgs w = av[0];
+            w.pk0 = k0;
+            w.pk1 = k0 + kPersistWindow;
+            launch_fill_empty(M->d_pslots, (long long)kPersistWindow * w.pslot_stride < M->pslots_cap
+                                               ? (long long)kPersistWindow * w.pslot_stride
+                                               : M->pslots_cap,
+                              M->stream);
+            launch_cg_persist(w, M->stream);
+        }
         if (events && iters > 0) HIP_TRY(hipEventRecord(M->ev[5], M->stream));
         HIP_TRY(hipGetLastError());
         done = iters;

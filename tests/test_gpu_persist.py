@@ -109,3 +109,25 @@ def test_persistent_retry_on_expired_wait(hp, gpu):
     assert _solve(hp, M, 60, gpu) == ref
     assert M.get_option("resident_update") == 0
     M.close()
+
+
+def test_persistent_windows(hp, gpu):
+    """A solve longer than one launch window (kPersistWindow = 512 iterations):
+    the second launch resumes from the state the first left (x stored, the r.r
+    history), bitwise the per-iteration launches -- to max_iter, and with a
+    tolerance exit inside the second window."""
+    M = hp.Matrix.generate(40, 36, 30)
+    M.set_option("resident_update", 0)
+    ref = _solve(hp, M, 1100, gpu)
+    tr = np.frombuffer(ref[2])
+    assert ref[0] > 700
+    tol = float(tr[700])
+    ref_tol = _solve(hp, M, 1100, gpu, tol=tol)
+    assert 512 < ref_tol[0] < 1099
+    M.set_option("resident_update", -1)
+    assert M.get_option("resident_update") == 8
+    assert _solve(hp, M, 1100, gpu) == ref
+    assert _solve(hp, M, 1100, gpu, tol=tol) == ref_tol
+    M.set_option("event_timing", 1)
+    assert _solve(hp, M, 1100, gpu) == ref
+    M.close()
