@@ -1741,19 +1741,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     __shared__ __attribute__((aligned(16))) double vring[kL > 0 ? kL * 2 * kBlock * kRpt : 2];
     const int wv = threadIdx.x / kWave;
     const int lane_ = threadIdx.x & (kWave - 1);
+    // (buffer form: the lane's byte offset in a VGPR, the slot's in an SGPR)
+    const __amdgpu_buffer_rsrc_t rsa = vec_rsrc(a.aval);
+    const int lb = lr * 8;
+    const int sb0 = s0 * kW * kSliceRows * 8, sb1 = s1 * kW * kSliceRows * 8;
     auto dma = [&](int j) {
-        __builtin_amdgcn_global_load_lds((const void*)(vp0 + (size_t)j * kSliceRows),
-                                         (lds_void*)(vring + ((j * 2 + 0) * 4 + wv) * (2 * kWave)), 16, 0,
-                                         kNT ? 2 : 0);
-        __builtin_amdgcn_global_load_lds((const void*)(vp1 + (size_t)j * kSliceRows),
-                                         (lds_void*)(vring + ((j * 2 + 1) * 4 + wv) * (2 * kWave)), 16, 0,
-                                         kNT ? 2 : 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_void*)(vring + ((j * 2 + 0) * 4 + wv) * (2 * kWave)), 16,
+                                                 lb, sb0 + j * kSliceRows * 8, 0, kNT ? 2 : 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_void*)(vring + ((j * 2 + 1) * 4 + wv) * (2 * kWave)), 16,
+                                                 lb, sb1 + j * kSliceRows * 8, 0, kNT ? 2 : 0);
     };
     auto lds_val = [&](int j, int h) -> Rows {
         const d2v t = *reinterpret_cast<const d2v*>(vring + ((j * 2 + h) * 4 + wv) * (2 * kWave) + 2 * lane_);
         return Rows{{t.x, t.y}};
     };
     constexpr int kA = (kL + 1) / 2;  // ring slots refilled during the p.Ap wait; the rest during the r.r wait
+
 #pragma unroll
     for (int j = 0; j < kL; j++) dma(j);
     // a raw workgroup barrier: __syncthreads() would drain the DMAs (vmcnt(0))
