@@ -1719,7 +1719,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     static_assert((kW - kPre) % kStep == 0 && (kL == 0 || kL == kPre), "slot steps");
     const int P = unit_of(a);
     if (P < 0) return;
-    if (a.pk0 > 1 && sld(a.kst + 1)) return;  // an earlier window ended the solve
+    // an earlier window ended the solve, or gave it up
+    if (a.pk0 > 1 && (sld(a.kst + 1) || sld(a.kst + kErrBase) != kErrNone)) return;
     const int s0 = 2 * P;
     const int nsl = min(2, a.nslices - s0);
     const int s1 = nsl > 1 ? s0 + 1 : s0;
