@@ -346,7 +346,8 @@ struct hpccg_hip_matrix {
     int* d_kst = nullptr;      // [0, kErrBase) iteration state, then the device error record (kErrWords)
     long long spin_us = kSpinTicksDefault / 100;  // bound of every in-kernel wait (option spin_budget_us)
     int dbg_withhold = 0;      // debug: slice + 1 whose p.Ap partial is withheld (guard test)
-    int dbg_resident_stall = 0;  // debug: k_spmv_ar's p.Ap wait expires (the retry test)
+    int dbg_resident_stall = 0;
+    int nt_load = -1;  // non-temporal matrix loads: -1 auto (image beyond the Infinity Cache), 0, 1  // debug: k_spmv_ar's p.Ap wait expires (the retry test)
     unsigned long long* d_tl = nullptr;  // diagnostics (dbg_timeline): per unit kTlWords block stamps
     int tl_units = 0;
     int solve_dirty = 0;       // a solve started and did not finish cleanly: reset the dot slots first
@@ -1134,6 +1135,9 @@ bool image_big(const hpccg_hip_matrix* M)
     return bytes > 256e6;
 }
 
+// Option nt_load (A/B): the matrix streams' cache policy (non-temporal loads)
+bool nt_load_of(const hpccg_hip_matrix* M) { return M->nt_load >= 0 ? M->nt_load != 0 : image_big(M); }
+
 bool kernel_available(const hpccg_hip_matrix* M, int k)
 {
     if (k == kSpmvSell) return M->has_sell;
@@ -1453,7 +1457,7 @@ bool resident_of(const hpccg_hip_matrix* M)
         M->kernel != kSpmvDirect || M->a_width != 27 || !fuse_update_effective(M))
         return false;
     const int pairs = (M->nslices + 1) / 2;
-    return resident_capacity(image_big(M)) >= grid_of(pairs);
+    return resident_capacity(nt_load_of(M)) >= grid_of(pairs);
 }
 
 // The persistent CG launch (k_cg_persist; option resident_update -1 auto or
@@ -1471,7 +1475,7 @@ bool persist_ok(const hpccg_hip_matrix* M)
     if (!persist_shape(M) || !resident_of(M)) return false;
     // (byte offsets of the p ring in 32 bits)
     if ((M->pstride * 2 + kGuardRows) * (long long)sizeof(double) >= (1LL << 31)) return false;
-    return persist_capacity(image_big(M)) >= grid_of((M->nslices + 1) / 2);
+    return persist_capacity(nt_load_of(M)) >= grid_of((M->nslices + 1) / 2);
 }
 // ... and its per-iteration slots are allocated: one window of kPersistWindow
 // iterations per launch (a longer solve runs several launches)
@@ -1539,7 +1543,7 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.sn0 = units;
     a.s1 = a.sn1 = 0;
     a.sgrid = grid_of(units);
-    a.nt = image_big(M) ? 1 : 0;
+    a.nt = nt_load_of(M) ? 1 : 0;
     a.a_width = M->a_width;
     a.apre = M->a_pre;
     a.ahist = M->d_ahist;
@@ -3972,6 +3976,9 @@ int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value)
             M->tl_units = 3 * M->nslices + 1024;  // >= the blocks of any SpMV launch (units, side, ghost, update)
             TRY(dev_alloc(M, &M->d_tl, (size_t)M->tl_units * kTlWords, true));
         }  // the graph cache compares the kernel arguments: a changed dbg_tl re-captures
+    } else if (!std::strcmp(key, "nt_load")) {
+        if (value < -1 || value > 1) return set_err(HPCCG_HIP_EINVAL, "nt_load: -1 (auto), 0 or 1");
+        M->nt_load = (int)value;
     } else if (!std::strcmp(key, "dbg_resident_stall")) {
         M->dbg_resident_stall = value ? 1 : 0;
     } else if (!std::strcmp(key, "dbg_withhold")) {
@@ -4049,7 +4056,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "has_pairs")) *value = M->has_pairs;
     else if (!std::strcmp(key, "a_width")) *value = M->a_width;
     else if (!std::strcmp(key, "lds_doubles")) *value = M->has_pairs ? M->alds2_doubles : 0;
-    else if (!std::strcmp(key, "nt")) *value = image_big(M) ? 1 : 0;
+    else if (!std::strcmp(key, "nt")) *value = nt_load_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "device_bytes")) *value = M->bytes;
     else if (!std::strcmp(key, "placement_pick")) *value = M->place_pick;
     else if (!std::strcmp(key, "peer_auto_ok")) *value = M->peer_auto_ok;
