@@ -156,6 +156,32 @@ def test_oracle_vs_live_reference_extra_sizes():
 
 
 @pytest.mark.skipif(not oracle.ref_available(), reason="reference build only in the dev container")
+@pytest.mark.parametrize("nx,ny,nz,ranks", [(16, 16, 16, 8), (8, 8, 8, 2)])
+def test_zstacked_goldens_matrix_is_the_reference_generators(nx, ny, nz, ranks):
+    """The z-stacked goldens (27pt_16x16x16_x8ranks, 27pt_8x8x8_x2ranks) were
+    solved by the reference on the oracle's global matrix. With MPI, rank r of
+    the reference's generate_matrix builds global rows start_row = nx*ny*nz*r
+    ... with global columns checked against total_nrow = nx*ny*nz*size
+    (generate_matrix.cpp:225-266): exactly rows [start_row, stop_row] of the
+    serial generate_matrix(nx, ny, nz*size). So the unmodified reference
+    generator, run serially on the global dims, pins those matrices too: CSR,
+    b, x and xexact bitwise, and every slab's columns stay within one plane of
+    its rows (the z-slab halo exchange_externals moves)."""
+    M, x0, b, xe = oracle.ref_generate(nx, ny, nz * ranks)
+    rp, cols, vals = M.to_csr()
+    A = oracle.generate(nx, ny, nz * ranks)
+    assert np.array_equal(rp, A.row_ptr) and np.array_equal(cols, A.cols)
+    assert np.array_equal(vals, A.vals) and np.array_equal(b, A.b)
+    assert np.array_equal(x0, A.x) and np.array_equal(xe, A.xexact)
+    M.close()
+    n_loc, plane = nx * ny * nz, nx * ny
+    for r in range(ranks):
+        lo, hi = rp[r * n_loc], rp[(r + 1) * n_loc]
+        c = cols[lo:hi]
+        assert c.min() >= max(0, r * n_loc - plane) and c.max() < min(ranks * n_loc, (r + 1) * n_loc + plane)
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="reference build only in the dev container")
 def test_reference_build_not_interposed_by_our_library(hp, golden):
     """Our libhpccg_hip.so exports the drop-in HPCCG() symbol; the reference
     build (linked -Bsymbolic, ours loaded RTLD_LOCAL) must still run its own
