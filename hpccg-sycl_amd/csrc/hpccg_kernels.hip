@@ -457,6 +457,26 @@ __device__ __forceinline__ double top_sum_wave(Ld ld, int ng, int lane)
     return s;
 }
 
+// The same sum from values already polled (ng <= kTopThreads: lane l of chunk
+// c holds group c * kWave + l in w[c]): top_sum_wave's exact operations,
+// without loading the group sums a second time after the poll that found them
+// all full (one round trip less on the dot's critical path).
+constexpr int kTopChunks = kTopThreads / kWave;
+__device__ __forceinline__ double top_sum_polled(const double (&w)[kTopChunks], int ng, int lane)
+{
+    double v[kTopChunks];
+#pragma unroll
+    for (int vw = 0; vw < kTopChunks; vw++) {
+        v[vw] = 0.0;
+        const double t = vw * kWave + lane < ng ? w[vw] : 0.0;
+        if (vw * kWave < ng) v[vw] += t;
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int vw = 0; vw < kTopChunks; vw++) s += wave_sum(v[vw]);
+    return s;
+}
+
 // Peer-memory all-reduce of one CG scalar (MPI_Allreduce in ddot.cpp:79-80),
 // one lane: this rank's local sum into slot [which][k & 1][prank] of every
 // rank's mailbox (system-scope stores: the mailboxes of other GPUs are
@@ -585,11 +605,19 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
         v = wave_sum(v);
         if (lane == 0) st_sc1(gp + g, v);
         if (g != top_group(m)) return;
+        double wp[kTopChunks] = {0.0, 0.0, 0.0, 0.0};  // (the polled group sums, ng <= kTopThreads)
+        static_assert(kTopChunks == 4, "wp");
         for (int j0 = 0; j0 < ng; j0 += kWave) {  // every other group's reducer came before
             for (;;) {
                 const int j = j0 + lane;
                 const double w = j < ng ? ld_sc1(gp + j) : 0.0;
-                if (__all(j >= ng || slot_full(w))) break;
+                if (__all(j >= ng || slot_full(w))) {
+                    if (j0 == 0) wp[0] = w;
+                    else if (j0 == kWave) wp[1] = w;
+                    else if (j0 == 2 * kWave) wp[2] = w;
+                    else if (j0 == 3 * kWave) wp[3] = w;
+                    break;
+                }
                 if ((++polls & 15) == 0 && wait_expired(a, t0)) {
                     if (lane == 0) abort_solve(a, kErrTopWait, j0, k, which);
                     return;
@@ -597,7 +625,8 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
                 __builtin_amdgcn_s_sleep(1);
             }
         }
-        const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
+        const double tot = ng <= kTopThreads ? top_sum_polled(wp, ng, lane)
+                                             : top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
         for (int j = lane; j < ng; j += kWave) st_sc1(gp + j, slot_empty());
         if (lane == 0) finish_dot(a, tot, which, k);
         return;
@@ -1672,11 +1701,18 @@ __device__ __forceinline__ void pers_dot(const CgArgs& a, int role, int s0, int 
     v = wave_sum(v);
     if (lane == 0) st_sc1(gp + g, v);
     if (!(role & 2)) return;
+    double wp[kTopChunks] = {0.0, 0.0, 0.0, 0.0};  // (the polled group sums, ng <= kTopThreads)
     for (int j0 = 0; j0 < ng; j0 += kWave) {
         for (;;) {
             const int j = j0 + lane;
             const double w = j < ng ? ld_sc1(gp + j) : 0.0;
-            if (__all(j >= ng || slot_full(w))) break;
+            if (__all(j >= ng || slot_full(w))) {
+                if (j0 == 0) wp[0] = w;
+                else if (j0 == kWave) wp[1] = w;
+                else if (j0 == 2 * kWave) wp[2] = w;
+                else if (j0 == 3 * kWave) wp[3] = w;
+                break;
+            }
             if ((++polls & 15) == 0 && wait_expired(a, t0)) {
                 if (lane == 0) abort_solve(a, kErrTopWait, j0, k, which);
                 return;
@@ -1684,12 +1720,12 @@ __device__ __forceinline__ void pers_dot(const CgArgs& a, int role, int s0, int 
             __builtin_amdgcn_s_sleep(1);
         }
     }
-    const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
-    if (lane == 0) {
-        double* const bc = pers_bcast(a, k, which);
-        for (int j = 0; j < kNumXcd; j++) st_sc1(bc + kReadyStride * j, tot);
-        stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
-    }
+    // top_sum_wave's shape from the polled values: no second round trip
+    double tot = ng <= kTopThreads ? top_sum_polled(wp, ng, lane)
+                                   : top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
+    tot = __shfl(tot, 0, kWave);
+    if (lane < kNumXcd) st_sc1(pers_bcast(a, k, which) + kReadyStride * lane, tot);  // the 8 copies at once
+    if (lane == 0) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
 }
 
 // One lane per block: iteration k's total of dot `which` (bounded wait).
