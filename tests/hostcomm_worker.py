@@ -7,6 +7,11 @@ planes pulled from the other process's memory (exchange_externals.cpp:
 51-131). Writes <out>/rank<r>.json (+ .npy vectors) for the test to check.
 
     python -m torch.distributed.run --nproc-per-node 2 tests/hostcomm_worker.py <out_dir>
+    python -m torch.distributed.run --nproc-per-node 8 tests/hostcomm_worker.py <out_dir> eight
+
+"eight": the 8-process job (the world size of the driver's 8-GPU run) on one
+GPU: the reference's 8-rank golden (27pt_16x16x16_x8ranks) through the default
+transport, every rank's mailbox mapped by the seven others.
 """
 import json
 import os
@@ -87,6 +92,9 @@ def main():
         M.close()
         return out
 
+    if len(sys.argv) > 2 and sys.argv[2] == "eight":
+        case("golden27x8", lambda: golden_case("27pt_16x16x16_x8ranks"))
+        return finish(res, out_dir, rank, hp, dist)
     case("golden27", lambda: golden_case("27pt_8x8x8_x2ranks"))
     case("golden7", lambda: golden_case("7pt_12x10x8_x2ranks"))
 
@@ -159,6 +167,10 @@ def main():
         return {"kat1": kat1, "rr": rr, "kat2": float(kat2_rr0(nx, ny, nz * world))}
 
     case("kernel_level", kernel_level)
+    finish(res, out_dir, rank, hp, dist)
+
+
+def finish(res, out_dir, rank, hp, dist):
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
         json.dump(res, f)
     hp.comm_destroy()

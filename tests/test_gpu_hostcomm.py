@@ -149,3 +149,33 @@ def test_hostcomm_kernel_level(hostcomm):
     for c in _case(res, "kernel_level"):
         assert c["kat1"]
         assert c["rr"] == c["kat2"]
+
+
+def test_hostcomm_eight_processes_golden(tmp_path, gpu):
+    """Eight processes on one GPU -- the world size of the driver's 8-GPU run --
+    through the default transport: every rank maps the seven other mailboxes
+    (the in-kernel all-reduce sums eight contributions in rank order) and pulls
+    its ghost planes from its z-neighbours' memory; all creation-time
+    self-tests pass on every rank and the solve meets the reference's 8-rank
+    golden (27pt_16x16x16_x8ranks: 16x16x128 global) at RTRANS_RTOL_MULTI.
+    Same caveats as above: no xGMI here."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    port = 29300 + os.getpid() % 250
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), WORKER, str(tmp_path), "eight"],
+                       env=env, capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-4000:]
+    res = []
+    for q in range(8):
+        with open(tmp_path / f"rank{q}.json") as f:
+            res.append(json.load(f))
+    assert len({d["pci"] for d in res}) == 1 and all(d["comm_mode"] == "host" for d in res)
+    cs = _case(res, "golden27x8")
+    for c in cs:
+        t = c["transport"]
+        assert t["peer_allreduce"] == 1 and t["halo_pull"] == 2 and t["rhalo"] == 1, t
+        assert t["peer_auto_ok"] == 1 and t["pull_auto_ok"] == 1 and t["proto_auto_ok"] == 1, t
+        assert c["checked"] >= 5 and c["x_err"] <= 1e-12
+        assert c["kpull_same"] and c["eager_same"]
+    # every rank reports the same global solve
+    assert len({(c["niters"], c["normr"]) for c in cs}) == 1
