@@ -131,3 +131,28 @@ def test_persistent_windows(hp, gpu):
     M.set_option("event_timing", 1)
     assert _solve(hp, M, 1100, gpu) == ref
     M.close()
+
+
+@pytest.mark.parametrize("dims,it", [((3, 3, 3), 30), ((5, 7, 9), 60), ((101, 101, 101), 40)])
+def test_persistent_edge_sizes(hp, gpu, dims, it):
+    """The smallest shapes that take the persistent launch (one slice, a short
+    odd slab) and the largest (101^3: 1008 pair blocks of the 1024 the chip
+    holds at 4 per CU), bitwise the per-iteration launches."""
+    M = hp.Matrix.generate(*dims)
+    assert M.get_option("resident_update") == 8
+    ref_default = _solve(hp, M, it, gpu)
+    M.set_option("resident_update", 0)
+    assert _solve(hp, M, it, gpu) == ref_default
+    M.close()
+
+
+def test_persistent_not_taken_beyond_the_chip(hp, gpu):
+    """102^3 has more pair blocks (1061) than the chip holds at once: auto
+    keeps the per-iteration launches (resident_update reads 0)."""
+    M = hp.Matrix.generate(102, 102, 102)
+    b, _, _ = M.vectors()
+    import torch
+    x = torch.zeros(102 ** 3, dtype=torch.float64, device=gpu)
+    hp.HPCCG(M, b, x, max_iter=5, device=True)
+    assert M.get_option("resident_update") == 0
+    M.close()
