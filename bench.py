@@ -236,7 +236,7 @@ def placement_report(tries, probe_us, pick):
     us = [float(v) for v in probe_us]
     creation, kept = us[0], min(us)
     return {"ran": True, "requested": tries,
-            "note": "setup, untimed: CG iterations timed on contiguous candidate placements of the values, the "
+            "note": "setup, untimed: CG iterations timed on candidate placements (plain allocations) of the values, the "
                     "p ring, r and Ap, fastest kept; rank 0's",
             "creation_us_per_iteration": round(creation, 2), "kept_us_per_iteration": round(kept, 2),
             "gain_frac": round(creation / kept - 1.0, 4),
