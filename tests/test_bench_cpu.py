@@ -106,3 +106,35 @@ def test_bench_multirank_line_schema():
     assert mr["frac_max_over_ranks"] == pytest.approx(2.05e9 / 350e-6 / 1e9 / 8000.0, rel=1e-3)
     assert mr["transport_used"].startswith("in-kernel")
     assert len(mr["verdicts_per_rank"]) == 2
+
+
+class _FakeInfoM(_FakeM):
+    def __init__(self, opts, info):
+        super().__init__(opts)
+        self._info = info
+
+    def info(self):
+        return self._info
+
+
+@pytest.mark.parametrize("ru,kname", [(8, "k_cg_persist"), (1, "k_spmv_ar"), (0, "k_spmv_a")])
+def test_roofline_bytes_per_launch_by_resident_mode(ru, kname):
+    """bench.roofline_of's compulsory bytes for the 100^3 launch forms: the
+    persistent launch (per iteration: 8 B per slot + 32 B per row, no side
+    blocks -- x stays in registers -- and no update blocks), k_spmv_ar (side
+    blocks, no update blocks), the unit + update-block launch (both)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    n = 100
+    nrow, slots = n ** 3, 27012096
+    opts = {"spmv_kernel": 1, "a2_ring": 3, "resident_update": ru, "fuse_p": 1, "x_defer": 2, "x_ring": 32,
+            "fuse_update": 1, "nt": 0}
+    M = _FakeInfoM(opts, {"nrow": nrow, "nnz": 26463592, "slots": slots})
+    roof, kernel, kfmt, fused, fupd = bench.roofline_of(M, n, 27, 45e-6)
+    assert roof["kernel"].startswith(kname + ":")
+    q = 31
+    side = (16.0 + 8.0 * q) / q * nrow
+    expect = 8.0 * slots + 32.0 * nrow + (0.0 if ru >= 6 else side) + (24.0 * nrow if ru == 0 else 0.0)
+    assert roof["bytes_per_launch"] == pytest.approx(expect)
+    assert roof["frac"] == pytest.approx(expect / 45e-6 / 1e9 / bench.HBM_PEAK_GBS, rel=1e-3)
+    assert ("launch_note" in roof) == (ru >= 6)
