@@ -36,16 +36,27 @@ roofline (the SpMV kernel, 84 % of the reference's time):
   SURVEY 8(d)'s fixed formula (12 nnz + 20 n SpMV + ddot/waxpby bytes the
   fused kernel absorbs) is reported as bytes only.
 cpu_baseline: the reference compiled from its own sources (oracle/_ref) on
-  a bounded sample of the same problem, rank 0. N = 1: three legs, the
-  OpenMP build with one thread per physical core of this process's CPU mask
-  (the full-host bar), the OpenMP build with the box's thread share
-  (OMP_NUM_THREADS), and the serial build; value = the fastest. N > 1: the
-  reference on the global nx x ny x (N nz) problem with the
-  box's thread share, sampled iterations; value in the same unit as the line's
-  (global-problem iterations/s x N, i.e. per-GPU-slab iterations summed).
-secondary (N = 1): the other single-GPU configs of BASELINE.json (27-pt 100^3,
-  7-pt 256^3) measured in the same run the same way: value, launch time,
-  compulsory-byte fraction, committed PMC traffic ratio; no CPU leg.
+  a bounded sample of the same problem, run by rank 0 after every GPU step in
+  a fresh child process (`bench.py --cpu-child`) whose CPU mask is widened to
+  the job's whole cpuset (cgroup cpuset.cpus.effective) before any OpenMP
+  runtime loads -- never the launched rank's own, possibly narrowed, mask.
+  Legs: the OpenMP build with one thread per physical core of that mask,
+  capped by the cgroup CPU quota (the host bar), the OpenMP build with the
+  box's thread share (OMP_NUM_THREADS) when that differs, and (N = 1) the
+  serial build; value = the fastest leg, cores = its thread count. N > 1: the
+  reference on the global nx x ny x (N nz) problem; value in
+  the same unit as the line's (global-problem iterations/s x N, i.e.
+  per-GPU-slab iterations summed).
+check.trace_vs_oracle: the same child runs the oracle (oracle/hpccg_oracle.c,
+  pinned to the reference) on the GLOBAL problem for its first iterations and
+  rank 0 compares its GPU rtrans trace point by point above the 1e-20 cutoff
+  (tests/conftest.py's stated tolerance: 1e-8 on one rank, 1e-7 over ranks);
+  a failed check makes the run exit 3 after the line is printed.
+secondary: the other configs of BASELINE.json measured in the same run the
+  same way -- N = 1: 27-pt 100^3 and 7-pt 256^3; N > 1: 27-pt 100^3 per GPU,
+  weak-scaled like the headline (north_star's second size at 1/2/4/8 GPUs):
+  value, launch time, compulsory-byte fraction, committed PMC traffic ratio,
+  its own trace check; no CPU leg.
 
 Multi-GPU runs describe themselves: every rank logs its stages on stderr
 (comm init, setup, first solve, timed steps), the line carries what RCCL
@@ -63,19 +74,20 @@ import subprocess
 import sys
 import time
 
-# the OpenMP leg of the CPU baseline: libgomp reads these when it first loads
-# (torch loads it), so they are set before anything is imported
-# (the process's CPU mask is read here too: libgomp later binds the main
-# thread to its first place). The box's share is OMP_NUM_THREADS (16 there);
-# spread over cores, so the threads reach more memory channels than 16
-# neighbouring cores would (the reference is memory-bound on the host too).
+# This process's CPU mask at start-up, for the record only: the CPU legs run
+# in a child that widens its own mask (cpu_child). No OpenMP binding variables
+# are set here: exported into the environment they would make torch's libgomp
+# bind this process -- and a torch.distributed.run launched from it, and so
+# every rank -- to a single core.
 AFFINITY_MASK = sorted(os.sched_getaffinity(0))
 AFFINITY_CPUS = len(AFFINITY_MASK)
-os.environ.setdefault("OMP_NUM_THREADS", str(AFFINITY_CPUS))
-os.environ.setdefault("OMP_PROC_BIND", "spread")
-os.environ.setdefault("OMP_PLACES", "cores")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# tests/conftest.py's stated fp64 parity tolerance on rtrans = normr^2
+RTRANS_RTOL_1GPU = 1e-8
+RTRANS_RTOL_MULTI = 1e-7
+RTRANS_CUTOFF = 1e-20
+TRACE_MIN_POINTS = 5
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 COPY_CEILING_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy, measured
 KERNEL_NAMES = {0: "k_spmv_sell", 1: "k_spmv_a", 2: "k_spmv_a2", 3: "k_spmv_a2r", 4: "k_spmv_ar", 5: "k_cg_persist"}
@@ -108,10 +120,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def host_cpu():
-    """CPU model and counts of the host (lscpu), and this process's affinity."""
-    info = {"affinity_cpus": AFFINITY_CPUS, "omp_proc_bind": os.environ.get("OMP_PROC_BIND"),
-            "omp_places": os.environ.get("OMP_PLACES")}
+def host_cpu(mask=None):
+    """CPU model and counts of the host (lscpu), the CPU mask the legs ran on
+    and the one this (launched) process started with."""
+    info = {"affinity_cpus": len(mask) if mask is not None else AFFINITY_CPUS,
+            "launch_affinity_cpus": AFFINITY_CPUS,
+            "omp_proc_bind": os.environ.get("OMP_PROC_BIND"), "omp_places": os.environ.get("OMP_PLACES")}
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         for line in out.splitlines():
@@ -121,25 +135,58 @@ def host_cpu():
                 info[k] = v
     except Exception as e:  # reported, not fatal
         info["lscpu_error"] = repr(e)
-    # the process's CPU bandwidth quota (cgroup v2 cpu.max "quota period"): on a
-    # shared box it, not the affinity mask, bounds how many threads run at once
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            q, per = f.read().split()
-        info["cgroup_cpu_max"] = f"{q} {per}"
-        if q != "max":
-            info["cgroup_cpu_quota_cores"] = round(int(q) / int(per), 2)
-    except (OSError, ValueError):
-        pass
+    q = cgroup_quota()
+    if q is not None:
+        info["cgroup_cpu_max"] = q[0]
+        if q[1] is not None:
+            info["cgroup_cpu_quota_cores"] = round(q[1], 2)
     return info
 
 
-def physical_cores():
-    """Physical cores (distinct package/core ids) among this process's CPUs,
-    from the mask read at start-up (libgomp later binds the main thread to
-    one place, so the mask at call time can be a single CPU)."""
+def cgroup_quota():
+    """The cgroup v2 CPU bandwidth quota ("quota period", cores or None when
+    unlimited): on a shared box it, not the affinity mask, bounds how many
+    threads run at once. None when the file is absent."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+    except (OSError, ValueError):
+        return None
+    return f"{q} {per}", (None if q == "max" else int(q) / int(per))
+
+
+def parse_cpulist(txt):
+    """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11}."""
+    cpus = set()
+    for part in txt.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def job_cpuset():
+    """The CPUs the job's cgroup may use (cpuset.cpus.effective), else every
+    online CPU."""
+    for p in ("/sys/fs/cgroup/cpuset.cpus.effective", "/sys/fs/cgroup/cpuset/cpuset.effective_cpus"):
+        try:
+            with open(p) as f:
+                cpus = parse_cpulist(f.read())
+            if cpus:
+                return cpus, p
+        except (OSError, ValueError):
+            continue
+    try:
+        with open("/sys/devices/system/cpu/online") as f:
+            return parse_cpulist(f.read()), "/sys/devices/system/cpu/online"
+    except (OSError, ValueError):
+        return set(range(os.cpu_count() or 1)), "os.cpu_count()"
+
+
+def physical_cores(mask):
+    """Physical cores (distinct package/core ids) among the CPUs of `mask`."""
     cores = set()
-    for c in AFFINITY_MASK:
+    for c in mask:
         t = f"/sys/devices/system/cpu/cpu{c}/topology"
         try:
             with open(f"{t}/physical_package_id") as f1, open(f"{t}/core_id") as f2:
@@ -149,65 +196,192 @@ def physical_cores():
     return len(cores)
 
 
-def cpu_baseline(nx, ny, nz, use_7pt, budget_s=15.0, budget_1t_s=10.0):
-    """The reference (oracle/_ref: its own sources compiled in this repo's
-    recipe) on the host cores, bounded: the first iterations of one HPCCG()
-    solve of the same matrix; OpenMP with one thread per physical core of the
-    process's CPU mask (full host), OpenMP with the box's thread share, serial."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def host_threads(mask):
+    """One OpenMP thread per physical core of `mask`, capped by the cgroup CPU
+    quota (more threads than the quota's cores only time-slice)."""
+    phys = physical_cores(mask)
+    q = cgroup_quota()
+    if q is not None and q[1] is not None:
+        return max(1, min(phys, int(q[1]))), phys
+    return max(1, phys), phys
+
+
+def rtrans_check(gpu_tr, ref_tr, rtol):
+    """tests/conftest.py check_trace as a record: every k with
+    rtrans_ref,k >= 1e-20 rtrans_ref,0 (rtrans = normr^2) compared at `rtol`;
+    ok when no point exceeds it and at least TRACE_MIN_POINTS were compared."""
+    g = [float(v) for v in gpu_tr]
+    r = [float(v) for v in ref_tr]
+    if not g or not r:
+        return {"checked": 0, "max_rel": None, "rtol": rtol, "ok": False, "note": "empty trace"}
+    r0 = r[0] ** 2
+    checked, max_rel, first_bad = 0, 0.0, None
+    for k in range(min(len(g), len(r))):
+        rr = r[k] ** 2
+        if rr < RTRANS_CUTOFF * r0:
+            break
+        rel = abs(g[k] ** 2 - rr) / rr if rr > 0 else abs(g[k] ** 2)
+        if rel > rtol and first_bad is None:
+            first_bad = k
+        max_rel = max(max_rel, rel)
+        checked += 1
+    return {"checked": checked, "max_rel": max_rel, "rtol": rtol, "first_failing_k": first_bad,
+            "ok": first_bad is None and checked >= TRACE_MIN_POINTS}
+
+
+def _ref_legs(oracle, A, legs, nx, ny, nz, use_7pt, world):
+    """The reference's HPCCG() (oracle/_ref) on `A`, one bounded solve per
+    leg (the first iterations of it, sized by a 3-iteration probe)."""
     import ctypes
-    import oracle  # test infrastructure: baseline leg only
-    share = int(os.environ["OMP_NUM_THREADS"])
-    phys = physical_cores()
-    A = oracle.generate(nx, ny, nz, use_7pt=use_7pt)
-    out = {"unit": "CG iterations/s", "host": host_cpu()}
-    out["host"]["physical_cores_in_affinity"] = phys
-    legs = []
-    if os.path.exists(oracle.REF_OMP_SO):
-        legs.append(("full_host", phys, budget_s))
-        if share != phys:
-            legs.append(("box_share", share, budget_s))
-    if os.path.exists(oracle.REF_SO):
-        legs.append(("serial", 1, budget_1t_s))
-    if not legs:
-        raise RuntimeError("oracle/_ref is not built (make -C oracle ref)")
     gomp = ctypes.CDLL("libgomp.so.1") if os.path.exists(oracle.REF_OMP_SO) else None  # the ref build's runtime
-    # the reference prints residual lines on fd 1: keep bench stdout to one JSON line
-    saved = os.dup(1)
+    out = {}
+    mats = {}
+    saved = os.dup(1)  # the reference prints its residual lines on fd 1
     null = os.open(os.devnull, os.O_WRONLY)
     os.dup2(null, 1)
     try:
         for leg, nthreads, budget in legs:
-            if leg != "serial":
+            omp = leg != "serial"
+            if omp:
                 gomp.omp_set_num_threads(nthreads)
-            M = oracle.ref_from_csr(A, omp=(leg != "serial"))
-            probe = 3
+            if omp not in mats:
+                mats[omp] = oracle.ref_from_csr(A, omp=omp)
+            M = mats[omp]
+            probe = 2 if world > 1 else 3
             t = oracle.ref_hpccg(M, A.b, max_iter=probe + 1)["times"][0]
-            per_it = max(t / probe, 1e-6)
-            iters = int(max(3, min(500, budget / per_it)))
+            iters = int(max(probe, min(500, budget / max(t / probe, 1e-6))))
             res = oracle.ref_hpccg(M, A.b, max_iter=iters + 1)
-            M.close()
             its = res["niters"] / res["times"][0]
-            sample = (f"{nx}x{ny}x{nz} {'7' if use_7pt else '27'}-pt, first {res['niters']} CG iterations of one "
-                      f"reference HPCCG() solve ({res['times'][0]:.1f} s)")
+            what = (f"global {nx}x{ny}x{nz} (the {world} slabs together)" if world > 1 else f"{nx}x{ny}x{nz}")
+            sample = (f"{what} {'7' if use_7pt else '27'}-pt, first {res['niters']} CG iterations of one reference "
+                      f"HPCCG() solve ({res['times'][0]:.1f} s)")
             desc = (f", OpenMP {nthreads} threads (OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
-                    f"OMP_PLACES={os.environ.get('OMP_PLACES')})" if leg != "serial" else ", serial")
-            out.setdefault("legs", {})[leg] = {"value": its, "threads": nthreads, "physical_cores": phys,
-                                               "kind": "reference", "sample": sample + desc}
-            if leg == "serial":
-                out["single_thread"] = {"value": its, "cores": 1, "kind": "reference", "sample": sample + desc}
+                    f"OMP_PLACES={os.environ.get('OMP_PLACES')})" if omp else ", serial")
+            out[leg] = {"value": its * world, "global_iterations_per_s": its, "threads": nthreads,
+                        "kind": "reference", "sample": sample + desc}
     finally:
-        import ctypes
         ctypes.CDLL(None).fflush(None)
         os.dup2(saved, 1)
         os.close(null)
         os.close(saved)
-    # headline: the fastest leg (the strongest CPU bar on this host)
-    best_leg = max(out["legs"], key=lambda k: out["legs"][k]["value"])
-    best = out["legs"][best_leg]
-    out.update({"value": best["value"], "cores": best["threads"], "threads": best["threads"],
-                "physical_cores": phys, "kind": "reference", "leg": best_leg, "sample": best["sample"]})
+        for M in mats.values():
+            M.close()
     return out
+
+
+def _oracle_trace(oracle, A, nthreads, iters, budget_s):
+    """The oracle's HPCCG() (hpccg_oracle.c: HPCCG.cpp:312-402 restated,
+    pinned to the reference) on `A`: the rtrans trace of its first iterations
+    (at most `iters`, fewer when a 2-iteration probe says the budget is short)."""
+    t0 = time.perf_counter()
+    oracle.hpccg(A, max_iter=3, nthreads=nthreads, trace=False)
+    per_it = max((time.perf_counter() - t0) / 2, 1e-6)
+    k = int(max(TRACE_MIN_POINTS + 2, min(iters, budget_s / per_it)))
+    t0 = time.perf_counter()
+    res = oracle.hpccg(A, max_iter=k + 1, nthreads=nthreads, trace=True)
+    return {"trace": [float(v) for v in res["trace"]], "iterations": res["niters"],
+            "seconds": round(time.perf_counter() - t0, 2), "threads": nthreads}
+
+
+def cpu_child(spec_path, out_path):
+    """`bench.py --cpu-child SPEC OUT`: rank 0's CPU work, in a fresh process
+    that has touched no GPU. The mask is widened to the job's cpuset before
+    any OpenMP runtime loads; then the reference's legs on the baseline
+    problem and the oracle's traces of the listed (global) problems; the
+    result goes to OUT as JSON."""
+    with open(spec_path) as f:
+        spec = json.load(f)
+    launch_mask = sorted(os.sched_getaffinity(0))
+    want, src = job_cpuset()
+    try:
+        os.sched_setaffinity(0, want)
+    except OSError as e:
+        log(f"cpu-child: could not widen the CPU mask to {src}: {e!r}")
+    mask = sorted(os.sched_getaffinity(0))
+    threads, phys = host_threads(mask)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    # before libgomp loads (the oracle and the reference build both use it)
+    os.environ.update(OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="spread", OMP_PLACES="cores")
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the baseline leg and the trace check only
+    result = {"mask": {"launch_cpus": len(launch_mask), "cpus": len(mask), "cpuset_source": src,
+                       "physical_cores": phys, "threads": threads}, "traces": {}}
+    cache = {}
+
+    def problem(nx, ny, nz, use_7pt):
+        key = (nx, ny, nz, use_7pt)
+        if key not in cache:
+            cache.clear()  # one global problem in memory at a time
+            cache[key] = oracle.generate(nx, ny, nz, use_7pt=use_7pt)
+        return cache[key]
+
+    base = spec.get("baseline")
+    if base:
+        t0 = time.time()
+        try:
+            A = problem(base["nx"], base["ny"], base["nz"], base["use_7pt"])
+            setup_s = time.time() - t0
+            world = base["world"]
+            legs = []
+            if os.path.exists(oracle.REF_OMP_SO):
+                legs.append(("host", threads, base["budget_s"]))
+                if share and share != threads:
+                    legs.append(("box_share", share, base["budget_s"]))
+            if world == 1 and os.path.exists(oracle.REF_SO):
+                legs.append(("serial", 1, base["budget_1t_s"]))
+            if not legs:
+                raise RuntimeError("oracle/_ref is not built (make -C oracle ref)")
+            out = {"unit": "CG iterations/s" if world == 1 else
+                   "CG iterations/s (global-problem iterations x %d slabs)" % world,
+                   "legs": _ref_legs(oracle, A, legs, base["nx"], base["ny"], base["nz"], base["use_7pt"], world),
+                   "host": host_cpu(mask), "setup_s": round(setup_s, 1)}
+            out["host"]["physical_cores_in_affinity"] = phys
+            out["host"]["cpuset_source"] = src
+            best_leg = max(out["legs"], key=lambda k: out["legs"][k]["value"])
+            best = out["legs"][best_leg]
+            out.update({"value": best["value"], "cores": best["threads"], "threads": best["threads"],
+                        "physical_cores": phys, "kind": "reference", "leg": best_leg, "sample": best["sample"]})
+            if world > 1:
+                out["global_iterations_per_s"] = best["global_iterations_per_s"]
+            if "serial" in out["legs"]:
+                s = out["legs"]["serial"]
+                out["single_thread"] = {"value": s["value"], "cores": 1, "kind": "reference", "sample": s["sample"]}
+            assert out["physical_cores"] >= out["threads"] or best_leg == "box_share", out
+            result["baseline"] = out
+        except Exception as e:  # reported, never silently replaced
+            result["baseline"] = {"error": repr(e)}
+    for name, tj in spec.get("traces", {}).items():
+        try:
+            A = problem(tj["nx"], tj["ny"], tj["nz"], tj["use_7pt"])
+            result["traces"][name] = _oracle_trace(oracle, A, threads, tj["iters"], tj["budget_s"])
+        except Exception as e:
+            result["traces"][name] = {"error": repr(e)}
+        log(f"cpu-child: trace {name} done")
+    with open(out_path, "w") as f:
+        json.dump(result, f)
+
+
+def run_cpu_child(spec, timeout_s):
+    """Rank 0: run cpu_child in a fresh process (a child, not an exec: this
+    process has initialised the GPU) and return its JSON, or {"error": ...}."""
+    import tempfile
+    with tempfile.TemporaryDirectory(prefix="hpccg_cpu_") as d:
+        sp, op = os.path.join(d, "spec.json"), os.path.join(d, "out.json")
+        with open(sp, "w") as f:
+            json.dump(spec, f)
+        env = {k: v for k, v in os.environ.items() if k not in ("OMP_PROC_BIND", "OMP_PLACES")}
+        t0 = time.time()
+        try:
+            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", sp, op],
+                               stdout=subprocess.DEVNULL, env=env, timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            return {"error": f"cpu child exceeded {timeout_s:.0f} s"}
+        if p.returncode != 0 or not os.path.exists(op):
+            return {"error": f"cpu child exited {p.returncode}"}
+        with open(op) as f:
+            out = json.load(f)
+        out["seconds"] = round(time.time() - t0, 1)
+        return out
 
 
 def pmc_traffic(tag, kernel, fused, xdefer, fupd, resident=0):
@@ -314,51 +488,6 @@ def opt_or_none(M, key):
         return None
 
 
-def cpu_baseline_global(nx, ny, nz_global, use_7pt, world, budget_s=15.0):
-    """N > 1: the reference (oracle/_ref, OpenMP, the box's thread share) on the
-    global z-stacked problem the N ranks solve together (the
-    200 x 200 x 1600 problem on the host cores), first iterations of one
-    HPCCG() solve. value is reported as global iterations/s x N: the unit of
-    the line's value (per-slab iterations summed over the N slabs)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ctypes
-    import oracle  # test infrastructure: baseline leg only
-    share = int(os.environ["OMP_NUM_THREADS"])
-    if not os.path.exists(oracle.REF_OMP_SO):
-        raise RuntimeError("oracle/_ref is not built (make -C oracle ref)")
-    t0 = time.time()
-    A = oracle.generate(nx, ny, nz_global, use_7pt=use_7pt)
-    gomp = ctypes.CDLL("libgomp.so.1")
-    gomp.omp_set_num_threads(share)
-    saved = os.dup(1)
-    null = os.open(os.devnull, os.O_WRONLY)
-    os.dup2(null, 1)
-    try:
-        M = oracle.ref_from_csr(A, omp=True)
-        b = A.b
-        del A  # the reference holds its own copy
-        setup_s = time.time() - t0
-        probe = 2
-        t = oracle.ref_hpccg(M, b, max_iter=probe + 1)["times"][0]
-        iters = int(max(2, min(500, budget_s / max(t / probe, 1e-6))))
-        res = oracle.ref_hpccg(M, b, max_iter=iters + 1)
-        M.close()
-    finally:
-        ctypes.CDLL(None).fflush(None)
-        os.dup2(saved, 1)
-        os.close(null)
-        os.close(saved)
-    its = res["niters"] / res["times"][0]
-    return {"value": its * world, "unit": "CG iterations/s (global-problem iterations x %d slabs)" % world,
-            "global_iterations_per_s": its, "cores": share, "threads": share, "kind": "reference",
-            "leg": "box_share", "physical_cores": physical_cores(), "host": host_cpu(),
-            "setup_s": round(setup_s, 1),
-            "sample": f"global {nx}x{ny}x{nz_global} {'7' if use_7pt else '27'}-pt (the {world} slabs together), "
-                      f"first {res['niters']} CG iterations of one reference HPCCG() solve "
-                      f"({res['times'][0]:.1f} s), OpenMP {share} threads "
-                      f"(OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, OMP_PLACES={os.environ.get('OMP_PLACES')})"}
-
-
 def measure(hp, torch, M, dev, max_iter, steps, warmup, event_steps, world, dist=None, stage=None):
     """Warmup, then `steps` timed solves bracketed by a barrier and a device
     sync on both sides; the first `event_steps` of them eager with hipEvents
@@ -436,7 +565,8 @@ def measure(hp, torch, M, dev, max_iter, steps, warmup, event_steps, world, dist
     return {"elapsed": elapsed, "local_elapsed": local_elapsed, "niters_total": niters_total, "it": it,
             "spmv_avg_s": spmv_avg_s, "timing_src": timing_src, "upd_ms": upd_ms, "upd_n": upd_n,
             "times_acc": times_acc, "step_s": step_s, "cold_s": cold_s, "graph_used": graph_used,
-            "chk": [chk[0].item(), chk[1].item()], "steps": steps, "event_steps": event_steps}
+            "chk": [chk[0].item(), chk[1].item()], "steps": steps, "event_steps": event_steps,
+            "trace": [float(v) for v in tr]}
 
 
 def roofline_of(M, n, stencil, spmv_avg_s):
@@ -557,30 +687,39 @@ def multirank_summary(ranks, bytes_per_launch):
             "allreduce_us_per_iteration_per_rank": [r["allreduce_us_per_iteration"] for r in ranks]}
 
 
-def secondary_config(hp, torch, n, stencil, dev, args):
-    """One other single-GPU config of BASELINE.json, measured like the headline."""
+def secondary_config(hp, torch, n, stencil, dev, args, world=1, dist=None, rank=0, comm="none", rt=None):
+    """One other config of BASELINE.json, measured like the headline (N > 1:
+    n^3 per GPU, z-stacked, every rank takes part)."""
     M = hp.Matrix.generate(n, n, n, use_7pt=stencil == 7)
     try:
-        meas = measure(hp, torch, M, dev, args.max_iter, args.secondary_steps, 2, 1, 1)
+        meas = measure(hp, torch, M, dev, args.max_iter, args.secondary_steps, 2, 1, world, dist)
         roof, kernel, kfmt, fused, fupd = roofline_of(M, n, stencil, meas["spmv_avg_s"])
-        value = meas["niters_total"] / meas["elapsed"]
-        return {"metric": f"CG iterations/sec + effective SpMV GB/s (% HBM peak), {stencil}-pt nx=ny=nz={n}",
-                "workload": f"HPCCG solve, {stencil}-pt {n}x{n}x{n}, max_iter={args.max_iter}, tolerance 0",
-                "value": round(value, 3), "unit": "CG iterations/s", "steps": meas["steps"],
-                "ms_per_step": round(meas["elapsed"] / meas["steps"] * 1e3, 3),
-                "avg_launch_us": roof["avg_launch_us"], "frac": roof["frac"],
-                "traffic_over_compulsory": roof["traffic_over_compulsory"], "roofline": roof,
-                "spmv_kernel": kernel, "graph_replay": bool(meas["graph_used"]),
-                "check": {"x_minus_xexact_inf": meas["chk"][0], "final_normr_over_initial": meas["chk"][1],
-                          "niters_per_solve": meas["it"]},
-                "cpu_baseline": None,
-                "cpu_note": "no CPU leg for secondary configs (the headline line carries the reference's)"}
+        ranks = gather_ranks(dist, world, rank_record(hp, M, rank, dev, comm, rt or {}, meas))
+        value = meas["niters_total"] / meas["elapsed"] * world
+        out = {"metric": f"CG iterations/sec + effective SpMV GB/s (% HBM peak), {stencil}-pt nx=ny=nz={n}",
+               "workload": f"HPCCG solve, {stencil}-pt {n}x{n}x{n}" + (" per GPU, z-stacked" if world > 1 else "") +
+                           f", max_iter={args.max_iter}, tolerance 0",
+               "value": round(value, 3),
+               "unit": "CG iterations/s" if world == 1 else
+                       "CG iterations/s (per-GPU %d^3 slab iterations, summed over GPUs)" % n,
+               "n_gpus": world, "scaling": "weak", "steps": meas["steps"],
+               "ms_per_step": round(meas["elapsed"] / meas["steps"] * 1e3, 3),
+               "avg_launch_us": roof["avg_launch_us"], "frac": roof["frac"],
+               "traffic_over_compulsory": roof["traffic_over_compulsory"], "roofline": roof,
+               "spmv_kernel": kernel, "graph_replay": bool(meas["graph_used"]),
+               "check": {"x_minus_xexact_inf": meas["chk"][0], "final_normr_over_initial": meas["chk"][1],
+                         "niters_per_solve": meas["it"]},
+               "cpu_baseline": None,
+               "cpu_note": "no CPU leg for secondary configs (the headline line carries the reference's)"}
+        if world > 1:
+            out["multirank"] = multirank_summary(ranks, roof["bytes_per_launch"])
+        return out, meas["trace"]
     finally:
         M.close()
 
 
 def build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt, ranks, cpu, secondary,
-               probe_report):
+               probe_report, trace_check=None):
     """The one JSON line (pure: the CPU suite checks its schema for N > 1)."""
     it_per_s = meas["niters_total"] / meas["elapsed"]  # per rank: every rank runs the same iterations
     value = it_per_s * world
@@ -646,6 +785,8 @@ def build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt
         "runtime": dict(rt, comm=comm, ranks=ranks),
         "cpu_baseline": cpu,
     }
+    if trace_check is not None:
+        out["check"]["trace_vs_oracle"] = trace_check
     if world > 1:
         out["multirank"] = multirank_summary(ranks, roof["bytes_per_launch"])
     if secondary is not None:
@@ -663,7 +804,12 @@ def main():
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="N = 1: skip the other single-GPU configs (27-pt 100^3, 7-pt 256^3)")
+                    help="skip the other configs (N = 1: 27-pt 100^3, 7-pt 256^3; N > 1: 27-pt 100^3 per GPU)")
+    ap.add_argument("--no-trace-check", action="store_true",
+                    help="skip check.trace_vs_oracle (the oracle's rtrans trace of the global problem)")
+    ap.add_argument("--trace-iters", type=int, default=40,
+                    help="CG iterations of the oracle's trace the GPU trace is checked against (fewer if the "
+                         "oracle's time budget is short)")
     ap.add_argument("--secondary-steps", type=int, default=10)
     ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "host"],
                     help="N > 1: rccl (one rank per GPU), host (hpccg_hip_comm_init_host: ranks may share a GPU); "
@@ -771,35 +917,77 @@ def main():
         rt["distinct_devices"] = 1
     M.close()
 
-    secondary = None
-    if world == 1 and not args.no_secondary:
+    secondary, sec_traces = None, {}
+    if not args.no_secondary:
         secondary = []
-        for n2, st2 in ((100, 27), (256, 7)):
+        # N = 1: BASELINE.json's other single-GPU configs; N > 1: north_star's
+        # second size, 100^3 per GPU, weak-scaled like the headline
+        for n2, st2 in (((100, 27), (256, 7)) if world == 1 else ((100, 27),)):
             if (n2, st2) == (n, args.stencil):
                 continue
             try:
-                secondary.append(secondary_config(hp, torch, n2, st2, dev, args))
-                stage("secondary", config=f"{st2}pt_{n2}", value=secondary[-1]["value"])
+                sec, tr2 = secondary_config(hp, torch, n2, st2, dev, args, world, dist, rank, comm, rt)
+                secondary.append(sec)
+                sec_traces[len(secondary) - 1] = (n2, st2, tr2)
+                stage("secondary", config=f"{st2}pt_{n2}", value=sec["value"])
             except Exception as e:  # reported, never silently dropped
                 secondary.append({"workload": f"{st2}-pt {n2}^3", "error": repr(e)})
 
+    exit_code = 0
     if rank == 0:
+        # rank 0's CPU work, after every GPU step, in a fresh child on the job's whole cpuset
+        spec = {"traces": {}}
+        if not args.no_cpu_baseline:
+            spec["baseline"] = {"nx": n, "ny": n, "nz": n * world, "use_7pt": use_7pt, "world": world,
+                                "budget_s": 15.0, "budget_1t_s": 10.0}
+        if not args.no_trace_check:
+            spec["traces"]["headline"] = {"nx": n, "ny": n, "nz": n * world, "use_7pt": use_7pt,
+                                          "iters": args.trace_iters, "budget_s": 20.0}
+            for i, (n2, st2, _) in sec_traces.items():
+                spec["traces"][f"secondary{i}"] = {"nx": n2, "ny": n2, "nz": n2 * world, "use_7pt": st2 == 7,
+                                                   "iters": args.trace_iters, "budget_s": 10.0}
+        child = run_cpu_child(spec, 900.0) if (spec.get("baseline") or spec["traces"]) else {}
+        stage("cpu_child", seconds=child.get("seconds"), error=child.get("error"))
         cpu = None
         if not args.no_cpu_baseline:
-            try:
-                cpu = cpu_baseline(n, n, n, use_7pt) if world == 1 else \
-                    cpu_baseline_global(n, n, n * world, use_7pt, world)
-            except Exception as e:  # reported, never silently replaced
-                cpu = {"error": repr(e)}
+            cpu = child.get("baseline") or {"error": child.get("error", "no baseline from the cpu child")}
+        rtol = RTRANS_RTOL_1GPU if world == 1 else RTRANS_RTOL_MULTI
+        ok_all = True
+
+        def trace_record(name, gpu_tr, nx, nz_g, st):
+            nonlocal ok_all
+            ct = (child.get("traces") or {}).get(name)
+            if ct is None or "error" in ct:
+                return {"ok": None, "error": (ct or {}).get("error", child.get("error", "not run"))}
+            rec = rtrans_check(gpu_tr, ct["trace"], rtol)
+            rec.update({"oracle": f"oracle/hpccg_oracle.c HPCCG() on the global {nx}x{nx}x{nz_g} {st}-pt problem, "
+                                  f"OpenMP {ct['threads']} threads, first {ct['iterations']} iterations "
+                                  f"({ct['seconds']} s)",
+                        "gpu": "rank 0's rtrans trace of the last timed solve (global, after the all-reduce)"})
+            ok_all = ok_all and rec["ok"]
+            return rec
+
+        tchk = trace_record("headline", meas["trace"], n, n * world, args.stencil) if not args.no_trace_check \
+            else None
+        for i, (n2, st2, tr2) in sec_traces.items():
+            if not args.no_trace_check:
+                secondary[i]["check"]["trace_vs_oracle"] = trace_record(f"secondary{i}", tr2, n2, n2 * world, st2)
         out = build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt, ranks, cpu, secondary,
-                         placement_report(args.placement, probe_us, pick))
+                         placement_report(args.placement, probe_us, pick), tchk)
+        if not ok_all:
+            log("bench: the GPU trace does not match the oracle's within the stated tolerance; exiting 3")
+            exit_code = 3
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()  # rank 0's CPU leg runs while the others wait here
         hp.comm_destroy()
         dist.destroy_process_group()
     stage.done.set()
+    return exit_code
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 4 and sys.argv[1] == "--cpu-child":
+        cpu_child(sys.argv[2], sys.argv[3])
+        sys.exit(0)
+    sys.exit(main())

@@ -59,8 +59,12 @@ def _worker(rank, world, port, q):
                    "kind": "reference", "sample": "synthetic"}
             opts = dict(transport, device_bytes=4.2e9, fuse_p=1, fold=1, x_defer=2, x_ring=32, rev_update=1,
                         overlap=0, graph_chunk=32, nt=1, a2_ring=3, nt_store=0)
-            line = bench.build_line(A, world, n, full, roof, 2, 3, 1, info, opts, dict(rt), ranks, cpu, None,
-                                    {"ran": False})
+            tchk = bench.rtrans_check([1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125], [1.0, 0.5, 0.25, 0.125, 0.0625,
+                                                                                   0.03125], bench.RTRANS_RTOL_MULTI)
+            sec = [{"workload": "HPCCG solve, 27-pt 100x100x100 per GPU, z-stacked", "value": 44000.0,
+                    "n_gpus": world, "check": {"trace_vs_oracle": tchk}}]
+            line = bench.build_line(A, world, n, full, roof, 2, 3, 1, info, opts, dict(rt), ranks, cpu, sec,
+                                    {"ran": False}, tchk)
             q.put(json.dumps(line))
         else:
             q.put(None)
@@ -106,6 +110,12 @@ def test_bench_multirank_line_schema():
     assert mr["frac_max_over_ranks"] == pytest.approx(2.05e9 / 350e-6 / 1e9 / 8000.0, rel=1e-3)
     assert mr["transport_used"].startswith("in-kernel")
     assert len(mr["verdicts_per_rank"]) == 2
+    # the N > 1 line checks itself against the oracle and
+    # carries north_star's second size (100^3 per GPU)
+    tv = d["check"]["trace_vs_oracle"]
+    assert tv["ok"] is True and tv["checked"] == 6 and tv["rtol"] == 1e-7
+    assert d["secondary"][0]["workload"].startswith("HPCCG solve, 27-pt 100x100x100 per GPU")
+    assert d["secondary"][0]["check"]["trace_vs_oracle"]["ok"] is True
 
 
 class _FakeInfoM(_FakeM):
@@ -138,3 +148,71 @@ def test_roofline_bytes_per_launch_by_resident_mode(ru, kname):
     assert roof["bytes_per_launch"] == pytest.approx(expect)
     assert roof["frac"] == pytest.approx(expect / 45e-6 / 1e9 / bench.HBM_PEAK_GBS, rel=1e-3)
     assert ("launch_note" in roof) == (ru >= 6)
+
+
+def test_rtrans_check():
+    """bench.rtrans_check is conftest.check_trace as a record: points above the
+    1e-20 cutoff compared on normr^2 at rtol; a miss or too few points fails."""
+    sys.path.insert(0, ROOT)
+    import bench
+    ref = [10.0 ** (-k) for k in range(14)]  # normr; rtrans falls below 1e-20 r0^2 at k = 11
+    r = bench.rtrans_check(ref, ref, 1e-7)
+    assert r["ok"] and r["checked"] == 11 and r["max_rel"] == 0.0
+    bad = list(ref)
+    bad[7] *= 1.0 + 1e-7  # rtrans off by 2e-7
+    r = bench.rtrans_check(bad, ref, 1e-7)
+    assert not r["ok"] and r["first_failing_k"] == 7 and r["max_rel"] == pytest.approx(2e-7, rel=1e-3)
+    assert bench.rtrans_check(bad, ref, 1e-6)["ok"]
+    assert not bench.rtrans_check(ref[:3], ref, 1e-7)["ok"]  # fewer than TRACE_MIN_POINTS
+    assert not bench.rtrans_check([], ref, 1e-7)["ok"]
+
+
+def test_cpulist_and_no_omp_binding_exported():
+    """The job's cpuset parser, and importing bench exports no
+    OpenMP binding: a torch.distributed.run started from it would otherwise
+    bind every rank to one core."""
+    sys.path.insert(0, ROOT)
+    env_before = {k: os.environ.get(k) for k in ("OMP_PROC_BIND", "OMP_PLACES")}
+    import bench
+    assert {k: os.environ.get(k) for k in env_before} == env_before
+    assert bench.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    cpus, src = bench.job_cpuset()
+    assert cpus and src
+
+
+def test_cpu_child_global_problem_and_trace(tmp_path):
+    """rank 0's CPU work in a fresh process (bench.py --cpu-child): the mask is
+    the job's whole cpuset, threads never exceed its physical cores, the
+    reference leg runs on the GLOBAL z-stacked problem of 2 slabs, and the
+    OpenMP oracle trace it returns matches the serial oracle's at the multi-
+    rank tolerance -- the trace rank 0 checks its GPU trace against."""
+    import subprocess
+    sys.path.insert(0, ROOT)
+    import bench
+    import oracle
+    spec = {"baseline": {"nx": 16, "ny": 16, "nz": 32, "use_7pt": False, "world": 2, "budget_s": 0.5,
+                         "budget_1t_s": 0.5},
+            "traces": {"headline": {"nx": 16, "ny": 16, "nz": 32, "use_7pt": False, "iters": 30, "budget_s": 5.0},
+                       "secondary0": {"nx": 12, "ny": 12, "nz": 24, "use_7pt": True, "iters": 30, "budget_s": 5.0}}}
+    sp, op = tmp_path / "spec.json", tmp_path / "out.json"
+    sp.write_text(json.dumps(spec))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("OMP_")}
+    subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-child", str(sp), str(op)], check=True,
+                   env=env, stdout=subprocess.DEVNULL, timeout=240)
+    out = json.loads(op.read_text())
+    m = out["mask"]
+    cpus, _ = bench.job_cpuset()
+    assert m["cpus"] == len(cpus & set(range(os.cpu_count())))
+    assert 1 <= m["threads"] <= m["physical_cores"]
+    base = out["baseline"]
+    assert "error" not in base, base
+    if oracle.ref_available():
+        assert base["kind"] == "reference" and base["leg"] == "host" and base["cores"] == m["threads"]
+        assert base["sample"].startswith("global 16x16x32 (the 2 slabs together)")
+        assert base["value"] == pytest.approx(2 * base["global_iterations_per_s"])
+    for name, (nx, nz, s7) in {"headline": (16, 32, False), "secondary0": (12, 24, True)}.items():
+        tr = out["traces"][name]
+        assert tr["iterations"] == 30 and len(tr["trace"]) == 31
+        serial = oracle.hpccg(oracle.generate(nx, nx, nz, use_7pt=s7), max_iter=31)["trace"]
+        chk = bench.rtrans_check(tr["trace"], serial, bench.RTRANS_RTOL_MULTI)
+        assert chk["ok"], chk

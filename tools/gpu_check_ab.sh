@@ -18,7 +18,7 @@ for cfg in "--n 200" "--n 100" "--n 256 --stencil 7"; do
   for rep in $(seq ${REPS:-3}); do
     for which in new base; do
       if [ $which = base ]; then export HPCCG_HIP_LIB=$PWD/lib_base/libhpccg_hip.so; else unset HPCCG_HIP_LIB; fi
-      timeout -k 10 200 python bench.py $cfg --no-cpu-baseline --steps ${STEPS:-10} > gpurun_out/chk/one.json \
+      timeout -k 10 200 python bench.py $cfg --no-cpu-baseline --no-trace-check --steps ${STEPS:-10} > gpurun_out/chk/one.json \
           2>> gpurun_out/chk/err.log || { tail -20 gpurun_out/chk/err.log; exit 1; }
       python3 -c "
 import json; d = json.load(open('gpurun_out/chk/one.json'))
