@@ -451,8 +451,7 @@ class Stages:
         import threading
         self.rank, self.t0, self.stage = rank, time.time(), "start"
         self.done = threading.Event()
-        if limit_s > 0:
-            threading.Thread(target=self._watch, args=(limit_s,), daemon=True).start()
+        threading.Thread(target=self._watch, args=(limit_s if limit_s > 0 else float("inf"),), daemon=True).start()
 
     def __call__(self, stage, **kv):
         self.stage = stage
@@ -460,9 +459,15 @@ class Stages:
         log(f"[rank {self.rank}] +{time.time() - self.t0:7.2f}s {stage} {extra}".rstrip())
 
     def _watch(self, limit_s):
-        if not self.done.wait(limit_s):
-            log(f"[rank {self.rank}] watchdog: still in stage '{self.stage}' after {limit_s:.0f} s; exiting 124")
-            os._exit(124)
+        # a heartbeat every 30 s (a long stage -- 8 ranks sharing one GPU, the
+        # CPU child on a global problem -- must not look hung), then the limit
+        t_end = self.t0 + limit_s
+        while not self.done.wait(min(30.0, max(0.0, t_end - time.time()))):
+            if time.time() >= t_end:
+                log(f"[rank {self.rank}] watchdog: still in stage '{self.stage}' after {limit_s:.0f} s; exiting 124")
+                os._exit(124)
+            if self.rank == 0:
+                log(f"[rank {self.rank}] +{time.time() - self.t0:7.2f}s ... in stage '{self.stage}'")
 
 
 def init_gloo(dist, rank, world):
@@ -754,9 +759,9 @@ def build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt
             "device_bytes_per_gpu": M_opts.get("device_bytes"),
             "graph_replay": bool(meas["graph_used"]),
             "placement_probe": probe_report,
-            "options": {k: M_opts.get(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update", "overlap",
-                                                   "graph_chunk", "nt", "a2_ring", "nt_store", "fuse_update", "rhalo",
-                                                   "peer_allreduce", "halo_pull", "resident_update")},
+            "options": {k: M_opts.get(k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "graph_chunk", "nt", "a2_ring",
+                                                   "nt_store", "fuse_update", "rhalo", "peer_allreduce", "halo_pull",
+                                                   "resident_update")},
         },
         "cg_iterations_per_s_global": round(it_per_s, 3),
         "spmv_effective_gbs": roof["achieved"],
@@ -807,7 +812,7 @@ def main():
                     help="skip the other configs (N = 1: 27-pt 100^3, 7-pt 256^3; N > 1: 27-pt 100^3 per GPU)")
     ap.add_argument("--no-trace-check", action="store_true",
                     help="skip check.trace_vs_oracle (the oracle's rtrans trace of the global problem)")
-    ap.add_argument("--trace-iters", type=int, default=40,
+    ap.add_argument("--trace-iters", type=int, default=60,
                     help="CG iterations of the oracle's trace the GPU trace is checked against (fewer if the "
                          "oracle's time budget is short)")
     ap.add_argument("--secondary-steps", type=int, default=10)
@@ -816,13 +821,10 @@ def main():
                          "auto = rccl when there are at least N GPUs")
     ap.add_argument("--kernel", type=int, default=-1, help="SpMV kernel: 0 SELL-512, 1 A direct, 2 A pairs")
     ap.add_argument("--fuse-p", type=int, default=-1, help="p update inside the SpMV (-1 auto, 0 off)")
-    ap.add_argument("--fold", type=int, default=-1, help="dot completion in the producer (-1 auto, 0..3)")
+    ap.add_argument("--fold", type=int, default=-1, help="dot completion in the producer (-1 auto, 0 k_finalize)")
     ap.add_argument("--graph-chunk", type=int, default=-1, help="CG iterations per hipGraph (-1 default)")
     ap.add_argument("--x-defer", type=int, default=-1, help="batched x update (-1 default)")
     ap.add_argument("--x-ring", type=int, default=-1, help="x-update deferral depth = p ring length")
-    ap.add_argument("--rev-update", type=int, default=-1, help="update kernel walks slices backwards")
-    ap.add_argument("--overlap", type=int, default=-1, help="multi-rank: halo beside the interior SpMV")
-    ap.add_argument("--a-pre", type=int, default=-1, help="direct kernel: value slots loaded before the test")
     ap.add_argument("--use-graph", type=int, default=-1, help="hipGraph replay (-1 default on)")
     ap.add_argument("--placement", type=int, default=0,
                     help="placement probe candidates at creation (default 0: off; -1 auto: 6 for images > 512 MB). "
@@ -888,7 +890,6 @@ def main():
         probe_us, pick = [], 0
     for opt, val in (("spmv_kernel", args.kernel), ("fuse_p", args.fuse_p), ("fold", args.fold),
                      ("graph_chunk", args.graph_chunk), ("x_defer", args.x_defer), ("x_ring", args.x_ring),
-                     ("rev_update", args.rev_update), ("overlap", args.overlap), ("a_pre", args.a_pre),
                      ("use_graph", args.use_graph)):
         if val != -1:
             M.set_option(opt, val)
@@ -902,9 +903,9 @@ def main():
     meas = measure(hp, torch, M, dev, args.max_iter, args.steps, args.warmup, args.event_steps, world, dist, stage)
     stage("timed", steps=args.steps, seconds=f"{meas['elapsed']:.3f}")
     roof, kernel, kfmt, fused, fupd = roofline_of(M, n, args.stencil, meas["spmv_avg_s"])
-    M_opts = {k: opt_or_none(M, k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "rev_update", "overlap",
-                                             "graph_chunk", "nt", "a2_ring", "nt_store", "fuse_update", "rhalo",
-                                             "peer_allreduce", "halo_pull", "device_bytes", "resident_update")}
+    M_opts = {k: opt_or_none(M, k) for k in ("fuse_p", "fold", "x_defer", "x_ring", "graph_chunk", "nt", "a2_ring",
+                                             "nt_store", "fuse_update", "rhalo", "peer_allreduce", "halo_pull",
+                                             "device_bytes", "resident_update")}
     ranks = gather_ranks(dist, world, rank_record(hp, M, rank, dev, comm, rt, meas))
     if world > 1:
         rt["pci_bus_ids"] = [r["pci_bus_id"] for r in ranks]
@@ -926,6 +927,7 @@ def main():
             if (n2, st2) == (n, args.stencil):
                 continue
             try:
+                stage("secondary_run", config=f"{st2}pt_{n2}")
                 sec, tr2 = secondary_config(hp, torch, n2, st2, dev, args, world, dist, rank, comm, rt)
                 secondary.append(sec)
                 sec_traces[len(secondary) - 1] = (n2, st2, tr2)
@@ -946,6 +948,7 @@ def main():
             for i, (n2, st2, _) in sec_traces.items():
                 spec["traces"][f"secondary{i}"] = {"nx": n2, "ny": n2, "nz": n2 * world, "use_7pt": st2 == 7,
                                                    "iters": args.trace_iters, "budget_s": 10.0}
+        stage("cpu_child_run", baseline=bool(spec.get("baseline")), traces=len(spec["traces"]))
         child = run_cpu_child(spec, 900.0) if (spec.get("baseline") or spec["traces"]) else {}
         stage("cpu_child", seconds=child.get("seconds"), error=child.get("error"))
         cpu = None

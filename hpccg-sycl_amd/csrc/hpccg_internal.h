@@ -76,11 +76,9 @@ struct CgArgs {
     int sgrid;             // SpMV launch grid (sn0 + sn1 rounded up to a multiple of kNumXcd)
     int nt;                // non-temporal matrix loads (image beyond the Infinity Cache)
     int a_width;           // SELL-512-A uniform slot count (27, 7, ...), 0 = per-slice widths
-    int apre;              // direct kernel: value slots loaded before the iteration test (-1 auto)
     double* ahist;         // [max_iter + 1]: alpha_k (for the deferred x update)
     int fuse_p;            // 1: p = r + beta p computed inside the SpMV
     int fold;              // dots completed in the producing kernel: 0 none, 1 both, 2 p.Ap only, 3 r.r only
-    unsigned int* tickets; // [2 x (ngroups + 1)] arrival counters (fold): groups, top
     double* Ap;
     double* partial;       // [2 x nslices] slice partials (p.Ap, r.r), then 2 x ngroups group sums
     double* g;             // [2] dot results after the all-reduce
@@ -100,23 +98,19 @@ struct CgArgs {
     const int* awin2;             // per pair, kAWin windows (first row - pair row, length, LDS base)
     const int* awn2;              // windows per pair
     const int* adiag2;            // per slice: LDS position of offset 0 (minus the pair row), -1 none
-    int lds_ep;                   // pair kernel: the rows' own p_k from the staged window
-    int stage16;                  // pair kernel: stage row pairs with 16-B loads / LDS stores
     const unsigned char* atri;    // direct kernel: per slice, 1 = offsets in the width's triple plan (null: off)
     int alds2_doubles;            // dynamic LDS per two-slice block
     int nt_store;                 // CG vector stores non-temporal
-    int slots;                    // folded dots complete through self-validating slots (launch covers all units)
     int a2_ring;                  // pair kernel: value slots in flight per wave through its LDS-DMA ring (0: register loads)
     int xside;                    // x_defer 2: this SpMV launch carries the side-flush blocks
     int fupd;                     // fused update: the SpMV launch's trailing blocks run the update (one rank,
                                   // direct kernel); k lives in kst[0] / kst[2] by parity (kpar)
     int kpar;                     // fused update: parity of the iteration this launch runs
-    int fu2;                      // fused update: two slices per update block (four rows per thread)
-    int resident;                 // fused update run by the resident pair kernel (k_spmv_ar, option resident_update)
+    int resident;                 // resident pair kernels: 1 k_spmv_ar, kResidentAuto k_cg_persist (option resident_update)
     int dbg_resident_stall;       // debug (retry test): k_spmv_ar's p.Ap wait never sees the total (it expires)
     int ubase;                    // fused update: first update block of the SpMV launch (set at launch)
     double* pready;               // fused update: self-validating slots of the p.Ap total (kNumXcd, kReadyStride apart)
-    double* pslots;               // persistent CG (resident >= 6): per iteration pslot_stride slots, emptied before the launch
+    double* pslots;               // persistent CG (resident == kResidentAuto): per iteration pslot_stride slots, emptied first
     long long pslot_stride;
     int pk0, pk1;                 // persistent CG: the launch runs iterations [pk0, pk1) (its window)
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
@@ -238,7 +232,6 @@ constexpr int kXRingMax = 64;
 // ---- launches (hpccg_kernels.hip) -----------------------------------------
 void launch_cg_prologue_copy(const CgArgs& a, hipStream_t s);   // p = x
 void launch_cg_p_update(const CgArgs& a, hipStream_t s);        // p = r + beta p
-void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s);  // same, halo rows only
 // gather plan: buf[i] = p_k[idx[i]] (computed when fused; prologue: p = x)
 void launch_cg_pack(const CgArgs& a, const int* idx, int cnt, double* buf, bool prologue, hipStream_t s);
 bool spmv_kernel_ok(int kernel);
@@ -278,8 +271,8 @@ void launch_pull(const CgArgs& a, const double* lo_src, double* lo_dst, int lo_c
 // the prologue's barrier (one lane, peer_allreduce on the kMboxBarrier slots):
 // every rank's p = x (and its x) is in place before any rank pulls x's rows
 void launch_peer_barrier(const CgArgs& a, hipStream_t s);
-// solve start: state zeroed (spin budget set), every dot slot empty, tickets zero
-void launch_rearm(int* kst, double* partial, int np, unsigned int* tickets, int nt, int budget, hipStream_t s);
+// solve start: state zeroed (spin budget set), every dot slot empty
+void launch_rearm(int* kst, double* partial, int np, int budget, hipStream_t s);
 void launch_cg_xflush(const CgArgs& a, hipStream_t s);  // pending deferred x updates
 
 // In-process rank group all-reduce of one CG scalar: g[which] of every rank =

@@ -280,27 +280,21 @@ __device__ __forceinline__ double* cur_p(const CgArgs& a, int k)
 // which = kPAP: p.Ap (HPCCG.cpp:381); kRR: r.r (HPCCG.cpp:353, 367), which
 // closes iteration k and advances kst[0].
 //
-// Folded (fold_of): completed inside the producing kernel, two ways.
-//  * Slots (a.slots, every launch that covers all units): every partial and
-//    group-sum slot holds kSlotEmpty (a NaN payload no arithmetic produces)
-//    until its value is stored. Producers store their partial with an
-//    agent-scope (sc1) store and leave -- no drain, no atomic. The group's
-//    member with the largest block index, i.e. the one dispatched last
-//    (group_last_unit), waits for the group's slots to fill, sums them, resets
-//    them to empty and stores the group sum; the group whose last member has
-//    the largest block index of all (top_group) then waits for every group
-//    sum and forms the total. A waiter only waits for blocks dispatched before
-//    it (dispatch is in block order on every XCD), so the wait always ends.
-//  * Tickets (launches over a unit subset: the eager halo overlap): every
-//    block publishes its partial (sc1), drains (s_waitcnt vmcnt(0)) and takes
-//    a relaxed agent-scope ticket on its group; the group's last arriver sums
-//    the group, tickets the top counter, whose last arriver forms the total
-//    (MI355X_MICROARCH.md, inter-workgroup visibility). It resets the slots it
-//    read as well, so the two ways mix freely.
+// Folded (fold_of): completed inside the producing kernel through
+// self-validating slots. Every partial and group-sum slot holds kSlotEmpty (a
+// NaN payload no arithmetic produces) until its value is stored. Producers
+// store their partial with an agent-scope (sc1) store and leave -- no drain,
+// no atomic. The group's member with the largest block index, i.e. the one
+// dispatched last (group_last_unit), waits for the group's slots to fill, sums
+// them, resets them to empty and stores the group sum; the group whose last
+// member has the largest block index of all (top_group) then waits for every
+// group sum and forms the total. A waiter only waits for blocks dispatched
+// before it (dispatch is in block order on every XCD), so the wait always ends.
 // Otherwise k_finalize computes the same two levels in a separate launch (and
 // resets the slots). Same shape every way: bitwise the same total.
-// 100^3 same-process A/B: the ticket's round trip made every block of the
-// short update kernel wait (update 10.3 -> 23.6 us with r.r folded by tickets).
+// (An arrival-ticket completion -- atomics, a drain per block -- lost: the
+// ticket's round trip made every block of the short 100^3 update kernel wait,
+// 10.3 -> 23.6 us; it served only the dropped eager halo overlap and is gone.)
 // ---------------------------------------------------------------------------
 constexpr int kGroup = 64;
 constexpr int kTopThreads = 256;
@@ -583,7 +577,7 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
     double* const gp = group_slots(a, which, ng);
     const int g = s0 / kGroup;
     const int i = g * kGroup + lane;  // the group's slot of this lane
-    if (a.slots) {
+    {
         // (a.dbg_withhold: the guard test's missing partial)
         if (lane < cnt && !(which == kPAP && s0 + lane == a.dbg_withhold - 1)) st_sc1(sp + s0 + lane, bs);
         if (u != group_last_unit(m, g)) return;
@@ -629,46 +623,6 @@ __device__ __forceinline__ void complete_dot_lanes(const CgArgs& a, const UnitMa
                                              : top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
         for (int j = lane; j < ng; j += kWave) st_sc1(gp + j, slot_empty());
         if (lane == 0) finish_dot(a, tot, which, k);
-        return;
-    }
-    unsigned* gt = a.tickets + which * (ng + 1);  // group tickets, then the top one
-    int role = 0;
-    if (lane < cnt) st_sc1(sp + s0 + lane, bs);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        const unsigned glen = (unsigned)min(kGroup, a.nslices - g * kGroup);
-        const unsigned t = __hip_atomic_fetch_add(gt + g, (unsigned)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        role = (t + (unsigned)cnt == glen) ? 1 : 0;
-        if (role) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    role = __shfl(role, 0, kWave);
-    if (role == 0) return;
-    // group reducer (this wave): sc1 loads of the group's partials
-    const double v = wave_sum(i < a.nslices ? ld_sc1(sp + i) : 0.0);
-    if (i < a.nslices) st_sc1(sp + i, slot_empty());
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the empties land before the publish
-    if (lane == 0) {
-        st_sc1(gp + g, v);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(gt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-        const unsigned t = __hip_atomic_fetch_add(gt + ng, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        role = (t == (unsigned)ng - 1u) ? 2 : 0;
-        if (role == 2) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    role = __shfl(role, 0, kWave);
-    if (role != 2) return;
-    const double tot = top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
-    for (int j = lane; j < ng; j += kWave) st_sc1(gp + j, slot_empty());
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        finish_dot(a, tot, which, k);
-        __hip_atomic_store(gt + ng, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
     }
 }
 
@@ -828,25 +782,6 @@ __global__ __launch_bounds__(kBlock) void k_p_update(CgArgs a)
 #pragma unroll
     for (int i = 0; i < kRpt; i++) o.v[i] = rv.v[i] + beta * yv.v[i];
     st_rows(cur_p(a, k), row, a.n, o);
-}
-
-// Multi-rank with the p update fused into the SpMV: the rows the neighbours
-// need (the first nlo and last nhi local rows) are updated first, by this
-// kernel, so the halo can move p_k before the SpMV computes the rest. Same
-// expression as k_p_update; the SpMV later stores the same bits there again.
-__global__ __launch_bounds__(256) void k_p_boundary(CgArgs a, int nlo, int nhi)
-{
-    const int k = a.kst[0];
-    const double rr = a.g[kRR];
-    if (!cg_run(a, k, true, rr)) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) stamp(a, k, kStampHalo);  // halo class from here
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= nlo + nhi) return;
-    const int row = i < nlo ? i : a.n - nhi + (i - nlo);
-    const double beta = (k == 1) ? 0.0 : rr / a.hist[k - 2];
-    const double rv = a.r[row];
-    const double yv = (k == 1) ? rv : cur_p(a, k - 1)[row];
-    cur_p(a, k)[row] = rv + beta * yv;
 }
 
 // Gather halo plan: pack p_k at the rows the requesting ranks need
@@ -1120,7 +1055,7 @@ __device__ __forceinline__ bool fused_update(const CgArgs& a, bool prologue, uns
     if ((int)blockIdx.x < a.ubase || (int)blockIdx.x >= a.gbase) return false;
     if (prologue) return true;
     const int bl = (int)blockIdx.x - a.ubase;  // a.ubase is a multiple of kNumXcd
-    const int spu = a.fu2 ? 2 : 1;
+    constexpr int spu = 2;  // two slices per update block (one measured slower: DESIGN.md 4)
     const int units = (a.nslices + spu - 1) / spu;
     const int ugrid = (units + kNumXcd - 1) / kNumXcd * kNumXcd;
     const int per = ugrid / kNumXcd;
@@ -1746,7 +1681,7 @@ __device__ __forceinline__ bool pers_wait(const CgArgs& a, int k, int which, dou
     return true;
 }
 
-template <bool kNT, int kPre = 2, int kStep = 1, int kL = 0>
+template <bool kNT, int kPre = 3, int kStep = 2, int kL = 3>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cg_persist(CgArgs a)
 {
     constexpr int kW = 27;
@@ -2029,50 +1964,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 // ---------------------------------------------------------------------------
 // The pair's windows into LDS (xs): fused, p_k = r + beta*p_{k-1} per staged
 // row (ghost rows of a multi-rank slab: r's received planes and p_{k-1}'s
-// stored ghosts, ghost_store); guard rows are zeros. stage16: row pairs (the windows' first row, length and LDS base are
-// even, pair_windows) with 16-B loads and LDS stores.
-template <bool kFuse>
-__device__ __forceinline__ void stage_pair_windows(const CgArgs& a, const IterState& st, int P, const double* __restrict__ p,
-                                                   const double* __restrict__ pold, double* __restrict__ xs)
-{
-    const int prow0 = 2 * P * kSliceRows;  // first row of the pair
-    const int nw = a.awn2[P];
-    const int* __restrict__ win = a.awin2 + (size_t)P * kAWin * 3;
-    for (int w = 0; w < nw; w++) {
-        const int st0 = prow0 + win[3 * w], len = win[3 * w + 1], base = win[3 * w + 2];
-        if (a.stage16) {
-            for (int i = 2 * threadIdx.x; i < len; i += 4 * kBlock) {
-                const int l = st0 + i;  // local rows l, l + 1 (< 0 / >= n: ghosts, guard or padding zeros)
-                d2v v;
-                if constexpr (kFuse) {  // ghost rows too: r's received planes, p_{k-1}'s stored ghosts (rhalo)
-                    const d2v rv = *reinterpret_cast<const d2v*>(a.r + l);
-                    const d2v yv = *reinterpret_cast<const d2v*>(pold + l);
-                    v.x = rv.x + st.beta * yv.x;
-                    v.y = rv.y + st.beta * yv.y;
-                } else {
-                    v = *reinterpret_cast<const d2v*>(p + l);
-                }
-                *reinterpret_cast<d2v*>(xs + base + i) = v;
-            }
-        } else {
-            for (int i = threadIdx.x; i < len; i += 2 * kBlock) {
-                const int l = st0 + i;  // local row (< 0 / >= n: ghosts, guard or padding zeros)
-                if constexpr (kFuse)
-                    xs[base + i] = a.r[l] + st.beta * pold[l];
-                else
-                    xs[base + i] = p[l];
-            }
-        }
-    }
-}
-
-// stage_pair_windows with every load of a round issued before its LDS
-// stores: the pair's windows are one LDS range [0, tot) (pair_windows lays
-// them out back to back, even bases and lengths), each thread stages the row
-// pairs e = 2 t + 1024 u of it, kU per round. Same values as
-// stage_pair_windows (stage16).
+// stored ghosts, ghost_store); guard rows are zeros. Every load of a round is
+// issued before its LDS stores: the pair's windows are one LDS range [0, tot)
+// (pair_windows lays them out back to back, even bases and lengths), each
+// thread stages the row pairs e = 2 t + 1024 u of it, kU per round (16-B
+// loads and LDS stores; one row at a time measured slower).
 template <bool kFuse, int kU = 5>
-__device__ __forceinline__ void stage_pair_windows_batched(const CgArgs& a, const IterState& st, int P,
+__device__ __forceinline__ void stage_pair_windows(const CgArgs& a, const IterState& st, int P,
                                                            const double* __restrict__ p, const double* __restrict__ pold,
                                                            double* __restrict__ xs)
 {
@@ -2120,7 +2018,7 @@ __device__ __forceinline__ void stage_pair_windows_batched(const CgArgs& a, cons
     }
 }
 
-// The pair kernel's epilogue: Ap, p_k (from the window when lds_ep), the two
+// The pair kernel's epilogue: Ap, p_k (from the window), the two
 // slices' p.Ap partials with block_sum<256>'s shape, completed (fold) or stored.
 template <bool kFuse>
 __device__ __forceinline__ void pair_epilogue(const CgArgs& a, const IterState& st, bool prologue, int P, int s, bool have,
@@ -2131,7 +2029,7 @@ __device__ __forceinline__ void pair_epilogue(const CgArgs& a, const IterState& 
     if (have) {
         const int prow = (threadIdx.x / kBlock) * kSliceRows + lrow;  // row within the pair
         const int pd = a.adiag2 ? a.adiag2[s] : -1;  // LDS position of the slice's offset 0
-        if (pd >= 0 && a.lds_ep) {
+        if (pd >= 0) {
             const Rows pk{{xs[prow + pd], xs[prow + pd + 1]}};
             d = spmv_rows_out<kFuse>(a, st, prologue, s * kSliceRows + lrow, sum, &pk);
         } else {
@@ -2295,10 +2193,7 @@ __global__ __launch_bounds__(2 * kBlock) void k_spmv_a2r(CgArgs a, bool prologue
     const double* __restrict__ p = cur_p(a, st.k);
     const double* __restrict__ pold = a.r;
     if constexpr (kFuse) pold = (st.k == 1) ? a.r : cur_p(a, st.k - 1);
-    if (a.stage16)
-        stage_pair_windows_batched<kFuse>(a, st, P, p, pold, xs);
-    else
-        stage_pair_windows<kFuse>(a, st, P, p, pold, xs);
+    stage_pair_windows<kFuse>(a, st, P, p, pold, xs);
     // raw barrier: __syncthreads() would drain the ring (vmcnt(0))
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -2660,16 +2555,14 @@ __global__ void k_peer_selftest(CgArgs a, int rounds, double* out)
 // Every solve starts here, stream-ordered before its prologue (HPCCG.cpp:
 // 342-356 starts from r = b - A x with nothing carried over): the iteration
 // state and error record zeroed with the spin budget set, every dot slot --
-// slice partials, group sums, the fused update's p.Ap ready slots -- empty,
-// the arrival tickets zero. No solve then depends on what an earlier solve,
-// an aborted one or the placement probe's timed solves left in them.
-__global__ __launch_bounds__(256) void k_rearm(int* kst, double* partial, int np, unsigned int* tickets, int nt,
-                                               int budget)
+// slice partials, group sums, the fused update's p.Ap ready slots -- empty.
+// No solve then depends on what an earlier solve, an aborted one or the
+// placement probe's timed solves left in them.
+__global__ __launch_bounds__(256) void k_rearm(int* kst, double* partial, int np, int budget)
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < 2 * kKstDoubles) kst[i] = i == kErrBase + kErrBudget ? budget : 0;
     if (i < np) partial[i] = slot_empty();
-    if (i < nt) tickets[i] = 0u;
 }
 
 // After the loop: x += alpha_j p_j for the iterations since the last batched
@@ -2921,11 +2814,6 @@ void launch_cg_p_update(const CgArgs& a, hipStream_t s)
     hipLaunchKernelGGL(k_p_update, dim3(a.grid), dim3(kBlock), 0, s, a);
 }
 
-void launch_cg_p_boundary(const CgArgs& a, int nlo, int nhi, hipStream_t s)
-{
-    if (nlo + nhi <= 0) return;
-    hipLaunchKernelGGL(k_p_boundary, dim3((nlo + nhi + 255) / 256), dim3(256), 0, s, a, nlo, nhi);
-}
 
 void launch_cg_pack(const CgArgs& a, const int* idx, int cnt, double* buf, bool prologue, hipStream_t s)
 {
@@ -2951,8 +2839,7 @@ int a2_ring_prepare()
         e = hipFuncSetAttribute((const void*)k_spmv_a2r<true, W, R>, hipFuncAttributeMaxDynamicSharedMemorySize, lim); \
     if (e == hipSuccess)                                                                                                \
         e = hipFuncSetAttribute((const void*)k_spmv_a2r<false, W, R>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    HPCCG_A2R_ATTR(27, 1) HPCCG_A2R_ATTR(27, 2) HPCCG_A2R_ATTR(27, 3) HPCCG_A2R_ATTR(27, 4)
-    HPCCG_A2R_ATTR(7, 1) HPCCG_A2R_ATTR(7, 2) HPCCG_A2R_ATTR(7, 3) HPCCG_A2R_ATTR(7, 4)
+    HPCCG_A2R_ATTR(27, kA2RingDefault) HPCCG_A2R_ATTR(7, kA2RingDefault)
 #undef HPCCG_A2R_ATTR
     if (e == hipSuccess)  // the timeline diagnostic's instantiation
         e = hipFuncSetAttribute((const void*)k_spmv_a2r<true, 27, 3, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2995,37 +2882,24 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         b.sgrid = (pairs + kNumXcd - 1) / kNumXcd * kNumXcd;
         b.send = b.sgrid + nside;
         b.ubase = b.gbase = INT_MAX;
-        // (a.resident - 1: the slot-loop shape, option resident_update 1..5; 1 and auto: 3 early, steps of 2)
-#define HPCCG_AR(PRE, STEP)                                                                                      \
-    do {                                                                                                         \
-        if (a.nt)                                                                                                \
-            hipLaunchKernelGGL((k_spmv_ar<true, PRE, STEP>), dim3(b.send), dim3(kBlock), 0, s, b, prologue);   \
-        else                                                                                                     \
-            hipLaunchKernelGGL((k_spmv_ar<false, PRE, STEP>), dim3(b.send), dim3(kBlock), 0, s, b, prologue);  \
-    } while (0)
-        switch (a.resident) {
-        case 2: HPCCG_AR(3, 3); break;
-        case 3: HPCCG_AR(3, 4); break;
-        case 4: HPCCG_AR(7, 4); break;
-        case 5: HPCCG_AR(7, 2); break;
-        default: HPCCG_AR(3, 2); break;
-        }
-#undef HPCCG_AR
+        if (a.nt)
+            hipLaunchKernelGGL((k_spmv_ar<true>), dim3(b.send), dim3(kBlock), 0, s, b, prologue);
+        else
+            hipLaunchKernelGGL((k_spmv_ar<false>), dim3(b.send), dim3(kBlock), 0, s, b, prologue);
         return;
     }
-    // update units: one slice per block, or two (a.fu2: four rows per thread)
-    const int ugrid = a.fu2 ? (((a.nslices + 1) / 2 + kNumXcd - 1) / kNumXcd * kNumXcd) : a.grid;
+    // update units: two slices per block (four rows per thread)
+    const int ugrid = ((a.nslices + 1) / 2 + kNumXcd - 1) / kNumXcd * kNumXcd;
     // fused update: [units | side | pad to kNumXcd | update | ghost]; else [units | side | ghost]
     b.ubase = fu ? (b.send + kNumXcd - 1) / kNumXcd * kNumXcd : 0;
     b.gbase = nghost ? (fu ? b.ubase + ugrid : b.send) : INT_MAX;
     const dim3 sg((fu ? b.ubase + ugrid : b.send) + nghost);
     // diagnostics: the block-timeline instantiations of the two fused-update defaults
-    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 7 && a.nt && a.atri &&
-        (a.apre < 0 || a.apre == 7)) {
+    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 7 && a.nt && a.atri) {
         hipLaunchKernelGGL((k_spmv_a<7, true, true, 7, true, true, true>), sg, dim3(kBlock), 0, s, b, prologue);
         return;
     }
-    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 27 && !a.nt && a.apre != 0) {
+    if (kernel == kSpmvDirect && fu && a.dbg_tl && a.a_width == 27 && !a.nt) {
         hipLaunchKernelGGL((k_spmv_a<27, false, true, 4, false, true, true>), sg, dim3(kBlock), 0, s, b, prologue);
         return;
     }
@@ -3059,21 +2933,11 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         else                                                                                                      \
             hipLaunchKernelGGL((k_spmv_a2r<false, W, R>), sg, dim3(2 * kBlock), smem, s, b, prologue); \
     } while (0)
-            if (a.a_width == 7) {
-                switch (a.a2_ring) {
-                case 1: HPCCG_A2R(7, 1); break;
-                case 2: HPCCG_A2R(7, 2); break;
-                case 3: HPCCG_A2R(7, 3); break;
-                default: HPCCG_A2R(7, 4); break;
-                }
-            } else {
-                switch (a.a2_ring) {
-                case 1: HPCCG_A2R(27, 1); break;
-                case 2: HPCCG_A2R(27, 2); break;
-                case 3: HPCCG_A2R(27, 3); break;
-                default: HPCCG_A2R(27, 4); break;
-                }
-            }
+            // (one ring depth, kA2RingDefault: 1, 2 and 4 measured slower)
+            if (a.a_width == 7)
+                HPCCG_A2R(7, kA2RingDefault);
+            else
+                HPCCG_A2R(27, kA2RingDefault);
 #undef HPCCG_A2R
             break;
         }
@@ -3085,20 +2949,13 @@ void launch_cg_spmv(const CgArgs& a, int kernel, bool prologue, hipStream_t s)
         break;
     }
     case kSpmvDirect:
+        // value slots loaded before the iteration test: 4 of 27 (the offsets
+        // early too), all 7 of 7 (7-pt 256^3 same-process A/B: 2445 vs 2422
+        // it/s against 3); other depths measured even or slower
         if (a.a_width == 27) {
-            if (a.apre == 0) {
-                if (a.nt) HPCCG_A(27, true, 0); else HPCCG_A(27, false, 0);
-            } else {
-                if (a.nt) HPCCG_A(27, true, 4); else HPCCG_A(27, false, 4);
-            }
+            if (a.nt) HPCCG_A(27, true, 4); else HPCCG_A(27, false, 4);
         } else if (a.a_width == 7) {
-            if (a.apre == 3) {
-                if (a.nt) HPCCG_A(7, true, 3); else HPCCG_A(7, false, 3);
-            } else if (a.apre == 0) {
-                if (a.nt) HPCCG_A(7, true, 0); else HPCCG_A(7, false, 0);
-            } else {  // auto: all 7 slots early (7-pt 256^3 same-process A/B: 2445 vs 2422 it/s)
-                if (a.nt) HPCCG_A(7, true, 7); else HPCCG_A(7, false, 7);
-            }
+            if (a.nt) HPCCG_A(7, true, 7); else HPCCG_A(7, false, 7);
         } else {
             if (a.nt) HPCCG_A(0, true, 0); else HPCCG_A(0, false, 0);
         }
@@ -3148,24 +3005,8 @@ int persist_capacity(bool nt)
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return 0;
-    // (the smallest of the shapes' figures)
-    int per_cu2 = 0, per_cu3 = 0, per_cu4 = 0;
-    hipError_t e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<true, 2, 1, 0>, kBlock, 0)
-                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<false, 2, 1, 0>, kBlock, 0);
-    if (e == hipSuccess)
-        e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_cg_persist<true, 1, 2, 0>, kBlock, 0)
-               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_cg_persist<false, 1, 2, 0>, kBlock, 0);
-    if (e == hipSuccess)
-        e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu3, k_cg_persist<true, 3, 2, 3>, kBlock, 0)
-               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu3, k_cg_persist<false, 3, 2, 3>, kBlock, 0);
-    if (e == hipSuccess)
-        e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu4, k_cg_persist<true, 3, 1, 3>, kBlock, 0)
-               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu4, k_cg_persist<false, 3, 1, 3>, kBlock, 0);
-    int per_cu5 = 0;
-    if (e == hipSuccess)
-        e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu5, k_cg_persist<true, 4, 1, 4>, kBlock, 0)
-               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu5, k_cg_persist<false, 4, 1, 4>, kBlock, 0);
-    per_cu = std::min(std::min(std::min(per_cu, per_cu2), std::min(per_cu3, per_cu4)), per_cu5);
+    const hipError_t e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<true>, kBlock, 0)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<false>, kBlock, 0);
     return e == hipSuccess ? per_cu * cus : 0;
 }
 
@@ -3179,23 +3020,10 @@ void launch_cg_persist(const CgArgs& a, hipStream_t s)
     b.sgrid = (pairs + kNumXcd - 1) / kNumXcd * kNumXcd;
     b.send = b.sgrid;
     b.ubase = b.gbase = INT_MAX;
-    // (resident_update 6: 2 early register slots + steps of 1; 7: 1 + steps of
-    // 2; 8, 9: 3 LDS-ring slots + steps of 2, 1)
-#define HPCCG_PS(PRE, STEP, L)                                                                             \
-    do {                                                                                                   \
-        if (a.nt)                                                                                          \
-            hipLaunchKernelGGL((k_cg_persist<true, PRE, STEP, L>), dim3(b.sgrid), dim3(kBlock), 0, s, b);  \
-        else                                                                                               \
-            hipLaunchKernelGGL((k_cg_persist<false, PRE, STEP, L>), dim3(b.sgrid), dim3(kBlock), 0, s, b); \
-    } while (0)
-    switch (a.resident - kResidentPersist) {
-    case 1: HPCCG_PS(1, 2, 0); break;
-    case 2: HPCCG_PS(3, 2, 3); break;
-    case 3: HPCCG_PS(3, 1, 3); break;
-    case 4: HPCCG_PS(4, 1, 4); break;
-    default: HPCCG_PS(2, 1, 0); break;
-    }
-#undef HPCCG_PS
+    if (a.nt)
+        hipLaunchKernelGGL((k_cg_persist<true>), dim3(b.sgrid), dim3(kBlock), 0, s, b);
+    else
+        hipLaunchKernelGGL((k_cg_persist<false>), dim3(b.sgrid), dim3(kBlock), 0, s, b);
 }
 
 __global__ __launch_bounds__(256) void k_fill_empty(double* p, long long n)
@@ -3252,11 +3080,10 @@ void launch_peer_selftest(const CgArgs& a, int rounds, double* out, hipStream_t 
     hipLaunchKernelGGL(k_peer_selftest, dim3(1), dim3(64), 0, s, a, rounds, out);
 }
 
-void launch_rearm(int* kst, double* partial, int np, unsigned int* tickets, int nt, int budget, hipStream_t s)
+void launch_rearm(int* kst, double* partial, int np, int budget, hipStream_t s)
 {
-    int cnt = np > nt ? np : nt;
-    if (cnt < 2 * kKstDoubles) cnt = 2 * kKstDoubles;
-    hipLaunchKernelGGL(k_rearm, dim3((cnt + 255) / 256), dim3(256), 0, s, kst, partial, np, tickets, nt, budget);
+    const int cnt = np > 2 * kKstDoubles ? np : 2 * kKstDoubles;
+    hipLaunchKernelGGL(k_rearm, dim3((cnt + 255) / 256), dim3(256), 0, s, kst, partial, np, budget);
 }
 
 void launch_group_sum(const GroupSum& gs, hipStream_t s)

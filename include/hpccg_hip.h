@@ -164,7 +164,7 @@ int hpccg_hip_solve_device(hpccg_hip_matrix* M, const double* b_dev, double* x_d
 /* normr computed in each iteration of the last solve: out[0] = initial
  * residual, out[k] = iteration k (k <= niters). Returns entries written. */
 int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
-/* Solver knobs (set / get):
+/* Solver options (set / get). Twelve settings of the solve:
  *   "spmv_kernel"   -1 auto (default), 0 SELL-512 gather, 1 SELL-512-A with x
  *                   read at the slice's offsets, 2 SELL-512-A with x from LDS
  *                   windows shared by slice pairs; get: the kernel in use
@@ -175,48 +175,23 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   count with the fused update (each captured launch bakes in
  *                   the parity of its k) and to a multiple of the p ring when a
  *                   halo is exchanged; get returns the effective count
- *   "spin_budget_us" bound of every in-kernel wait (the dot slots, the fused
- *                   update's p.Ap total), default 1000000. A wait that outlives
- *                   it records itself on the device and ends the solve: the
- *                   call returns HPCCG_HIP_EHIP naming the wait (block, group,
- *                   iteration, dot), every rank of an RCCL job returns it, and
- *                   the dot slots are reset before the next solve
- *   "dbg_timeline"  diagnostics: 1 = the ring pair kernel (width 27, ring 3)
- *                   records a per-block timeline (hpccg_hip_diag_timeline)
- *   "dbg_withhold"  debug (guard test): slice + 1 whose p.Ap partial is never
- *                   published, so the solve must time out (0 = off)
- *   "rhalo_group"   multi-rank r-halo exchange (get "rhalo": in use; z-slab
- *                   ranks with the p update fused): r's boundary planes move
- *                   after the update into r's ghost planes and the SpMV forms
- *                   p_k at ghost rows itself. 1 (default): the r.r all-reduce
- *                   and the planes in one RCCL group; 0: the all-reduce first
- *   "peer_allreduce" -1 auto (default: an RCCL job whose creation-time
- *                   self-test passed on every rank, and the force_comm 2
- *                   emulation), 0 RCCL, 1 on: the two CG scalars summed inside
- *                   the kernels through IPC-mapped mailboxes
- *   "group_fold"    in-process group run in member order with both dots
- *                   folded: -1 auto (on) / 0: the last member's kernels sum
- *                   the dots in rank order (k_group_sum's sum) instead of a
- *                   k_group_sum launch per dot (get: used by the last solve)
- *   "halo_pull"     r-halo by pull: -1 auto (default), 0 off (the RCCL plane
- *                   group / peer copies), 1 k_pull before each SpMV launch,
- *                   2 in-launch: the iteration's last launch pulls once its
- *                   r.r completion is in (needs the peer all-reduce; auto picks
- *                   it there, else 1); 3 diagnostics (force_comm 2 only):
- *                   in-launch with no rows
- *   "event_timing" 1 = eager launches with hipEvents around every SpMV and
- *                   update (hpccg_hip_kernel_times)
  *   "fuse_p"        -1 auto / 0 off: p = r + beta p formed inside the SpMV
  *                   (pair and direct kernels; on several ranks with the z-slab
- *                   plan, through the r-halo exchange below)
- *   "fold"          dots completed inside the producing kernel (self-validating
- *                   slots; tickets on unit-subset launches): 0 neither
- *                   (k_finalize), 1 both (auto), 2 p.Ap only, 3 r.r only
+ *                   plan, through the r-halo exchange; get "rhalo": in use)
+ *   "fold"          dots completed inside the producing kernel through
+ *                   self-validating slots: -1 / 1 both (default), 0 neither
+ *                   (a k_finalize launch per dot)
  *   "fuse_update"   -1 auto (on) / 0 / 1: one rank, direct kernel: the update
  *                   runs as trailing blocks of the SpMV launch (one launch per
  *                   iteration; same bits); 2: also in an in-process group with
  *                   the peer all-reduce (tests: small members only)
- *   "fused_update_slices"  1 or 2 (default): slices per fused update block
+ *   "resident_update" -1 auto (default): the persistent launch (k_cg_persist,
+ *                   one launch per solve) where every pair block of the matrix
+ *                   fits on the chip at once, else the per-iteration resident
+ *                   pair launch (k_spmv_ar) where that fits; 1 k_spmv_ar only;
+ *                   0 off. get: 8 persistent, 1 k_spmv_ar, 0 neither. A
+ *                   resident solve whose wait expired is re-run with the other
+ *                   launch; get "resident_retries" counts such re-runs
  *   "x_defer"       x += alpha p deferred over the p ring: 1 = every x_ring-th
  *                   update applies it to all rows; 2 (default) = trailing blocks
  *                   of every SpMV launch apply it to the 1/(x_ring-1) of the
@@ -224,33 +199,46 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  *                   with the others); 0 = every iteration (same bits all ways)
  *   "x_ring"        p ring length = x deferral depth, 2..64; -1 auto: 32 for
  *                   matrix images over 512 MB, else 8
- *   "rev_update"    1 = the update kernel walks each XCD's slices backwards
- *   "overlap"       1 = multi-rank, eager launches: halo exchange on a second
- *                   stream beside the interior SpMV (default 0; hipGraph
- *                   replays always run the halo in line on the main stream --
- *                   see DESIGN.md section 6 for the measurements)
  *   "a2_ring"       pair kernel: value slots in flight per wave through its
- *                   LDS-DMA ring, -1 auto (3), 0 register loads, 1..4
- *                   (uniform widths 27 and 7)
- *   "nt_store"      CG vector stores non-temporal: -1 auto (direct kernel on
- *                   an image beyond the Infinity Cache), 0, 1
- *   "lds_ep"        pair kernel: the rows' own p_k taken from the staged
- *                   window instead of reloading r and p_{k-1} (default 1)
- *   "stage16"       pair kernel: windows staged as row pairs with 16-B loads
- *                   and LDS stores (default 1; 0 = one row per thread)
- *   "tri"           direct kernel at width 7: the x triple (offsets -1, 0, +1)
- *                   read once, neighbours from adjacent lanes (default 1)
- *   "a_pre"         direct SELL-512-A kernel: value slots loaded before the
- *                   iteration test, -1 auto (4 at width 27, 7 at width 7), 0,
- *                   3 or 7 (width 7), 4 (width 27)
- *   "force_comm"    diagnostics, 1-rank communicator: 1 = route the two CG
- *                   scalars through ncclAllReduce; 2 = also the multi-rank
- *                   iteration (boundary rows, a plane-sized ncclSend/ncclRecv
- *                   to itself as the halo); captured in the graph like N > 1
+ *                   LDS-DMA ring, -1 auto (3), 0 register loads (uniform widths
+ *                   27 and 7; other depths measured slower and are refused)
+ *   "peer_allreduce" -1 auto (default: an RCCL job whose creation-time
+ *                   self-test passed on every rank, and the force_comm 2
+ *                   emulation), 0 RCCL, 1 on: the two CG scalars summed inside
+ *                   the kernels through IPC-mapped mailboxes
+ *   "halo_pull"     r-halo by pull: -1 auto (default), 0 off (the RCCL plane
+ *                   group / peer copies), 1 k_pull before each SpMV launch,
+ *                   2 in-launch: the iteration's last launch pulls once its
+ *                   r.r completion is in (needs the peer all-reduce; auto picks
+ *                   it there, else 1); 3 diagnostics (force_comm 2 only):
+ *                   in-launch with no rows
+ * Diagnostics:
+ *   "event_timing" 1 = eager launches with hipEvents around every SpMV and
+ *                   update (hpccg_hip_kernel_times)
+ *   "spin_budget_us" bound of every in-kernel wait (the dot slots, the fused
+ *                   update's p.Ap total), default 1000000. A wait that outlives
+ *                   it records itself on the device and ends the solve: the
+ *                   call returns HPCCG_HIP_EHIP naming the wait (block, group,
+ *                   iteration, dot), every rank of an RCCL job returns it, and
+ *                   the dot slots are reset before the next solve
+ *   "force_comm"    1-rank communicator: 1 = route the two CG scalars through
+ *                   ncclAllReduce; 2 = also the multi-rank iteration (a
+ *                   plane-sized ncclSend/ncclRecv to itself as the halo);
+ *                   captured in the graph like N > 1
+ *   "dbg_timeline"  1 = the ring pair kernel (width 27, ring 3) records a
+ *                   per-block timeline (hpccg_hip_diag_timeline)
+ *   "dbg_withhold"  (guard test) slice + 1 whose p.Ap partial is never
+ *                   published, so the solve must time out (0 = off)
+ *   "dbg_resident_stall" (retry test) 1 = the resident launches' p.Ap wait
+ *                   never sees the total, so it expires
  * get only: "has_sell", "has_a", "has_pairs", "a_width", "lds_doubles", "nt",
- * "halo_mode", "num_external", "overlap", "device_bytes" (device memory M
- * holds). None of the knobs changes a computed value: every kernel, fusion and
- * fold setting gives the same bits. */
+ * "nt_store", "halo_mode", "num_external", "group_fold" (the last in-process
+ * group solve summed its dots in its members' kernels), "resident_retries",
+ * "peer_auto_ok", "pull_auto_ok", "proto_auto_ok" (the creation-time
+ * self-tests' verdicts), "placement_pick", "device_bytes" (device memory M
+ * holds). None of the options changes a computed value: every kernel, fusion
+ * and fold setting gives the same bits. Variants that measured even or slower
+ * than these defaults were removed. */
 int hpccg_hip_set_option(hpccg_hip_matrix* M, const char* key, long long value);
 int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* value);
 /* hipEvent kernel timings of the last solve with event_timing on:

@@ -26,16 +26,13 @@ CASES = 64
 OPTIONS = {
     "spmv_kernel": (0, 1, 2, -1),
     "fuse_p": (0, -1),
-    "fold": (0, 1, 2, 3),
+    "fold": (0, 1, -1),
     "x_defer": (0, 1, 2),
     "x_ring": (2, 3, 5, 8, 32, -1),
     "use_graph": (0, 1),
     "graph_chunk": (1, 3, 8, 32),
-    "a2_ring": (-1, 0, 1, 2, 3, 4),
-    "rev_update": (0, 1),
-    "nt_store": (0, 1, -1),
+    "a2_ring": (-1, 0, 3),
     "fuse_update": (0, 1),
-    "fused_update_slices": (1, 2),
 }
 
 
@@ -49,10 +46,10 @@ def _cases():
         max_iter = int(rng.integers(1, 91))
         early = bool(rng.integers(3) == 0)
         opts = {k: int(rng.choice(v)) for k, v in OPTIONS.items()}
-        # the resident fused update (default where it fits) against the other
-        # launch and a second slot-loop shape; drawn apart so the cases above
-        # stay the seed's
-        opts["resident_update"] = (0, -1, 5, 1, 6, 10)[i % 6]
+        # the resident launches (the persistent one by default where it fits;
+        # the per-iteration k_spmv_ar) against the other launch; drawn apart
+        # so the cases above stay the seed's
+        opts["resident_update"] = (0, -1, 1)[i % 3]
         out.append((i, (nx, ny, nz), s7, max_iter, early, opts))
     return out
 

@@ -56,27 +56,22 @@ def test_group_matches_global_reference(hp, gpu, golden, name):
 def test_group_kernel_variants_bitwise(hp, gpu):
     """Multi-rank SpMV kernels (SELL-512 gather, SELL-512-A direct, SELL-512-A
     pair windows whose windows include the ghost planes), the p update fused
-    into the pair and direct kernels (halo rows by k_p_boundary first; the
-    direct kernel's halo lands in r's ghost planes), the halo
-    overlapped with the interior units, the dot completion modes, the deferred
-    x update and graph replay give the same bits."""
+    into the pair and direct kernels (r's halo lands in r's ghost planes), the
+    dot completion modes, the deferred x update and graph replay give the same
+    bits."""
     hp.set_keep_sell(True)
     try:
         Ms = hp.group_generate(24, 20, 9, 3)
     finally:
         hp.set_keep_sell(False)
     ref = None
-    for kernel, fold, fuse, defer, ovl, graph in itertools.product((2, 1, 0), (0, 1, 2), (0, -1), (0, 1, 2),
-                                                                   (0, 1), (0, 1)):
+    for kernel, fold, fuse, defer, graph in itertools.product((2, 1, 0), (0, 1), (0, -1), (0, 1, 2), (0, 1)):
         for M in Ms:
             M.set_option("spmv_kernel", kernel)
             M.set_option("fold", fold)
             M.set_option("fuse_p", fuse)
             M.set_option("x_defer", defer)
-            M.set_option("overlap", ovl)  # eager: halo on the second stream beside the interior SpMV
             M.set_option("use_graph", graph)
-        if kernel > 0:  # graph replays run the halo in line (captured fork/join: DESIGN 6)
-            assert Ms[1].get_option("overlap") == (ovl if not graph else 0)
         # p = r + beta p inside the SpMV on multiple ranks: the pair kernel, and the
         # direct kernel with the halo received into r's ghost planes (z-slab plan)
         assert Ms[1].get_option("fuse_p") == (1 if (fuse and kernel in (1, 2)) else 0)
@@ -87,14 +82,13 @@ def test_group_kernel_variants_bitwise(hp, gpu):
         if ref is None:
             ref = got
         if got != ref:  # (a plain assert would diff megabytes of bytes)
-            pytest.fail(f"{(kernel, fold, fuse, defer, ovl, graph)}: niters {got[0]} vs {ref[0]}, normr {got[1]} "
+            pytest.fail(f"{(kernel, fold, fuse, defer, graph)}: niters {got[0]} vs {ref[0]}, normr {got[1]} "
                         f"vs {ref[1]}, trace equal {got[2] == ref[2]}")
     # the x ring length and graph chunk (a multiple of the ring with a halo)
-    for ring, chunk, fold in ((5, 8, 1), (16, 3, 3), (-1, 8, 2), (32, 1, 0), (2, 13, 2)):
+    for ring, chunk, fold in ((5, 8, 1), (16, 3, 1), (-1, 8, 0), (32, 1, 0), (2, 13, 1)):
         for M in Ms:
             M.set_option("spmv_kernel", -1)
             M.set_option("fuse_p", -1)
-            M.set_option("overlap", 1)
             M.set_option("x_defer", 1 + ring % 2)  # batched / staggered
             M.set_option("x_ring", ring)
             M.set_option("graph_chunk", chunk)
@@ -119,7 +113,7 @@ def test_group_8x200_weak_scaled(hp, gpu):
     nnz = sum(M.info()["nnz"] for M in Ms)
     assert nnz == 1715783992  # (3*200-2)^2 * (3*1600-2)
     for r, M in enumerate(Ms):
-        assert M.get_option("spmv_kernel") == 2 and M.get_option("overlap") == 0
+        assert M.get_option("spmv_kernel") == 2
         assert M.get_option("device_bytes") <= 4.6e9
     niters, normr, xs, times = _solve_group(hp, Ms, max_iter=500)
     assert Ms[0].get_option("graph_used") == 1

@@ -1,9 +1,10 @@
-"""Group fold (option group_fold, on by default): an in-process group run in
-member order sums its two dots in the last member's kernels -- the same
-rank-ordered sum k_group_sum makes (ddot.cpp:79-80's MPI_Allreduce) -- instead
-of a k_group_sum launch per dot. Bar: bitwise the k_group_sum group on every
-kernel, graph and eager, halo by pull and by plane copies, 2 and 3 members;
-off where it does not apply (peer all-reduce, k_finalize)."""
+"""Group fold (always on where it applies; get_option("group_fold") reports
+whether the last solve used it): an in-process group run in member order sums
+its two dots in the last member's kernels -- the same rank-ordered sum
+k_group_sum makes (ddot.cpp:79-80's MPI_Allreduce) -- instead of a
+k_group_sum launch per dot. Bar: bitwise the k_finalize + k_group_sum group
+(fold 0) on every kernel, graph and eager, halo by pull and by plane copies,
+2 and 3 members; off where it does not apply (peer all-reduce, k_finalize)."""
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -40,7 +41,7 @@ CASES = {
 @pytest.mark.parametrize("case", list(CASES))
 def test_group_fold_bitwise(hp, gpu, case):
     dims, P, p7, opts, want = CASES[case]
-    ref, used0 = _solve(hp, gpu, dims, P, p7, dict(opts, group_fold=0))
+    ref, used0 = _solve(hp, gpu, dims, P, p7, dict(opts, fold=0))
     got, used1 = _solve(hp, gpu, dims, P, p7, opts)
     assert used0 == 0 and used1 == want
     assert got == ref

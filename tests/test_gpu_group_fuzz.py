@@ -22,11 +22,10 @@ CASES = 48
 OPTIONS = {
     "spmv_kernel": (0, 1, 2, -1),
     "fuse_p": (0, -1),
-    "fold": (0, 1, 2, 3),
+    "fold": (0, 1, -1),
     "x_defer": (0, 1, 2),
     "x_ring": (2, 4, 8, 32, -1),
     "use_graph": (0, 1),
-    "overlap": (0, 1),
     "a2_ring": (-1, 0, 3),
 }
 

@@ -101,27 +101,17 @@ def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
         assert M.get_option("spmv_kernel") == kernel
         assert M.get_option("fuse_p") == (1 if (fuse and kernel != SELL) else 0)
         out[(kernel, fuse)] = solve_bits(hp, M, prob.b, 120)
-    # the direct kernel's variants: prefetch depth; at width 7 the x triple read
-    # once and shared across lanes (tri), the pair kernel's staging forms
-    M.set_option("spmv_kernel", DIRECT)
-    for fuse, pre, tri in itertools.product((0, -1), ((0, 3, 7) if s7 else (0, 4)), (0, 1)):
-        M.set_option("fuse_p", fuse)
-        M.set_option("a_pre", pre)
-        M.set_option("tri", tri)
-        out[("direct", fuse, pre, tri)] = solve_bits(hp, M, prob.b, 120)
-    M.set_option("spmv_kernel", PAIRS)
-    for fuse, st16, ep in itertools.product((0, -1), (0, 1), (0, 1)):
-        M.set_option("fuse_p", fuse)
-        M.set_option("stage16", st16)
-        M.set_option("lds_ep", ep)
-        out[("pairs", fuse, st16, ep)] = solve_bits(hp, M, prob.b, 120)
     # the pair kernel's value stream: register loads (0) or the LDS-DMA ring
-    # (uniform widths 27 and 7)
-    for fuse, ring in itertools.product((0, -1), (-1, 0, 1, 2, 3, 4)):
+    # (uniform widths 27 and 7); other ring depths are refused
+    M.set_option("spmv_kernel", PAIRS)
+    for fuse, ring in itertools.product((0, -1), (-1, 0, 3)):
         M.set_option("fuse_p", fuse)
         M.set_option("a2_ring", ring)
         assert M.get_option("a2_ring") == (3 if ring < 0 else ring)
         out[("ring", fuse, ring)] = solve_bits(hp, M, prob.b, 120)
+    for ring in (1, 2, 4):
+        with pytest.raises(hp.HPCCGError):
+            M.set_option("a2_ring", ring)
     # x_defer 2: the deferred x terms applied by trailing blocks of the ring
     # kernel's launch (119 iterations: a different remainder per slice for k_xflush)
     for fuse, xring, graph in ((-1, 32, 1), (0, 32, 0), (-1, 2, 1), (-1, 5, 0), (0, 9, 1)):
@@ -137,27 +127,22 @@ def test_kernels_agree_bitwise(hp, gpu, keep_sell, dims, s7):
     M.set_option("a2_ring", -1)
     # and by trailing blocks of the direct kernel's launch
     M.set_option("spmv_kernel", DIRECT)
-    for fuse, xring, pre in ((-1, 32, -1), (0, 8, 0), (-1, 3, -1)):
+    for fuse, xring in ((-1, 32), (0, 8), (-1, 3)):
         M.set_option("fuse_p", fuse)
         M.set_option("x_ring", xring)
-        M.set_option("a_pre", pre)
         assert M.get_option("x_defer") == 2
-        out[("side-direct", fuse, xring, pre)] = solve_bits(hp, M, prob.b, 120)
+        out[("side-direct", fuse, xring)] = solve_bits(hp, M, prob.b, 120)
     # the update as trailing blocks of the direct kernel's launch (fused update)
     M.set_option("x_ring", -1)
-    M.set_option("a_pre", -1)
-    for graph, chunk, tri, spu in ((1, 32, 1, 1), (0, 8, 1, 2), (1, 7, 0, 1), (1, 3, 1, 2), (0, 32, 0, 2)):
+    for graph, chunk in ((1, 32), (0, 8), (1, 7), (1, 3), (0, 32)):
         M.set_option("fuse_p", -1)
         M.set_option("fold", 1)
         M.set_option("use_graph", graph)
         M.set_option("graph_chunk", chunk)
-        M.set_option("tri", tri)
         M.set_option("fuse_update", 1)
-        M.set_option("fused_update_slices", spu)
         assert M.get_option("fuse_update") == 1
-        out[("fused-update", graph, chunk, tri, spu)] = solve_bits(hp, M, prob.b, 120)
+        out[("fused-update", graph, chunk)] = solve_bits(hp, M, prob.b, 120)
     M.set_option("fuse_update", 0)
-    M.set_option("fused_update_slices", 1)
     M.set_option("graph_chunk", 32)
     M.set_option("spmv_kernel", SELL)
     assert M.get_option("x_defer") == 1
@@ -182,13 +167,11 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     M.set_option("resident_update", 0)
     for kernel in (DIRECT, PAIRS):
         M.set_option("spmv_kernel", kernel)
-        for fuse, fold, graph, defer in itertools.product((0, -1), (0, 1, 2, 3), (0, 1), (0, 1, 2)):
+        for fuse, fold, graph, defer in itertools.product((0, -1), (0, 1), (0, 1), (0, 1, 2)):
             M.set_option("fuse_p", fuse)
             M.set_option("fold", fold)
             M.set_option("use_graph", graph)
             M.set_option("x_defer", defer)
-            M.set_option("rev_update", (fold + defer) % 2)
-            M.set_option("nt_store", (fold + graph) % 2)
             assert M.get_option("fold") == fold
             # 119 iterations: x updates left for k_xflush
             results.append(solve_bits(hp, M, prob.b, 120))
@@ -198,7 +181,6 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
     # rings of 2 .. 64, 119 iterations leave 1 .. 55 updates for k_xflush
     # (staggered: a different remainder per slice)
     M.set_option("fold", -1)
-    M.set_option("nt_store", -1)
     for i, (ring, graph) in enumerate(((2, 1), (5, 0), (16, 1), (32, 1), (64, 0), (8, 1), (-1, 1), (32, 0), (5, 1))):
         M.set_option("x_defer", 1 + i % 2)
         M.set_option("x_ring", ring)

@@ -1,4 +1,4 @@
-"""Option resident_update -1 (auto: 8) and 6..10: the persistent CG launch (k_cg_persist) --
+"""Option resident_update -1 (auto; get_option reads 8): the persistent CG launch (k_cg_persist) --
 every iteration after the prologue in ONE launch, each pair block holding its
 rows' x in registers, the dots completed through per-iteration slots and
 neighbour values read with sc1 loads. HPCCG.cpp:358-385 with the same
@@ -22,15 +22,18 @@ def _solve(hp, M, it, gpu, b=None, x0=None, tol=0.0):
 
 @pytest.mark.parametrize("dims,it", [((100, 100, 100), 90), ((40, 36, 30), 120), ((16, 16, 2), 40),
                                      ((64, 64, 64), 60), ((50, 50, 50), 50)])
-@pytest.mark.parametrize("shape", [6, 7, 8, 9, 10])
-def test_persistent_bitwise(hp, gpu, dims, it, shape):
+def test_persistent_bitwise(hp, gpu, dims, it):
     M = hp.Matrix.generate(*dims)
     assert M.get_option("resident_update") == 8  # eligible: the persistent launch is the default here
     M.set_option("resident_update", 0)
     ref = _solve(hp, M, it, gpu)
-    M.set_option("resident_update", shape)
+    M.set_option("resident_update", -1)
     got = _solve(hp, M, it, gpu)
-    assert M.get_option("resident_update") == shape
+    assert M.get_option("resident_update") == 8 and M.get_option("resident_retries") == 0
+    # the per-iteration resident launch (k_spmv_ar) too
+    M.set_option("resident_update", 1)
+    assert _solve(hp, M, it, gpu) == ref and M.get_option("resident_update") == 1
+    M.set_option("resident_update", -1)
     assert got == ref, dims
     # a second solve on the same slots and buffers
     assert _solve(hp, M, it, gpu) == ref
@@ -51,7 +54,7 @@ def test_persistent_tolerance_exit_and_nonzero_x0(hp, gpu):
     tol = float(tr[60])  # the run stops at iteration 61 (normr <= tol there)
     ref = _solve(hp, M, 400, gpu, b, x0, tol)
     assert 50 < ref[0] < 80
-    M.set_option("resident_update", 6)
+    M.set_option("resident_update", -1)
     assert _solve(hp, M, 400, gpu, b, x0, tol) == ref
     M.close()
 
@@ -60,7 +63,7 @@ def test_persistent_max_iter_one(hp, gpu):
     M = hp.Matrix.generate(16, 16, 16)
     M.set_option("resident_update", 0)
     ref = [_solve(hp, M, it, gpu) for it in (1, 2, 3)]
-    M.set_option("resident_update", 6)
+    M.set_option("resident_update", -1)
     assert [_solve(hp, M, it, gpu) for it in (1, 2, 3)] == ref
     M.close()
 
@@ -71,7 +74,7 @@ def test_persistent_event_timing(hp, gpu):
     M = hp.Matrix.generate(40, 36, 30)
     M.set_option("resident_update", 0)
     ref = _solve(hp, M, 50, gpu)
-    M.set_option("resident_update", 6)
+    M.set_option("resident_update", -1)
     M.set_option("event_timing", 1)
     assert _solve(hp, M, 50, gpu) == ref
     kt = M.kernel_times()
@@ -84,14 +87,14 @@ def test_persistent_guard(hp, gpu):
     the spin budget (EHIP, after the per-iteration re-run hits the same
     withheld partial) and the next solve is bitwise the first."""
     M = hp.Matrix.generate(40, 36, 30)
-    M.set_option("resident_update", 6)
+    M.set_option("resident_update", -1)
     ref = _solve(hp, M, 60, gpu)
     M.set_option("spin_budget_us", 100000)
     M.set_option("dbg_withhold", 3)
     with pytest.raises(hp.HPCCGError, match="timed out"):
         _solve(hp, M, 60, gpu)
     M.set_option("dbg_withhold", 0)
-    M.set_option("resident_update", 6)
+    M.set_option("resident_update", -1)
     assert _solve(hp, M, 60, gpu) == ref
     M.close()
 
@@ -99,15 +102,28 @@ def test_persistent_guard(hp, gpu):
 def test_persistent_retry_on_expired_wait(hp, gpu):
     """A persistent launch whose wait expires (dbg_resident_stall: as when not
     every block can be resident) is re-run with the per-iteration launches:
-    the caller gets the default solve's bits."""
+    the caller gets the default solve's bits. Every retry is counted
+    (resident_retries); the matrix tries the persistent launch again at its
+    next solve until three retries have happened, then keeps the other launch."""
     M = hp.Matrix.generate(40, 36, 30)
     M.set_option("resident_update", 0)
     ref = _solve(hp, M, 60, gpu)
-    M.set_option("resident_update", 6)
+    M.set_option("resident_update", -1)
     M.set_option("spin_budget_us", 50000)
     M.set_option("dbg_resident_stall", 1)
+    assert M.get_option("resident_retries") == 0
     assert _solve(hp, M, 60, gpu) == ref
-    assert M.get_option("resident_update") == 0
+    assert M.get_option("resident_retries") == 1 and M.get_option("resident_update") == 8  # re-armed
+    assert _solve(hp, M, 60, gpu) == ref
+    assert _solve(hp, M, 60, gpu) == ref
+    assert M.get_option("resident_retries") == 3 and M.get_option("resident_update") == 0  # kept off now
+    assert _solve(hp, M, 60, gpu) == ref
+    assert M.get_option("resident_retries") == 3  # (no resident attempt any more)
+    M.set_option("dbg_resident_stall", 0)
+    M.set_option("resident_update", -1)  # switched back on by hand
+    assert M.get_option("resident_update") == 8
+    assert _solve(hp, M, 60, gpu) == ref
+    assert M.get_option("resident_retries") == 3
     M.close()
 
 

@@ -71,16 +71,20 @@ def test_resident_update_retry_on_expired_wait(hp, gpu):
     """A resident launch whose p.Ap wait expires -- what happens when another
     process holds part of the GPU and not every unit block can be resident;
     simulated by dbg_resident_stall -- is re-run from the caller's inputs with
-    the unit + update-block launch, which the matrix keeps: the call returns
-    the default solve's bits, resident_update then reads 0, and it can be
-    switched back on."""
+    the unit + update-block launch: the call returns the default solve's
+    bits, the retry is counted, and the matrix tries the resident launch
+    again at its next solve (after three retries it keeps the other launch
+    until switched back on)."""
     M = hp.Matrix.generate(40, 36, 30)
     M.set_option("resident_update", 1)
     ref = _solve(hp, M, 60, gpu)
     M.set_option("spin_budget_us", 50000)
     M.set_option("dbg_resident_stall", 1)
     assert _solve(hp, M, 60, gpu) == ref  # (the failed resident attempt, then the re-run)
-    assert M.get_option("resident_update") == 0
+    assert M.get_option("resident_retries") == 1 and M.get_option("resident_update") == 1
+    assert _solve(hp, M, 60, gpu) == ref
+    assert _solve(hp, M, 60, gpu) == ref
+    assert M.get_option("resident_retries") == 3 and M.get_option("resident_update") == 0
     assert _solve(hp, M, 60, gpu) == ref
     M.set_option("dbg_resident_stall", 0)
     M.set_option("resident_update", 1)

@@ -85,3 +85,17 @@ def test_default_kernels_within_register_budget():
             assert r["vgpr_count"] <= budget, f"{n}: {r['vgpr_count']} VGPRs > budget {budget}"
             assert r.get("vgpr_spill_count", 0) == 0, f"{n}: VGPR spills"
             assert r.get("private_segment_fixed_size", 0) <= 32, f"{n}: scratch {r.get('private_segment_fixed_size')}"
+
+
+def test_instantiation_count():
+    """the variants that measured even or slower are out of
+    the library -- one slot-loop shape each for the resident and persistent
+    launches, one LDS-DMA ring depth, the default prefetch depths (round 5's
+    library held 136 kernels, round 4's 118)."""
+    import collections
+    ks = _kernels()
+    by = collections.Counter(n.split("<")[0].split("(")[0].replace("void ", "") for n in ks)
+    assert by["k_cg_persist"] == 2 and by["k_spmv_ar"] == 2, by
+    assert by["k_spmv_a2r"] <= 5, by  # (27, 7) x fused / not, + the timeline's
+    assert "k_p_boundary" not in by
+    assert len(ks) <= 80, len(ks)

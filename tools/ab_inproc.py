@@ -4,7 +4,7 @@ per-process placement spread does not enter): variants run round-robin,
 `--reps` rounds of `--solves` solves each; prints the median CG it/s and the
 SpMV / update launch averages (one eager event-timed solve per variant).
 
-usage: tools/ab_inproc.py --n 256 --stencil 7 --variants "a_pre=0;a_pre=3"
+usage: tools/ab_inproc.py --n 256 --stencil 7 --variants "x_ring=8;x_ring=32"
 """
 import argparse
 import json

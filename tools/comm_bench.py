@@ -4,7 +4,7 @@
 force_comm = 1 (p.Ap and r.r through ncclAllReduce) or 2 (also the
 multi-rank iteration: halo fork/join on the second stream, a plane-sized
 ncclSend/ncclRecv to itself), against the plain single-GPU solve. One JSON
-line per (force_comm, overlap, use_graph).
+line per (force_comm, use_graph).
 
 usage: tools/comm_bench.py [--n 200] [--steps 3]
 """
@@ -25,8 +25,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--7pt", dest="s7", action="store_true")
-    ap.add_argument("--variants", default="0:0:1,1:0:1,2:0:1,2:1:1,2:0:0,2:1:0",
-                    help="force_comm:overlap:use_graph triples, optionally :spmv_kernel[:rhalo_group[:peer_allreduce[:halo_pull]]] (-1 auto)")
+    ap.add_argument("--variants", default="0:1,1:1,2:1,2:0",
+                    help="force_comm:use_graph pairs, optionally :spmv_kernel[:peer_allreduce[:halo_pull]] (-1 auto)")
     args = ap.parse_args()
     import torch
     hp = load_pkg()
@@ -41,13 +41,11 @@ def main():
         traces = {}
         for v in args.variants.split(","):
             f = [int(t) for t in v.split(":")]
-            fc, ovl, graph = f[:3]
-            M.set_option("spmv_kernel", f[3] if len(f) > 3 else -1)
-            M.set_option("rhalo_group", f[4] if len(f) > 4 else 1)
-            M.set_option("peer_allreduce", f[5] if len(f) > 5 else -1)
-            M.set_option("halo_pull", f[6] if len(f) > 6 else -1)
+            fc, graph = f[:2]
+            M.set_option("spmv_kernel", f[2] if len(f) > 2 else -1)
+            M.set_option("peer_allreduce", f[3] if len(f) > 3 else -1)
+            M.set_option("halo_pull", f[4] if len(f) > 4 else -1)
             M.set_option("force_comm", fc)
-            M.set_option("overlap", ovl)
             M.set_option("use_graph", graph)
 
             def solve():
@@ -64,12 +62,12 @@ def main():
             if base is None:
                 base = us
             traces[v] = M.last_trace().tobytes()
-            print(json.dumps({"n": args.n, "stencil": 7 if args.s7 else 27, "force_comm": fc, "overlap": ovl,
+            print(json.dumps({"n": args.n, "stencil": 7 if args.s7 else 27, "force_comm": fc,
                               "use_graph": graph, "us_per_iter": round(us, 2),
                               "added_us_per_iter": round(us - base, 2),
-                              "overlap_in_use": M.get_option("overlap"), "graph_used": M.get_option("graph_used"),
+                              "graph_used": M.get_option("graph_used"),
                               "kernel": M.get_option("spmv_kernel"), "fuse_p": M.get_option("fuse_p"),
-                              "rhalo": M.get_option("rhalo"), "rhalo_group": M.get_option("rhalo_group"),
+                              "rhalo": M.get_option("rhalo"),
                               "peer_allreduce": M.get_option("peer_allreduce"),
                               "halo_pull": M.get_option("halo_pull"),
                               "fuse_update": M.get_option("fuse_update"),

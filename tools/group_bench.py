@@ -4,7 +4,7 @@ number): P z-slab ranks of n^3 each run as an in-process group on cuda:0
 (k_p_boundary, halo peer copies, rank-ordered scalar sums, graph replay when
 use_graph is on), against P single-rank solves of the same size. The
 difference per iteration is what the multi-rank path adds besides RCCL's own
-latency. One JSON line per group variant (graph on/off x overlap on/off).
+latency. One JSON line per group variant (graph on/off x fold).
 
 usage: tools/group_bench.py [--n 200] [--P 2] [--steps 3]
 """
@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--7pt", dest="s7", action="store_true")
-    ap.add_argument("--variants", default="1:1,1:0,0:1,0:0", help="use_graph:overlap[:group_fold]")
+    ap.add_argument("--variants", default="1:-1,1:0,0:-1", help="use_graph:fold (fold 0: k_finalize + k_group_sum)")
     ap.add_argument("--no-single", action="store_true")
     args = ap.parse_args()
     import torch
@@ -69,24 +69,21 @@ def main():
 
     for v in args.variants.split(","):
             f = [int(t) for t in v.split(":")]
-            graph, overlap = f[0], f[1]
-            gfold = f[2] if len(f) > 2 else -1  # optional third field: group_fold
+            graph, fold = f[0], f[1]
             for M in Ms:
                 M.set_option("use_graph", graph)
-                M.set_option("overlap", overlap)
-                M.set_option("group_fold", gfold)
+                M.set_option("fold", fold)
             group = timed(group_step, 1)
             print(json.dumps({
                 "n": args.n, "P": args.P, "stencil": 7 if args.s7 else 27,
-                "use_graph": graph, "overlap": overlap, "group_fold": Ms[0].get_option("group_fold"),
+                "use_graph": graph, "fold": fold, "group_fold": Ms[0].get_option("group_fold"),
                 "group_us_per_iter": round(group, 2),
                 "P_x_single_us_per_iter": round(single, 2),
                 "multi_rank_overhead_us_per_iter": round(group - single, 2),
                 "overhead_frac": round(group / single - 1, 4),
                 "group": {"kernel": Ms[0].get_option("spmv_kernel"),
                           "graph_used": Ms[0].get_option("graph_used"),
-                          "fuse_p": Ms[0].get_option("fuse_p"),
-                          "overlap": Ms[0].get_option("overlap")},
+                          "fuse_p": Ms[0].get_option("fuse_p")},
                 "single": single_info}), flush=True)
 
 

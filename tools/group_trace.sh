@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel + copy timeline of the in-process group (tools/group_bench.py) for
-# one use_graph:overlap variant per pass; read with tools/trace_gaps.py.
+# one use_graph:fold variant per pass; read with tools/trace_gaps.py.
 set -u
 export TMPDIR=/tmp
 N=${N:-100}
