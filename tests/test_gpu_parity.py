@@ -197,8 +197,8 @@ def test_fusion_options_bitwise_equal(hp, gpu, dims):
 @pytest.mark.parametrize("dims,reps", [((64, 64, 48), 12), ((96, 96, 100), 4)])
 def test_folded_dot_completion_stress(hp, gpu, dims, reps):
     """The in-kernel (fold) dot completion hands partials between workgroups on
-    different XCDs (self-validating slots, or sc1 publish + tickets for unit
-    subsets). Any stale read would change a sum: repeat many solves and compare
+    different XCDs (self-validating slots). Any stale read would change a sum:
+    repeat many solves and compare
     every trace bitwise with the separate k_finalize path (data handed over by
     a kernel boundary). 96x96x100: 1800 slices, 29 groups that straddle the
     XCD eighths of the grid (the waiting member is then not the group's last
@@ -209,7 +209,7 @@ def test_folded_dot_completion_stress(hp, gpu, dims, reps):
         M.set_option("spmv_kernel", kernel)
         M.set_option("fold", 0)
         ref = solve_bits(hp, M, prob.b, 150)
-        for fold in (1, 2, 3):
+        for fold in (1, -1):
             M.set_option("fold", fold)
             for graph in (1, 0):
                 M.set_option("use_graph", graph)
