@@ -87,6 +87,7 @@ def lib() -> C.CDLL:
         "hpccg_hip_comm_destroy": (ip, []),
         "hpccg_hip_comm_size": (ip, [PI, PI]),
         "hpccg_hip_comm_allreduce_host": (ip, [PD, ip, ip]),
+        "hpccg_hip_transport_verdict": (ip, [PI, PI]),
         "hpccg_hip_device_name": (ip, [C.c_char_p, ip, PI]),
         "hpccg_hip_runtime_info": (ip, [PI, C.c_char_p, ip, C.c_char_p, C.c_char_p, ip]),
         "hpccg_generate_matrix": (ip, [ip, ip, ip, ip, ip, ip, C.POINTER(C.POINTER(_HPCMatrix)),
@@ -528,6 +529,16 @@ def comm_allreduce_host(vals, op: str = "sum") -> np.ndarray:
                                                {"sum": 0, "min": 1, "max": 2}[op]),
            "comm_allreduce_host")
     return a
+
+
+def transport_verdict(local) -> list:
+    """The job's in-kernel transport verdicts [peer all-reduce, halo pull,
+    protocol] from this rank's own self-test results (collective over the
+    communicator; what matrix creation decides with)."""
+    a = (C.c_int * 3)(*[int(bool(v)) for v in local])
+    out = (C.c_int * 3)()
+    _check(lib().hpccg_hip_transport_verdict(a, out), "transport_verdict")
+    return list(out)
 
 
 def torch_allgather(data: bytes) -> list:

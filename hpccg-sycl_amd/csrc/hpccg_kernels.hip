@@ -2987,7 +2987,13 @@ void launch_stream_a(const CgArgs& a, hipStream_t s)
     hipLaunchKernelGGL(k_stream_a, dim3(a.grid), dim3(kBlock), 0, s, a);
 }
 
-// Blocks of k_spmv_ar the whole chip holds at once (the host's residency check).
+// Blocks of k_spmv_ar the whole chip holds at once (the host's residency
+// check), at most 4 per CU -- the occupancy the kernel is built for
+// (amdgpu_waves_per_eu(4, 4)). The occupancy API reported 5 once the pruned
+// build brought the kernel to 90 VGPRs, yet a 1040-block launch (102^3) then
+// timed out in its p.Ap wait on the GPU (not every block was resident):
+// residency is only trusted at the designed 4.
+constexpr int kResidentPerCu = 4;
 int resident_capacity(bool nt)
 {
     int per_cu = 0, dev = 0, cus = 0;
@@ -2996,7 +3002,7 @@ int resident_capacity(bool nt)
         return 0;
     const hipError_t e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spmv_ar<true>, kBlock, 0)
                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spmv_ar<false>, kBlock, 0);
-    return e == hipSuccess ? per_cu * cus : 0;
+    return e == hipSuccess ? (per_cu < kResidentPerCu ? per_cu : kResidentPerCu) * cus : 0;
 }
 
 int persist_capacity(bool nt)
@@ -3007,7 +3013,7 @@ int persist_capacity(bool nt)
         return 0;
     const hipError_t e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<true>, kBlock, 0)
                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<false>, kBlock, 0);
-    return e == hipSuccess ? per_cu * cus : 0;
+    return e == hipSuccess ? (per_cu < kResidentPerCu ? per_cu : kResidentPerCu) * cus : 0;
 }
 
 void launch_cg_persist(const CgArgs& a, hipStream_t s)

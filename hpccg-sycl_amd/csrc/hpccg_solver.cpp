@@ -149,6 +149,22 @@ int comm_min(int v, int* out)
     return 0;
 }
 
+// The job's in-kernel transport verdicts from every rank's own self-test
+// results (collective; hpccg_hip_transport_verdict): local = {peer all-reduce,
+// halo pull, production protocol} as this rank saw them. The peer all-reduce
+// and the pull each stay on only where every rank passed; the protocol test
+// counts only where both did, and a protocol failure on any rank turns both
+// off on every rank (RCCL then carries the scalars and r's planes). Every
+// rank computes the same three values from the same gathered table.
+int transport_verdict(const int local[3], int out[3])
+{
+    TRY(comm_min(local[0] ? 1 : 0, &out[0]));
+    TRY(comm_min(local[1] ? 1 : 0, &out[1]));
+    TRY(comm_min((out[0] && out[1] && local[2]) ? 1 : 0, &out[2]));
+    if (out[0] && out[1] && !out[2]) out[0] = out[1] = 0;
+    return 0;
+}
+
 // Gather halo plan (make_local_matrix.cpp:58-610, exchange_externals.cpp:51-131)
 // for partitions the z-slab plan cannot serve: the external columns get local
 // indices n, n+1, ... grouped by owning rank, groups in order of first
@@ -2494,9 +2510,9 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
 // rank passes; otherwise both fall back to RCCL.
 constexpr int kProtoIters = 12;
 
-int protocol_autotest(hpccg_hip_matrix* M, int* all_ok)
+int protocol_autotest(hpccg_hip_matrix* M, int* local_ok)
 {
-    *all_ok = 0;
+    *local_ok = 0;
     int ok = 1;
     const size_t np = M->npad;
     // b and x: the matrix's own workspace (x is the buffer the neighbours have
@@ -2553,7 +2569,12 @@ int protocol_autotest(hpccg_hip_matrix* M, int* all_ok)
             M->selftest_note += "protocol test: the ranks' traces differ; ";
             ok = 0;
         }
-    TRY(comm_min(ok, all_ok));
+    // debug (the fallback tests): this rank reports a failed protocol test
+    if (ok && std::getenv("HPCCG_DBG_FAIL_PROTO")) {
+        M->selftest_note += "protocol test: failed on purpose (HPCCG_DBG_FAIL_PROTO); ";
+        ok = 0;
+    }
+    *local_ok = ok;  // (the job's verdict: transport_verdict)
     return 0;
 }
 
@@ -3009,17 +3030,18 @@ int finish_matrix(hpccg_hip_matrix* M)
         const bool pull = M->halo_pull != 0 && !M->general && (host || !std::getenv("HPCCG_NO_PULL_AUTO"));
         if (peer) TRY(peer_autotest(M));
         if (pull) TRY(pull_autotest(M));
-        M->proto_auto_ok = 0;
-        if (peer && pull && M->peer_auto_ok && M->pull_auto_ok) {  // (the verdicts are every rank's)
-            int ok = 0;
-            TRY(protocol_autotest(M, &ok));
-            M->proto_auto_ok = ok;
-            if (!ok) {  // both fall back to RCCL
-                M->peer_auto_ok = M->pull_auto_ok = 0;
-                for (void* ptr : M->ipc_r_opened) (void)hipIpcCloseMemHandle(ptr);
-                M->ipc_r_opened.clear();
-                M->d_pull_lo = M->d_pull_hi = M->d_pullx_lo = M->d_pullx_hi = nullptr;
-            }
+        // (the peer and pull verdicts so far are every rank's)
+        const bool both = peer && pull && M->peer_auto_ok && M->pull_auto_ok;
+        int local[3] = {M->peer_auto_ok, M->pull_auto_ok, 0}, v[3] = {0, 0, 0};
+        if (both) TRY(protocol_autotest(M, &local[2]));
+        TRY(transport_verdict(local, v));  // collective: the same on every rank
+        M->peer_auto_ok = v[0];
+        M->pull_auto_ok = v[1];
+        M->proto_auto_ok = v[2];
+        if (both && !v[2]) {  // both fall back to RCCL
+            for (void* ptr : M->ipc_r_opened) (void)hipIpcCloseMemHandle(ptr);
+            M->ipc_r_opened.clear();
+            M->d_pull_lo = M->d_pull_hi = M->d_pullx_lo = M->d_pullx_hi = nullptr;
         }
         if (host && !(M->peer_auto_ok && M->pull_auto_ok))
             return set_err(HPCCG_HIP_EPLAN, "host-bootstrapped communicator: the %s self-test failed on some rank "
@@ -3395,6 +3417,13 @@ int hpccg_hip_comm_allreduce_host(double* vals, int n, int op)
     (void)hipFree(d);
     (void)hipStreamDestroy(s);
     return 0;
+}
+
+int hpccg_hip_transport_verdict(const int local[3], int verdict[3])
+{
+    if (!local || !verdict) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    if (!comm_up()) return set_err(HPCCG_HIP_EINVAL, "no communicator (hpccg_hip_comm_init / _init_host first)");
+    return transport_verdict(local, verdict);
 }
 
 int hpccg_hip_runtime_info(int ints_out[6], char* pci_bus_id, int pci_cap, char* rccl_path, char* hip_path,

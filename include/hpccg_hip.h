@@ -75,6 +75,17 @@ int hpccg_hip_comm_mode(int* mode);
 /* Host-value all-reduce over the communicator (main.cpp:206-208,
  * compute_residual.cpp:73): op 0 = sum, 1 = min, 2 = max. In place. */
 int hpccg_hip_comm_allreduce_host(double* vals, int n, int op);
+/* The job's in-kernel transport verdicts (collective over the communicator;
+ * matrix creation calls it after the self-tests): local = this rank's own
+ * results {peer all-reduce, halo pull, production protocol}, verdict = the
+ * job's, the same on every rank -- the peer all-reduce and the pull stay on
+ * only where every rank passed, the protocol counts only where both did, and
+ * a protocol failure on any rank turns both off everywhere (RCCL carries the
+ * scalars and r's planes; a host-bootstrapped job refuses the matrix).
+ * Replaces nothing in the reference (its exchange has one transport). Debug:
+ * HPCCG_DBG_FAIL_PROTO in a rank's environment makes its protocol self-test
+ * report a failure, to exercise the collective fallback. */
+int hpccg_hip_transport_verdict(const int local[3], int verdict[3]);
 /* Device name and compute-unit count of the current device. */
 int hpccg_hip_device_name(char* buf, int cap, int* compute_units);
 /* Runtime identity of this process (diagnostics; replaces nothing in the

@@ -21,6 +21,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
+# scenario -> (this rank's local {peer, pull, protocol} results, the job's verdict)
+SCENARIOS = [
+    (lambda r, w: (1, 1, 1), [1, 1, 1]),                          # every rank passed
+    (lambda r, w: (1, 1, 0 if r == w - 1 else 1), [0, 0, 0]),     # the last rank's protocol test failed: both off
+    (lambda r, w: (0 if r == 0 else 1, 1, 1), [0, 1, 0]),         # rank 0's peer test failed: the pull stays
+    (lambda r, w: (1, 0 if r == 1 else 1, 1), [1, 0, 0]),         # rank 1's pull test failed: the peer stays
+    (lambda r, w: (0 if r == 1 else 1, 1, 0 if r == 0 else 1), [0, 1, 0]),  # protocol counts only with both
+]
+
+
+def _local(sc, rank, world):
+    return SCENARIOS[sc][0](rank, world)
+
+
 def _worker(rank, world, port, q):
     import ctypes as C
 
@@ -41,6 +55,9 @@ def _worker(rank, world, port, q):
         out["sum"] = hp.comm_allreduce_host(v, "sum").tolist()
         out["min"] = hp.comm_allreduce_host(v, "min").tolist()
         out["max"] = hp.comm_allreduce_host(v, "max").tolist()
+        # the self-tests' collective verdict: ranks with
+        # different local results all reach the job's one verdict
+        out["verdicts"] = [hp.transport_verdict(_local(sc, rank, world)) for sc in range(len(SCENARIOS))]
         hp.comm_destroy()
         out["mode_after"] = hp.comm_mode()
         # a callback that returns the wrong shape is refused at init (the
@@ -80,3 +97,4 @@ def test_host_bootstrap_allreduce(world):
         assert np.array(d["sum"]).tobytes() == want_sum.tobytes()
         assert d["min"] == np.min(vs, axis=0).tolist() and d["max"] == np.max(vs, axis=0).tolist()
         assert "comm_init_host failed" in d["bad_cb"] and d["mode_bad"] == "none"
+        assert d["verdicts"] == [want for _, want in SCENARIOS], d["verdicts"]
