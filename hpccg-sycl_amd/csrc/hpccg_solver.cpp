@@ -3047,7 +3047,7 @@ int finish_matrix(hpccg_hip_matrix* M)
             return set_err(HPCCG_HIP_EPLAN, "host-bootstrapped communicator: the %s self-test failed on some rank "
                                             "(peer %d, pull %d, protocol %d); this transport needs all three. "
                                             "This rank: %s",
-                           !M->peer_auto_ok ? "peer all-reduce" : !M->pull_auto_ok ? "halo pull" : "protocol",
+                           both ? "production-protocol" : !M->peer_auto_ok ? "peer all-reduce" : "halo pull",
                            M->peer_auto_ok, M->pull_auto_ok, M->proto_auto_ok,
                            M->selftest_note.empty() ? "passed" : M->selftest_note.c_str());
         if ((peer && !M->peer_auto_ok) || (pull && !M->pull_auto_ok))  // (an RCCL job falls back; say why)

@@ -167,6 +167,31 @@ def main():
         return {"kat1": kat1, "rr": rr, "kat2": float(kat2_rr0(nx, ny, nz * world))}
 
     case("kernel_level", kernel_level)
+
+    # 6: the collective fallback: rank 1's production-
+    # protocol self-test reports a failure (HPCCG_DBG_FAIL_PROTO); every rank
+    # must reach the same verdict -- a host-bootstrapped job has no RCCL to
+    # fall back to, so the matrix is refused on EVERY rank -- and the next
+    # creation, with no failure injected, passes on every rank again
+    def fallback():
+        out = {}
+        if rank == 1:
+            os.environ["HPCCG_DBG_FAIL_PROTO"] = "1"
+        try:
+            M = hp.Matrix.generate(16, 16, 8)
+            out["refused"] = None
+            M.close()
+        except hp.HPCCGError as e:
+            out["refused"] = str(e)
+        finally:
+            os.environ.pop("HPCCG_DBG_FAIL_PROTO", None)
+        dist.barrier()
+        M = hp.Matrix.generate(16, 16, 8)
+        out["after"] = transport(M)
+        M.close()
+        return out
+
+    case("fallback", fallback)
     finish(res, out_dir, rank, hp, dist)
 
 

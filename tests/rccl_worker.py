@@ -62,8 +62,26 @@ def main():
     _, it3, nr3, _ = hp.HPCCG(M, b, x, max_iter=500, device=True)
     assert M.get_option("halo_pull") == (1 if pull_auto else 0)
     assert (it3, nr3, M.last_trace().tobytes(), x.cpu().numpy().tobytes()) == got
-    print(f"RCCL-WORKER-OK rank {rank} graph_used={M.get_option('graph_used')}", flush=True)
+    graph_used = M.get_option("graph_used")
     M.close()
+    # the collective fallback: rank 1's production-protocol
+    # self-test fails (HPCCG_DBG_FAIL_PROTO) -- every rank must reach the same
+    # verdict (both in-kernel transports off) and solve through RCCL: the
+    # scalars by ncclAllReduce, r's planes by ncclSend/ncclRecv
+    if rank == 1:
+        os.environ["HPCCG_DBG_FAIL_PROTO"] = "1"
+    F = hp.Matrix.generate(c["nx"], c["ny"], c["nz"])
+    os.environ.pop("HPCCG_DBG_FAIL_PROTO", None)
+    verdicts = [F.get_option(k) for k in ("peer_auto_ok", "pull_auto_ok", "proto_auto_ok")]
+    assert verdicts == [0, 0, 0], verdicts
+    assert F.get_option("peer_allreduce") == 0 and F.get_option("halo_pull") == 0
+    b, _, _ = F.vectors()
+    x.zero_()
+    _, it4, nr4, times4 = hp.HPCCG(F, b, x, max_iter=500, device=True)
+    assert (it4, nr4, F.last_trace().tobytes(), x.cpu().numpy().tobytes()) == got
+    assert times4[4] > 0.0 and times4[5] > 0.0  # (RCCL's all-reduce and plane exchange stamped)
+    F.close()
+    print(f"RCCL-WORKER-OK rank {rank} graph_used={graph_used}", flush=True)
     hp.comm_destroy()
     dist.destroy_process_group()
 

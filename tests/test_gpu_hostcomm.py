@@ -151,6 +151,22 @@ def test_hostcomm_kernel_level(hostcomm):
         assert c["rr"] == c["kat2"]
 
 
+def test_hostcomm_collective_fallback_verdict(hostcomm):
+    """Rank 1's production-protocol self-test fails (HPCCG_DBG_FAIL_PROTO):
+    both ranks reach the same verdict through the collective
+    hpccg_hip_transport_verdict -- a host-bootstrapped job cannot fall back to
+    RCCL, so the matrix is refused on both, naming the protocol test -- and the
+    next creation passes every self-test on both ranks again."""
+    _, res = hostcomm
+    cs = _case(res, "fallback")
+    for c in cs:
+        assert c["refused"] and "(-5)" in c["refused"] and "protocol" in c["refused"], c["refused"]
+        assert "peer 0, pull 0, protocol 0" in c["refused"], c["refused"]
+        t = c["after"]
+        assert t["peer_auto_ok"] == 1 and t["pull_auto_ok"] == 1 and t["proto_auto_ok"] == 1, t
+    assert "failed on purpose" in cs[1]["refused"]
+
+
 def test_hostcomm_eight_processes_golden(tmp_path, gpu):
     """Eight processes on one GPU -- the world size of the driver's 8-GPU run --
     through the default transport: every rank maps the seven other mailboxes

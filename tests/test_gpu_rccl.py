@@ -100,7 +100,11 @@ def test_rccl_two_processes(hp, gpu, golden):
     """The RCCL job itself: torch.distributed.run launches 2 ranks, one per
     GPU; each generates its z-slab of the 2 x 8^3 problem on its GPU and
     solves with the RCCL halo + all-reduce, graph-replayed; the trace must
-    meet the reference's 2-rank golden (27pt_8x8x8_x2ranks, 1e-7)."""
+    meet the reference's 2-rank golden (27pt_8x8x8_x2ranks, 1e-7). Then the
+    in-kernel transport (peer all-reduce, in-launch pull) bitwise, and the
+    collective fallback: rank 1's protocol self-test fails on purpose
+    (HPCCG_DBG_FAIL_PROTO), both ranks turn the in-kernel transport off and
+    the RCCL solve gives the same bits."""
     import torch
     if torch.cuda.device_count() < 2:
         pytest.skip("needs two visible GPUs (RCCL refuses two ranks on one GPU)")
