@@ -556,7 +556,9 @@ def measure(hp, torch, M, dev, max_iter, steps, warmup, event_steps, world, dist
     # outside the timed region: the last solve's answer (xexact = 1, generate_matrix.cpp:286)
     # and residual reduction, max over ranks -- a wrong multi-rank exchange shows here
     tr = M.last_trace()
-    chk = torch.tensor([(x - 1.0).abs().max().item(), float(nr / tr[0]) if tr[0] > 0 else 0.0],
+    # resident launches re-run after an expired wait (none expected on a box of our own)
+    retries = opt_or_none(M, "resident_retries") or 0
+    chk = torch.tensor([(x - 1.0).abs().max().item(), float(nr / tr[0]) if tr[0] > 0 else 0.0, float(retries)],
                        dtype=torch.float64)
     if world > 1:
         dist.all_reduce(chk, op=dist.ReduceOp.MAX)
@@ -570,7 +572,7 @@ def measure(hp, torch, M, dev, max_iter, steps, warmup, event_steps, world, dist
     return {"elapsed": elapsed, "local_elapsed": local_elapsed, "niters_total": niters_total, "it": it,
             "spmv_avg_s": spmv_avg_s, "timing_src": timing_src, "upd_ms": upd_ms, "upd_n": upd_n,
             "times_acc": times_acc, "step_s": step_s, "cold_s": cold_s, "graph_used": graph_used,
-            "chk": [chk[0].item(), chk[1].item()], "steps": steps, "event_steps": event_steps,
+            "chk": [chk[0].item(), chk[1].item(), int(chk[2].item())], "steps": steps, "event_steps": event_steps,
             "trace": [float(v) for v in tr]}
 
 
@@ -652,7 +654,7 @@ def roofline_of(M, n, stencil, spmv_avg_s):
 
 
 TRANSPORT_KEYS = ("peer_allreduce", "halo_pull", "rhalo", "fuse_update", "peer_auto_ok", "pull_auto_ok",
-                  "proto_auto_ok")
+                  "proto_auto_ok", "persist_auto_ok", "resident_update", "resident_retries")
 
 
 def rank_record(hp, M, rank, dev, comm_mode, rt, meas):
@@ -681,13 +683,17 @@ def multirank_summary(ranks, bytes_per_launch):
     ach = bytes_per_launch / (worst["spmv_avg_us"] * 1e-6) / 1e9
     tr = [r["transport"] for r in ranks]
     in_kernel = all(t.get("peer_allreduce") == 1 and t.get("halo_pull") in (1, 2) for t in tr)
+    persistent = all(t.get("resident_update") == 8 for t in tr)
     return {"spmv_avg_us_max_over_ranks": worst["spmv_avg_us"], "slowest_rank": worst["rank"],
             "frac_max_over_ranks": round(ach / HBM_PEAK_GBS, 4),
             "spmv_avg_us_per_rank": [r["spmv_avg_us"] for r in ranks],
-            "transport_used": ("in-kernel: peer all-reduce + halo pull (no collective call per iteration)"
+            "transport_used": ("in-kernel: peer all-reduce + halo pull inside one persistent launch per solve"
+                               if (in_kernel and persistent) else
+                               "in-kernel: peer all-reduce + halo pull (no collective call per iteration)"
                                if in_kernel else "RCCL (all-reduce and/or send/recv per iteration) on some rank"),
-            "verdicts_per_rank": [{k: t.get(k) for k in ("peer_auto_ok", "pull_auto_ok", "proto_auto_ok")}
-                                  for t in tr],
+            "verdicts_per_rank": [{k: t.get(k) for k in ("peer_auto_ok", "pull_auto_ok", "proto_auto_ok",
+                                                         "persist_auto_ok")} for t in tr],
+            "resident_retries_per_rank": [t.get("resident_retries") for t in tr],
             "halo_us_per_iteration_per_rank": [r["halo_us_per_iteration"] for r in ranks],
             "allreduce_us_per_iteration_per_rank": [r["allreduce_us_per_iteration"] for r in ranks]}
 
@@ -713,7 +719,7 @@ def secondary_config(hp, torch, n, stencil, dev, args, world=1, dist=None, rank=
                "traffic_over_compulsory": roof["traffic_over_compulsory"], "roofline": roof,
                "spmv_kernel": kernel, "graph_replay": bool(meas["graph_used"]),
                "check": {"x_minus_xexact_inf": meas["chk"][0], "final_normr_over_initial": meas["chk"][1],
-                         "niters_per_solve": meas["it"]},
+                         "niters_per_solve": meas["it"], "resident_retries_max_over_ranks": meas["chk"][2]},
                "cpu_baseline": None,
                "cpu_note": "no CPU leg for secondary configs (the headline line carries the reference's)"}
         if world > 1:
@@ -772,7 +778,7 @@ def build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt
         "update_kernel_avg_us": round(meas["upd_ms"] / meas["upd_n"] * 1e3, 2) if (meas["upd_n"] and not fupd)
         else None,
         "check": {"x_minus_xexact_inf": meas["chk"][0], "final_normr_over_initial": meas["chk"][1],
-                  "niters_per_solve": meas["it"]},
+                  "niters_per_solve": meas["it"], "resident_retries_max_over_ranks": meas["chk"][2]},
         # per-solve wall times on rank 0 (first/cold and median of the solves);
         # event steps launch eagerly with hipEvents and are slower than the graph replays
         "solve_ms": {"cold": round(meas["cold_s"] * 1e3, 3) if meas["cold_s"] is not None else None,
@@ -977,8 +983,13 @@ def main():
                 secondary[i]["check"]["trace_vs_oracle"] = trace_record(f"secondary{i}", tr2, n2, n2 * world, st2)
         out = build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt, ranks, cpu, secondary,
                          placement_report(args.placement, probe_us, pick), tchk)
+        retries = [meas["chk"][2]] + [s_["check"]["resident_retries_max_over_ranks"] for s_ in (secondary or [])
+                                       if "check" in s_]
         if not ok_all:
             log("bench: the GPU trace does not match the oracle's within the stated tolerance; exiting 3")
+            exit_code = 3
+        elif any(retries):
+            log(f"bench: resident launches were re-run after an expired wait ({retries}); exiting 3")
             exit_code = 3
         print(json.dumps(out), flush=True)
     if world > 1:

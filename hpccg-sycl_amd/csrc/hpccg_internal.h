@@ -113,6 +113,7 @@ struct CgArgs {
     double* pslots;               // persistent CG (resident == kResidentAuto): per iteration pslot_stride slots, emptied first
     long long pslot_stride;
     int pk0, pk1;                 // persistent CG: the launch runs iterations [pk0, pk1) (its window)
+    int pguard;                   // rows below local row 0 in r and in every p buffer (guard + ghost_lo padding)
     int dbg_withhold;             // debug (guard test): slice + 1 whose p.Ap partial is never published; 0 off
     unsigned long long* dbg_tl;   // diagnostics (option dbg_timeline): per unit 8 words of block clock stamps
                                   // (kTlWords below); null off. Only the timeline instantiation writes it.

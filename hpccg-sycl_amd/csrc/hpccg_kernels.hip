@@ -1611,6 +1611,7 @@ __device__ __forceinline__ double* pers_bcast(const CgArgs& a, int k, int which)
 // wave 0, lane j holds slice s0 + j's partial.
 // role: bit 0 this block waits for its group's partials, bit 1 (with bit 0)
 // its group is the top group (group_last_unit / top_group, once per launch)
+template <bool kMR>
 __device__ __forceinline__ void pers_dot(const CgArgs& a, int role, int s0, int cnt, double bs, int which, int k)
 {
     const int lane = threadIdx.x;
@@ -1658,6 +1659,18 @@ __device__ __forceinline__ void pers_dot(const CgArgs& a, int role, int s0, int 
     // top_sum_wave's shape from the polled values: no second round trip
     double tot = ng <= kTopThreads ? top_sum_polled(wp, ng, lane)
                                    : top_sum_wave([gp](int j) { return ld_sc1(gp + j); }, ng, lane);
+    if constexpr (kMR) {
+        // several ranks: the job's total (MPI_Allreduce, ddot.cpp:79-80) -- this
+        // rank's sum into every rank's mailbox, the contributions summed in rank
+        // order (peer_allreduce; drained: one launch runs every iteration)
+        int bad = 0;
+        if (lane == 0) {
+            stamp(a, k, which == kRR ? kStampArRR : kStampArPAP);
+            tot = peer_allreduce(a, tot, which, k, true);
+            bad = ld_sc1_i(kst_of(a) + kErrBase) != kErrNone;
+        }
+        if (__shfl(bad, 0, kWave)) return;  // (the solve was given up: the waiters see the error record)
+    }
     tot = __shfl(tot, 0, kWave);
     if (lane < kNumXcd) st_sc1(pers_bcast(a, k, which) + kReadyStride * lane, tot);  // the 8 copies at once
     if (lane == 0) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
@@ -1681,7 +1694,11 @@ __device__ __forceinline__ bool pers_wait(const CgArgs& a, int k, int which, dou
     return true;
 }
 
-template <bool kNT, int kPre = 3, int kStep = 2, int kL = 3>
+// kMR: several ranks (z-slabs of a process-per-GPU job): the dots summed over
+// the ranks in the kernel, r's ghost rows pulled from the neighbours at the
+// top of every iteration. Its own instantiation: the one-rank kernel keeps
+// its registers.
+template <bool kNT, bool kMR = false, int kPre = 3, int kStep = 2, int kL = 3>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cg_persist(CgArgs a)
 {
     constexpr int kW = 27;
@@ -1692,6 +1709,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     if (P < 0) return;
     // an earlier window ended the solve, or gave it up
     if (a.pk0 > 1 && (sld(a.kst + 1) || sld(a.kst + kErrBase) != kErrNone)) return;
+    // several ranks (z-slabs): the ghost rows of r this pair reads -- its
+    // windows (awin2: one per offset cluster, holes included) cut to the ghost
+    // planes [-ghost_lo, 0) and [n, n + ghost_hi) -- as segments of one index
+    // range [0, gtot), pulled from the neighbours at the top of every iteration
+    __shared__ int gseg_row[kMR ? 2 * kAWin : 1], gseg_end[kMR ? 2 * kAWin : 1];
+    __shared__ int gseg_tot;
+    if constexpr (kMR) {
+        if (threadIdx.x == 0) {
+            const int prow0 = 2 * P * kSliceRows, nw = a.awn2[P];
+            const int* win = a.awin2 + (size_t)P * kAWin * 3;
+            int ns = 0, tot = 0;
+            for (int w = 0; w < nw; w++) {
+                const int w0 = prow0 + win[3 * w], w1 = w0 + win[3 * w + 1];
+                const int lo0 = max(w0, -a.ghost_lo), lo1 = min(w1, 0);
+                const int hi0 = max(w0, a.n), hi1 = min(w1, a.n + a.ghost_hi);
+                if (lo1 > lo0) {
+                    gseg_row[ns] = lo0;
+                    tot += lo1 - lo0;
+                    gseg_end[ns++] = tot;
+                }
+                if (hi1 > hi0) {
+                    gseg_row[ns] = hi0;
+                    tot += hi1 - hi0;
+                    gseg_end[ns++] = tot;
+                }
+            }
+            for (int j = ns; j < 2 * kAWin; j++) gseg_end[j] = INT_MAX;
+            gseg_tot = tot;
+        }
+        __syncthreads();  // (before the first ring DMAs: nothing to drain yet)
+    }
+    const int gtot = kMR ? gseg_tot : 0;  // block-uniform
     const int s0 = 2 * P;
     const int nsl = min(2, a.nslices - s0);
     const int s1 = nsl > 1 ? s0 + 1 : s0;
@@ -1741,10 +1790,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
             __syncthreads();
         }
     };
-    // r and the p ring through buffer resources based at their guard zones
-    const __amdgpu_buffer_rsrc_t rsr = vec_rsrc(a.r - kGuardRows);
-    const __amdgpu_buffer_rsrc_t rsp = vec_rsrc(a.p - kGuardRows);
-    const int b0 = (row0 + (int)kGuardRows) * 8, b1 = (row1 + (int)kGuardRows) * 8;
+    // r and the p ring through buffer resources based at the start of their
+    // buffers (guard zone, then the ghost_lo planes of several ranks)
+    const __amdgpu_buffer_rsrc_t rsr = vec_rsrc(a.r - a.pguard);
+    const __amdgpu_buffer_rsrc_t rsp = vec_rsrc(a.p - a.pguard);
+    const int b0 = (row0 + a.pguard) * 8, b1 = (row1 + a.pguard) * 8;
     const int pstr = (int)(a.pstride * 8);
     // the rows' x (in registers for the whole solve)
     Rows xv0 = ld(a.x + row0), xv1 = ld(a.x + row1);
@@ -1784,6 +1834,49 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
         }
         if (!run) break;
         const double beta = (k == 1) ? 0.0 : rr1 / rr2;
+        if (kMR && gtot > 0) {
+            // r_{k-1}'s ghost rows from the neighbours (exchange_externals.cpp:
+            // 84-126): system-scope loads of their r, stored write-through there
+            // and drained before their r.r contribution, which the r.r total
+            // this iteration started from includes; they overwrite it only
+            // after this rank's p.Ap contribution, i.e. after this slot loop.
+            // Kept in r's ghost rows, and p_k = r + beta p_{k-1} formed at them
+            // (k_p_update's expression; the owner forms the same bits) into
+            // ring buffer k & 1 for the next iteration's p_{k-1}. Every block
+            // pulls all the ghost rows it reads itself (blocks that share a
+            // row store the same value).
+            if (P == 0 && threadIdx.x == 0) stamp(a, k, kStampHalo);
+            const double* const yg = a.p + (size_t)((k - 1) & 1) * a.pstride;
+            double* const pg = a.p + (size_t)(k & 1) * a.pstride;
+            constexpr int kPullU = 6;  // remote loads in flight per thread
+            for (int e0 = threadIdx.x; e0 < gtot; e0 += kPullU * kBlock) {
+                double v[kPullU];
+                int g[kPullU];
+#pragma unroll
+                for (int u = 0; u < kPullU; u++) {
+                    const int e = e0 + u * kBlock;
+                    g[u] = INT_MIN;
+                    v[u] = 0.0;
+                    if (e < gtot) {
+                        int j = 0;
+                        while (e >= gseg_end[j]) j++;
+                        const int row = gseg_row[j] + (e - (j ? gseg_end[j - 1] : 0));
+                        g[u] = row;
+                        const double* src = row < 0 ? a.pl_src_lo + (row + a.ghost_lo) : a.pl_src_hi + (row - a.n);
+                        v[u] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kPullU; u++) {
+                    if (g[u] == INT_MIN) continue;
+                    const double y = k == 1 ? v[u] : ld_sc1(yg + g[u]);  // (k = 1: p_1 = r_0 + 0 r_0)
+                    st_sc1(a.r + g[u], v[u]);
+                    st_sc1(pg + g[u], v[u] + beta * y);
+                }
+            }
+            vm_wait(0);  // this block's ghost rows are in place before any of its waves reads them
+            bar();
+        }
         // p_{k-1}: ring buffer (k - 1) & 1 (k = 1: r_0, beta 0)
         const __amdgpu_buffer_rsrc_t rsy = k == 1 ? rsr : rsp;
         const int yb = k == 1 ? 0 : ((k - 1) & 1) * pstr;
@@ -1855,7 +1948,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 #pragma unroll
                 for (int i = 0; i < kBlock / kWave; i++) bsj += ws2[lane][i];
             }
-            pers_dot(a, role, s0, nsl, bsj, kPAP, k);
+            pers_dot<kMR>(a, role, s0, nsl, bsj, kPAP, k);
         }
         // the next iteration's first ring slots, landing during the p.Ap wait
         // (this lane's reads of those entries are done: lgkmcnt)
@@ -1910,7 +2003,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 #pragma unroll
                 for (int i = 0; i < kBlock / kWave; i++) bsj += ws2[lane][i];
             }
-            pers_dot(a, role, s0, nsl, bsj, kRR, k);
+            pers_dot<kMR>(a, role, s0, nsl, bsj, kRR, k);
         }
         // the next iteration's early value slots, in flight across the wait
 #pragma unroll
@@ -3011,8 +3104,13 @@ int persist_capacity(bool nt)
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return 0;
-    const hipError_t e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<true>, kBlock, 0)
-                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<false>, kBlock, 0);
+    int per_cu_mr = 0;  // (the multi-rank form's figure too: the smaller counts)
+    hipError_t e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<true>, kBlock, 0)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg_persist<false>, kBlock, 0);
+    if (e == hipSuccess)
+        e = nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_mr, k_cg_persist<true, true>, kBlock, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_mr, k_cg_persist<false, true>, kBlock, 0);
+    per_cu = per_cu < per_cu_mr ? per_cu : per_cu_mr;
     return e == hipSuccess ? (per_cu < kResidentPerCu ? per_cu : kResidentPerCu) * cus : 0;
 }
 
@@ -3026,10 +3124,16 @@ void launch_cg_persist(const CgArgs& a, hipStream_t s)
     b.sgrid = (pairs + kNumXcd - 1) / kNumXcd * kNumXcd;
     b.send = b.sgrid;
     b.ubase = b.gbase = INT_MAX;
-    if (a.nt)
+    if (a.pranks > 1) {  // (a z-slab rank: the peer all-reduce and the pull in the kernel)
+        if (a.nt)
+            hipLaunchKernelGGL((k_cg_persist<true, true>), dim3(b.sgrid), dim3(kBlock), 0, s, b);
+        else
+            hipLaunchKernelGGL((k_cg_persist<false, true>), dim3(b.sgrid), dim3(kBlock), 0, s, b);
+    } else if (a.nt) {
         hipLaunchKernelGGL((k_cg_persist<true>), dim3(b.sgrid), dim3(kBlock), 0, s, b);
-    else
+    } else {
         hipLaunchKernelGGL((k_cg_persist<false>), dim3(b.sgrid), dim3(kBlock), 0, s, b);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_fill_empty(double* p, long long n)

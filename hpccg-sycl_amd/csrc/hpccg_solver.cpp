@@ -304,6 +304,7 @@ struct hpccg_hip_matrix {
     int resident_failed = 0;      // a resident launch's wait expired (GPU shared): the unit + update launch from then on
     int resident_used = 0;        // the last solve ran k_spmv_ar
     int last_dev_err = 0;         // the device error code the last failed solve recorded (DevError)
+    int last_dev_err_all = 0;     // ... its maximum over a job's ranks (all-reduced: the same on every rank)
     size_t npartial = 0;  // dot slots (the last one: the fused update's p.Ap total)
     int a2_ring = kA2RingDefault;  // pair kernel: LDS-DMA value ring depth per wave (0: register loads; uniform widths 27 and 7)
     int fold = -1;        // -1 auto: 1 (both dots completed in their producers); 0 k_finalize
@@ -359,6 +360,7 @@ struct hpccg_hip_matrix {
     int halo_pull = -1;
     int pull_auto_ok = 0;              // RCCL job: the creation-time pull test passed on every rank
     int proto_auto_ok = 0;             // ... and the production-protocol test (protocol_autotest)
+    int persist_auto_ok = 0;           // ... and its persistent-launch run (every rank's blocks co-resident, same bits)
     std::string selftest_note;         // why a creation-time self-test failed on this rank (diagnostics)
     double* d_pull_lo = nullptr;       // rank - 1's r (its local row 0), mapped here (RCCL job)
     double* d_pull_hi = nullptr;       // rank + 1's r
@@ -1410,11 +1412,24 @@ bool resident_of(const hpccg_hip_matrix* M)
 // LDS-ring slots + steps of 2 (four other shapes measured even or slower and
 // are gone: DESIGN.md 4). a.resident = kResidentAuto marks it.
 int persist_shape(const hpccg_hip_matrix* M) { return M->resident_update == -1 ? kResidentAuto : 0; }
+// Several ranks: a process's z-slab rank whose in-kernel
+// transport passed every creation-time test -- the peer all-reduce, the
+// pull, the production protocol and its persistent run on every rank --
+// runs the persistent launch too (its multi-rank instantiation: the dots
+// summed over the ranks in the kernel, r's ghost rows pulled at the top of
+// every iteration), so a 100^3-per-GPU job keeps one launch per solve. The
+// per-iteration resident kernel (k_spmv_ar) has no multi-rank form.
+bool persist_multi_of(const hpccg_hip_matrix* M)
+{
+    return M->nranks > 1 && !M->in_group && M->resident_update == -1 && !M->resident_failed && !M->d_tl &&
+           M->persist_auto_ok && peer_ar_of(M) && pull_of(M) && M->halo_pull != 1 && !M->general && M->has_pairs &&
+           M->kernel == kSpmvDirect && M->a_width == 27 && fuse_update_effective(M);
+}
 bool persist_ok(const hpccg_hip_matrix* M)
 {
-    if (!persist_shape(M) || !resident_of(M)) return false;
+    if (!(persist_shape(M) && resident_of(M)) && !persist_multi_of(M)) return false;
     // (byte offsets of the p ring in 32 bits)
-    if ((M->pstride * 2 + kGuardRows) * (long long)sizeof(double) >= (1LL << 31)) return false;
+    if (M->pstride * 2 * (long long)sizeof(double) >= (1LL << 31)) return false;
     return persist_capacity(nt_load_of(M)) >= grid_of((M->nslices + 1) / 2);
 }
 // ... and its per-iteration slots are allocated: one window of kPersistWindow
@@ -1465,13 +1480,17 @@ CgArgs make_args(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, 
     a.r = M->d_r;
     a.p = M->d_p;
     a.pstride = M->pstride;
+    a.pguard = (int)(kGuardRows + ((size_t)M->ghost_lo + kSliceRows - 1) / kSliceRows * kSliceRows);
     a.fuse_p = fuse_p_effective(M) ? 1 : 0;
     a.xdefer = x_defer_effective(M);
     a.xside = 1;
     a.fupd = fuse_update_effective(M) ? 1 : 0;
     // (1: k_spmv_ar; kResidentAuto: the persistent launch)
     a.resident = 0;
-    if (a.fupd && resident_of(M)) a.resident = persist_of(M, max_iter) ? persist_shape(M) : 1;
+    if (a.fupd && resident_of(M))
+        a.resident = persist_of(M, max_iter) ? persist_shape(M) : 1;
+    else if (a.fupd && persist_multi_of(M) && persist_of(M, max_iter))
+        a.resident = kResidentAuto;
     a.pready = M->d_partial + (M->npartial - kNumXcd * kReadyStride);
     if (a.resident >= kResidentPersist) {
         a.pslots = M->d_pslots;
@@ -2578,6 +2597,76 @@ int protocol_autotest(hpccg_hip_matrix* M, int* local_ok)
     return 0;
 }
 
+// After the protocol test passed on every rank: the persistent launch's
+// multi-rank form (persist_multi_of) on the job's own devices -- a short
+// solve of this matrix with it against the per-iteration launches, bitwise,
+// every rank's blocks co-resident on its GPU for the whole launch (a launch
+// that is not ends in a bounded wait: the solve fails, on every rank). Runs
+// under a short spin budget; the verdict (comm_min) keeps the launch only
+// where every rank passed. Debug: HPCCG_DBG_FAIL_PERSIST fails it here.
+int persist_autotest(hpccg_hip_matrix* M, int* local_ok)
+{
+    *local_ok = 0;
+    int ok = 1;
+    const size_t np = M->npad;
+    std::vector<double> hb(np, 0.0), hx(np, 0.0);
+    for (int i = 0; i < M->nrow; i++) {
+        hb[i] = 1.0 + (double)(((long long)M->start_row + i) % 11) * 0.25;
+        hx[i] = 0.125 * (double)(((long long)M->start_row + i) % 5 - 2);
+    }
+    if (h2d(M, M->d_b, hb.data(), sizeof(double) * np)) ok = 0;
+    struct Run {
+        int it = -1, resident = 0;
+        double nr = 0.0;
+        std::vector<double> trace, x;
+    } run[2];
+    const int ru0 = M->resident_update, pa0 = M->persist_auto_ok, rf0 = M->resident_failed;
+    const long long spin0 = M->spin_us;
+    M->spin_us = std::min<long long>(spin0, 200000);
+    for (int v = 0; v < 2; v++) {  // collective: every rank runs both solves
+        M->resident_update = v == 0 ? 0 : -1;
+        M->persist_auto_ok = v;
+        M->resident_failed = 0;
+        const double* b = M->d_b;
+        double* x = M->d_x;
+        if (h2d(M, x, hx.data(), sizeof(double) * np)) ok = 0;
+        const int rc = solve_ranks(&M, 1, &b, &x, kProtoIters + 1, 0.0, &run[v].it, &run[v].nr, nullptr, 0);
+        run[v].resident = M->resident_used;
+        if (rc) {
+            if (ok) M->selftest_note += "persistent test: a solve failed (" + g_err + "); ";
+            ok = 0;
+        }
+        run[v].trace = M->trace;
+        run[v].x.assign(M->nrow, 0.0);
+        if (rc == 0 && d2h(M->stream, run[v].x.data(), x, sizeof(double) * M->nrow)) ok = 0;
+    }
+    (void)hipGetLastError();
+    M->resident_update = ru0;
+    M->persist_auto_ok = pa0;
+    M->resident_failed = rf0;
+    M->spin_us = spin0;
+    M->trace.clear();
+    M->last_niters = 0;
+    if (ok && run[1].resident != kResidentAuto) {
+        M->selftest_note += "persistent test: not eligible on this rank (the chip cannot hold its blocks); ";
+        ok = 0;
+    }
+    if (ok && !(run[0].it == kProtoIters && run[1].it == run[0].it &&
+                std::memcmp(&run[0].nr, &run[1].nr, sizeof(double)) == 0 &&
+                run[0].trace.size() == run[1].trace.size() &&
+                std::memcmp(run[0].trace.data(), run[1].trace.data(), sizeof(double) * run[0].trace.size()) == 0 &&
+                std::memcmp(run[0].x.data(), run[1].x.data(), sizeof(double) * M->nrow) == 0)) {
+        M->selftest_note += "persistent test: the persistent and the per-iteration launches differ; ";
+        ok = 0;
+    }
+    if (ok && std::getenv("HPCCG_DBG_FAIL_PERSIST")) {
+        M->selftest_note += "persistent test: failed on purpose (HPCCG_DBG_FAIL_PERSIST); ";
+        ok = 0;
+    }
+    *local_ok = ok;
+    return 0;
+}
+
 // After a failed solve: every dot slot empty again, the
 // error record cleared, so the next solve starts from the allocation state.
 int reset_dot_state(hpccg_hip_matrix* M)
@@ -2614,7 +2703,10 @@ int check_device_error(hpccg_hip_matrix* const* Ms, int P, const int* err0)
         if (e[0] != kErrNone || (P == 1 && e[kErrAllRanks] != kErrNone)) bad_rank = r;
     }
     if (bad_rank < 0) return 0;
-    for (int r = 0; r < P; r++) Ms[r]->last_dev_err = e[0] != kErrNone ? e[0] : e[kErrAllRanks];
+    for (int r = 0; r < P; r++) {
+        Ms[r]->last_dev_err = e[0] != kErrNone ? e[0] : e[kErrAllRanks];
+        Ms[r]->last_dev_err_all = e[kErrAllRanks];
+    }
     for (int r = 0; r < P; r++) {
         TRY(reset_dot_state(Ms[r]));
         Ms[r]->solve_dirty = 0;  // reset here (a second reset at the next solve's start could empty a slot a
@@ -2777,7 +2869,7 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
     }
     for (int r = 0; r < P; r++) Ms[r]->gfold_used = av[0].gn > 0 ? 1 : 0;
     M->resident_used = av[0].resident;
-    M->last_dev_err = 0;
+    M->last_dev_err = M->last_dev_err_all = 0;
     const Ranks R{Ms, av.data(), P, gev.data()};
     if (events) TRY(ensure_events(M, iters + 1));
     TRY(enqueue_prologue(R, events));
@@ -2969,11 +3061,23 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
 constexpr int kResidentMaxRetries = 3;
 bool resident_retry(hpccg_hip_matrix* M, int rc)
 {
-    // (the persistent launch waits on every block at each dot: any of its waits)
+    // (the persistent launch waits on every block at each dot: any of its
+    // waits; across ranks also the peer all-reduce's)
     const bool persist_wait = M->resident_used >= kResidentPersist &&
-                              (M->last_dev_err == kErrGroupWait || M->last_dev_err == kErrTopWait);
-    if (rc != HPCCG_HIP_EHIP || !M->resident_used || (M->last_dev_err != kErrReadyWait && !persist_wait))
-        return false;
+                              (M->last_dev_err == kErrGroupWait || M->last_dev_err == kErrTopWait ||
+                               (M->nranks > 1 && M->last_dev_err == kErrPeerWait));
+    bool want = rc == HPCCG_HIP_EHIP && M->resident_used && (M->last_dev_err == kErrReadyWait || persist_wait);
+    if (M->nranks > 1 && !M->in_group && comm_up()) {
+        // a job's ranks re-run together or not at all (every rank returned
+        // EHIP: the error code is all-reduced); one rank's expired wait is
+        // another's missing peer contribution
+        // (a device wait gave up: every rank holds the same all-ranks code and
+        // returned EHIP, so every rank comes here)
+        int none = 1;
+        if (rc != HPCCG_HIP_EHIP || M->last_dev_err_all == kErrNone || comm_min(want ? 0 : 1, &none)) return false;
+        want = none == 0;
+    }
+    if (!want) return false;
     M->resident_failed = 1;
     M->resident_retries++;
     std::fprintf(stderr, "hpccg_hip: the resident launch's wait expired (a shared GPU?); the solve is re-run with "
@@ -3042,6 +3146,15 @@ int finish_matrix(hpccg_hip_matrix* M)
             for (void* ptr : M->ipc_r_opened) (void)hipIpcCloseMemHandle(ptr);
             M->ipc_r_opened.clear();
             M->d_pull_lo = M->d_pull_hi = M->d_pullx_lo = M->d_pullx_hi = nullptr;
+        }
+        // the persistent launch across the ranks: only after the protocol
+        // passed everywhere (v[2] is every rank's), and only where its own
+        // test passed on every rank
+        M->persist_auto_ok = 0;
+        if (v[2]) {
+            int lp = 0;
+            TRY(persist_autotest(M, &lp));
+            TRY(comm_min(lp, &M->persist_auto_ok));
         }
         if (host && !(M->peer_auto_ok && M->pull_auto_ok))
             return set_err(HPCCG_HIP_EPLAN, "host-bootstrapped communicator: the %s self-test failed on some rank "
@@ -3829,7 +3942,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "x_ring")) *value = x_ring_effective(M);
     else if (!std::strcmp(key, "fuse_update")) *value = fuse_update_effective(M) ? 1 : 0;
     else if (!std::strcmp(key, "resident_update"))
-        *value = !resident_of(M) ? 0 : persist_ok(M) ? persist_shape(M) : 1;
+        *value = persist_ok(M) ? kResidentAuto : resident_of(M) ? 1 : 0;
     else if (!std::strcmp(key, "resident_retries")) *value = M->resident_retries;
     else if (!std::strcmp(key, "halo_mode")) *value = M->nranks == 1 ? 0 : (M->general ? 2 : 1);
     else if (!std::strcmp(key, "graph_chunk")) {  // effective: see graph_chunk_of
@@ -3870,6 +3983,7 @@ int hpccg_hip_get_option(const hpccg_hip_matrix* M, const char* key, long long* 
     else if (!std::strcmp(key, "peer_auto_ok")) *value = M->peer_auto_ok;
     else if (!std::strcmp(key, "pull_auto_ok")) *value = M->pull_auto_ok;
     else if (!std::strcmp(key, "proto_auto_ok")) *value = M->proto_auto_ok;
+    else if (!std::strcmp(key, "persist_auto_ok")) *value = M->persist_auto_ok;
     else return set_err(HPCCG_HIP_EINVAL, "unknown option '%s'", key);
     return 0;
 }

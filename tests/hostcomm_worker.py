@@ -49,7 +49,8 @@ def main():
 
     def transport(M):
         return {k: M.get_option(k) for k in ("peer_allreduce", "halo_pull", "rhalo", "fuse_update", "spmv_kernel",
-                                             "peer_auto_ok", "pull_auto_ok", "proto_auto_ok", "graph_used")}
+                                             "peer_auto_ok", "pull_auto_ok", "proto_auto_ok", "graph_used",
+                                             "resident_update", "persist_auto_ok", "resident_retries")}
 
     def case(name, fn):
         t0 = time.time()
@@ -192,6 +193,63 @@ def main():
         return out
 
     case("fallback", fallback)
+
+    # 7: the persistent launch across the processes: one
+    # launch per solve on every rank, the dots summed over the ranks inside it
+    # and r's ghost rows pulled at the top of every iteration -- bitwise the
+    # per-iteration launches of the same transport (resident_update 0), on the
+    # size VERDICT r5 names (2 x 40x36x30) and on 2 x 80^3 (500 pair blocks
+    # per rank: both ranks' blocks co-resident on this one GPU), with the
+    # iteration times of both forms (emulated: the two ranks share the GPU)
+    def persist_case(dims, steps):
+        M = hp.Matrix.generate(*dims)
+        b, _, _ = M.vectors()
+        out = {"transport": transport(M)}
+        solve(M, b)  # (warm)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            it, nr, tr, x, _ = solve(M, b)
+        dist.barrier()
+        out["us_per_iter_persistent"] = (time.perf_counter() - t0) / steps / it * 1e6
+        got = (it, nr, tr.tobytes(), x.tobytes())
+        out["used"] = M.get_option("resident_update")
+        M.set_option("resident_update", 0)
+        solve(M, b)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            it0, nr0, tr0, x0, _ = solve(M, b)
+        dist.barrier()
+        out["us_per_iter_launches"] = (time.perf_counter() - t0) / steps / it0 * 1e6
+        out["same"] = (it0, nr0, tr0.tobytes(), x0.tobytes()) == got
+        out["niters"], out["normr"] = it, nr.hex()
+        out["retries"] = M.get_option("resident_retries")
+        M.close()
+        return out
+
+    case("persist40", lambda: persist_case((40, 36, 30), 3))
+    case("persist80", lambda: persist_case((80, 80, 80), 5))
+
+    # 8: rank 1's persistent-launch self-test fails (HPCCG_DBG_FAIL_PERSIST):
+    # every rank keeps the in-kernel transport but runs the per-iteration
+    # launches (the collective verdict), the same bits
+    def persist_fallback():
+        if rank == 1:
+            os.environ["HPCCG_DBG_FAIL_PERSIST"] = "1"
+        try:
+            M = hp.Matrix.generate(40, 36, 30)
+        finally:
+            os.environ.pop("HPCCG_DBG_FAIL_PERSIST", None)
+        b, _, _ = M.vectors()
+        out = {"transport": transport(M)}
+        it, nr, tr, x, _ = solve(M, b)
+        out["niters"], out["normr"] = it, nr.hex()
+        M.close()
+        return out
+
+    case("persist_fallback", persist_fallback)
     finish(res, out_dir, rank, hp, dist)
 
 

@@ -40,7 +40,8 @@ def _worker(rank, world, port, q):
         sys.path.insert(0, ROOT)
         import bench
         transport = {"peer_allreduce": 1, "halo_pull": 2, "rhalo": 1, "fuse_update": 0, "peer_auto_ok": 1,
-                     "pull_auto_ok": 1, "proto_auto_ok": 1}
+                     "pull_auto_ok": 1, "proto_auto_ok": 1, "persist_auto_ok": 1, "resident_update": 0,
+                     "resident_retries": 0}
         M = _FakeM(transport)
         meas = {"spmv_avg_s": (340.0 + 10.0 * rank) * 1e-6, "local_elapsed": 3.5 + 0.01 * rank,
                 "times_acc": [3.5, 0.01, 0.2, 3.0, 0.004, 0.002, 0.0], "niters_total": 499 * 20}
@@ -52,7 +53,7 @@ def _worker(rank, world, port, q):
             n = 200
             info = {"nrow": n ** 3, "nnz": 213847192, "slots": 216006144}
             full = dict(meas, elapsed=3.52, it=499, step_s=[0.176] * 20, cold_s=0.5, graph_used=1, upd_ms=31.0,
-                        upd_n=500, chk=[4e-15, 1e-70], steps=20, event_steps=1, timing_src="synthetic")
+                        upd_n=500, chk=[4e-15, 1e-70, 0], steps=20, event_steps=1, timing_src="synthetic")
             roof = {"bound": "hbm", "achieved": 6000.0, "peak": 8000.0, "unit": "GB/s", "frac": 0.75,
                     "traffic": 2.04e9, "bytes_per_launch": 2.05e9, "avg_launch_us": 340.0}
             cpu = {"value": 12.0, "unit": "CG iterations/s (global-problem iterations x 2 slabs)", "cores": 16,
@@ -109,6 +110,7 @@ def test_bench_multirank_line_schema():
     assert mr["spmv_avg_us_max_over_ranks"] == pytest.approx(350.0) and mr["slowest_rank"] == 1
     assert mr["frac_max_over_ranks"] == pytest.approx(2.05e9 / 350e-6 / 1e9 / 8000.0, rel=1e-3)
     assert mr["transport_used"].startswith("in-kernel")
+    assert d["check"]["resident_retries_max_over_ranks"] == 0 and mr["resident_retries_per_rank"] == [0, 0]
     assert len(mr["verdicts_per_rank"]) == 2
     # the N > 1 line checks itself against the oracle and
     # carries north_star's second size (100^3 per GPU)

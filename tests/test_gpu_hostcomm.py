@@ -77,6 +77,8 @@ def test_hostcomm_golden(hostcomm, name):
         t = c["transport"]
         assert t["peer_allreduce"] == 1 and t["halo_pull"] == 2 and t["rhalo"] == 1, t
         assert t["peer_auto_ok"] == 1 and t["pull_auto_ok"] == 1 and t["proto_auto_ok"] == 1, t
+        # 27-pt: the persistent launch across the processes (7-pt: per-iteration launches)
+        assert t["persist_auto_ok"] == 1 and t["resident_update"] == (8 if name == "golden27" else 0), t
         assert c["checked"] >= 5 and c["x_err"] <= 1e-12
         assert c["kpull_same"] and c["eager_same"]
         assert c["halo_s"] > 0.0  # the pull stamps the halo class
@@ -90,8 +92,8 @@ def test_hostcomm_bitwise_in_process_group(hostcomm, hp, gpu):
     import torch
     out, res = hostcomm
     cs = _case(res, "bits64")
-    for c in cs:
-        assert c["transport"]["fuse_update"] == 1 and c["transport"]["graph_used"] == 1
+    for c in cs:  # (the persistent launch on both processes: 2 x 256 pair blocks on this GPU)
+        assert c["transport"]["fuse_update"] == 1 and c["transport"]["resident_update"] == 8, c["transport"]
     Ms = hp.group_generate(64, 64, 64, 2)
     xs = [torch.zeros(64 ** 3, dtype=torch.float64, device="cuda:0") for _ in Ms]
     _, it, nr, _ = hp.group_HPCCG(Ms, [M.vectors()[0] for M in Ms], xs, max_iter=500)
@@ -139,6 +141,37 @@ def test_hostcomm_withheld_contribution(hostcomm):
         assert c["error"] and "(-2)" in c["error"] and "timed out" in c["error"], c["error"]
         assert c["seconds_failed"] < 20 * c["budget_s"] + 2.0, c
         assert c["after_same"]
+
+
+@pytest.mark.parametrize("name", ["persist40", "persist80"])
+def test_hostcomm_persistent_across_processes(hostcomm, name):
+    """The persistent launch across two processes (one launch per solve on
+    each, the dots summed over the ranks inside it, r's ghost rows pulled from
+    the other process at the top of every iteration) is bitwise the
+    per-iteration launches of the same transport, with no retry; both ranks
+    report one solve. The per-iteration times of both forms are recorded
+    (emulated: the two ranks share this GPU)."""
+    _, res = hostcomm
+    cs = _case(res, name)
+    for c in cs:
+        assert c["used"] == 8 and c["transport"]["persist_auto_ok"] == 1, c
+        assert c["same"] and c["retries"] == 0, c
+    assert cs[0]["niters"] == cs[1]["niters"] and cs[0]["normr"] == cs[1]["normr"]
+    print(name, {k: round(cs[0][k], 2) for k in ("us_per_iter_persistent", "us_per_iter_launches")})
+
+
+def test_hostcomm_persistent_fallback_verdict(hostcomm):
+    """Rank 1's persistent-launch self-test fails (HPCCG_DBG_FAIL_PERSIST):
+    both ranks keep the in-kernel transport and run the per-iteration
+    launches, and solve the same bits as the persistent launch did."""
+    _, res = hostcomm
+    cs = _case(res, "persist_fallback")
+    ref = _case(res, "persist40")
+    for c in cs:
+        t = c["transport"]
+        assert t["persist_auto_ok"] == 0 and t["resident_update"] == 0, t
+        assert t["peer_auto_ok"] == 1 and t["pull_auto_ok"] == 1 and t["proto_auto_ok"] == 1, t
+        assert (c["niters"], c["normr"]) == (ref[0]["niters"], ref[0]["normr"])
 
 
 def test_hostcomm_kernel_level(hostcomm):

@@ -35,9 +35,12 @@ BUDGETS = {
     # the 977 pair units of 100^3 at once (the host also checks occupancy)
     "k_spmv_ar<false, 3, 2>": 128,
     "k_spmv_ar<true, 3, 2>": 128,
-    # the persistent CG launch (4 blocks per CU: every pair block of 100^3 resident)
-    "k_cg_persist<false, 3, 2, 3>": 128,
-    "k_cg_persist<true, 3, 2, 3>": 128,
+    # the persistent CG launch (4 blocks per CU: every pair block of 100^3
+    # resident); its multi-rank form (peer all-reduce + ghost pull) too
+    "k_cg_persist<false, false, 3, 2, 3>": 128,
+    "k_cg_persist<true, false, 3, 2, 3>": 128,
+    "k_cg_persist<false, true, 3, 2, 3>": 128,
+    "k_cg_persist<true, true, 3, 2, 3>": 128,
 }
 
 
@@ -90,12 +93,13 @@ def test_default_kernels_within_register_budget():
 def test_instantiation_count():
     """the variants that measured even or slower are out of
     the library -- one slot-loop shape each for the resident and persistent
-    launches, one LDS-DMA ring depth, the default prefetch depths (round 5's
+    launches (the persistent one also in its multi-rank form), one LDS-DMA
+    ring depth, the default prefetch depths (round 5's
     library held 136 kernels, round 4's 118)."""
     import collections
     ks = _kernels()
     by = collections.Counter(n.split("<")[0].split("(")[0].replace("void ", "") for n in ks)
-    assert by["k_cg_persist"] == 2 and by["k_spmv_ar"] == 2, by
+    assert by["k_cg_persist"] == 4 and by["k_spmv_ar"] == 2, by  # (one- and multi-rank persistent forms)
     assert by["k_spmv_a2r"] <= 5, by  # (27, 7) x fused / not, + the timeline's
     assert "k_p_boundary" not in by
     assert len(ks) <= 80, len(ks)
