@@ -77,8 +77,10 @@ def test_hostcomm_golden(hostcomm, name):
         t = c["transport"]
         assert t["peer_allreduce"] == 1 and t["halo_pull"] == 2 and t["rhalo"] == 1, t
         assert t["peer_auto_ok"] == 1 and t["pull_auto_ok"] == 1 and t["proto_auto_ok"] == 1, t
-        # 27-pt: the persistent launch across the processes (7-pt: per-iteration launches)
-        assert t["persist_auto_ok"] == 1 and t["resident_update"] == (8 if name == "golden27" else 0), t
+        # 27-pt: the persistent launch across the processes (7-pt: per-iteration
+        # launches -- the persistent kernel is the width-27 one, so its test fails there)
+        p = 1 if name == "golden27" else 0
+        assert t["persist_auto_ok"] == p and t["resident_update"] == 8 * p, t
         assert c["checked"] >= 5 and c["x_err"] <= 1e-12
         assert c["kpull_same"] and c["eager_same"]
         assert c["halo_s"] > 0.0  # the pull stamps the halo class
