@@ -3152,9 +3152,16 @@ int finish_matrix(hpccg_hip_matrix* M)
         // test passed on every rank
         M->persist_auto_ok = 0;
         if (v[2]) {
-            int lp = 0;
-            TRY(persist_autotest(M, &lp));
-            TRY(comm_min(lp, &M->persist_auto_ok));
+            M->persist_auto_ok = 1;  // (would the launch be taken on this rank?)
+            const int elig = persist_ok(M) ? 1 : 0;
+            M->persist_auto_ok = 0;
+            int all = 0;
+            TRY(comm_min(elig, &all));  // (7-pt, images the chip cannot hold: not tested, stays off)
+            if (all) {
+                int lp = 0;
+                TRY(persist_autotest(M, &lp));
+                TRY(comm_min(lp, &M->persist_auto_ok));
+            }
         }
         if (host && !(M->peer_auto_ok && M->pull_auto_ok))
             return set_err(HPCCG_HIP_EPLAN, "host-bootstrapped communicator: the %s self-test failed on some rank "
