@@ -932,6 +932,13 @@ def main():
         for n2, st2 in (((100, 27), (256, 7)) if world == 1 else ((100, 27),)):
             if (n2, st2) == (n, args.stencil):
                 continue
+            if world > 2 * ndev:
+                # an emulation (--comm host, more than two ranks per GPU): the fused 100^3
+                # launches of all the ranks sharing a GPU cannot be resident at once, and their
+                # in-launch waits on each other's p.Ap would expire (creation refuses the matrix)
+                secondary.append({"workload": f"{st2}-pt {n2}^3 per GPU", "skipped":
+                                  f"{world} ranks share {ndev} GPU(s): the fused launches cannot all be resident"})
+                continue
             try:
                 stage("secondary_run", config=f"{st2}pt_{n2}")
                 sec, tr2 = secondary_config(hp, torch, n2, st2, dev, args, world, dist, rank, comm, rt)

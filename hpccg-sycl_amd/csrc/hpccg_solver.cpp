@@ -2602,8 +2602,10 @@ int protocol_autotest(hpccg_hip_matrix* M, int* local_ok)
 // solve of this matrix with it against the per-iteration launches, bitwise,
 // every rank's blocks co-resident on its GPU for the whole launch (a launch
 // that is not ends in a bounded wait: the solve fails, on every rank). Runs
-// under a short spin budget; the verdict (comm_min) keeps the launch only
-// where every rank passed. Debug: HPCCG_DBG_FAIL_PERSIST fails it here.
+// under the matrix's spin budget (a shorter one could expire while another
+// rank's process still loads the kernel's code object); the verdict
+// (comm_min) keeps the launch only where every rank passed. Debug:
+// HPCCG_DBG_FAIL_PERSIST fails it here.
 int persist_autotest(hpccg_hip_matrix* M, int* local_ok)
 {
     *local_ok = 0;
@@ -2621,8 +2623,6 @@ int persist_autotest(hpccg_hip_matrix* M, int* local_ok)
         std::vector<double> trace, x;
     } run[2];
     const int ru0 = M->resident_update, pa0 = M->persist_auto_ok, rf0 = M->resident_failed;
-    const long long spin0 = M->spin_us;
-    M->spin_us = std::min<long long>(spin0, 200000);
     for (int v = 0; v < 2; v++) {  // collective: every rank runs both solves
         M->resident_update = v == 0 ? 0 : -1;
         M->persist_auto_ok = v;
@@ -2644,7 +2644,6 @@ int persist_autotest(hpccg_hip_matrix* M, int* local_ok)
     M->resident_update = ru0;
     M->persist_auto_ok = pa0;
     M->resident_failed = rf0;
-    M->spin_us = spin0;
     M->trace.clear();
     M->last_niters = 0;
     if (ok && run[1].resident != kResidentAuto) {
