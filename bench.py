@@ -251,7 +251,7 @@ def _ref_legs(oracle, A, legs, nx, ny, nz, use_7pt, world):
             t = oracle.ref_hpccg(M, A.b, max_iter=probe + 1)["times"][0]
             iters = int(max(probe, min(500, budget / max(t / probe, 1e-6))))
             res = oracle.ref_hpccg(M, A.b, max_iter=iters + 1)
-            its = res["niters"] / res["times"][0]
+            its = res["niters"] / max(res["times"][0], 1e-9)  # (a tiny sample can round to 0 s)
             what = (f"global {nx}x{ny}x{nz} (the {world} slabs together)" if world > 1 else f"{nx}x{ny}x{nz}")
             sample = (f"{what} {'7' if use_7pt else '27'}-pt, first {res['niters']} CG iterations of one reference "
                       f"HPCCG() solve ({res['times'][0]:.1f} s)")

@@ -253,16 +253,10 @@ constexpr int kPersistWindow = 512;  // iterations per persistent launch (its sl
 int persist_capacity(bool nt);
 void launch_cg_persist(const CgArgs& a, hipStream_t s);
 void launch_fill_empty(double* p, long long n, hipStream_t s);
-// slots per iteration of the persistent launch (kPersW partials per slice:
-// one per wave where every wave publishes its own, HPCCG_PW)
-#ifdef HPCCG_PW
-constexpr int kPersW = 4;
-#else
-constexpr int kPersW = 1;
-#endif
+// slots per iteration of the persistent launch
 inline long long persist_slot_stride(int nslices)
 {
-    return 2LL * kPersW * nslices + 2LL * ((nslices + 63) / 64) + 2LL * kNumXcd * kReadyStride;
+    return 2LL * nslices + 2LL * ((nslices + 63) / 64) + 2LL * kNumXcd * kReadyStride;
 }
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);

@@ -1604,58 +1604,30 @@ __device__ __forceinline__ double* pers_slots(const CgArgs& a, int k)
 __device__ __forceinline__ double* pers_bcast(const CgArgs& a, int k, int which)
 {
     const int ng = ngroups_of(a);
-    return pers_slots(a, k) + 2 * kPersW * a.nslices + 2 * ng + which * kNumXcd * kReadyStride;
+    return pers_slots(a, k) + 2 * a.nslices + 2 * ng + which * kNumXcd * kReadyStride;
 }
 
 // complete_dot_lanes' slot protocol on iteration k's own slots (no resets):
 // wave 0, lane j holds slice s0 + j's partial.
 // role: bit 0 this block waits for its group's partials, bit 1 (with bit 0)
 // its group is the top group (group_last_unit / top_group, once per launch)
-// HPCCG_PW: every wave publishes its own partials (slot [slice][wave]) right
-// after its own drain, no block barrier; the group waiter sums a slice's four
-// in the block's order from 0.0 (the same bits as the block sum).
-__device__ __forceinline__ __attribute__((unused)) void pers_pub(const CgArgs& a, int s0, int cnt, double w0, double w1, int which, int k,
-                                         int wv)
-{
-    double* const sp = pers_slots(a, k) + which * kPersW * a.nslices;
-    if (!(which == kPAP && s0 == a.dbg_withhold - 1)) st_sc1(sp + s0 * kPersW + wv, w0);
-    if (cnt > 1 && !(which == kPAP && s0 + 1 == a.dbg_withhold - 1)) st_sc1(sp + (s0 + 1) * kPersW + wv, w1);
-}
 template <bool kMR>
 __device__ __forceinline__ void pers_dot(const CgArgs& a, int role, int s0, int cnt, double bs, int which, int k)
 {
     const int lane = threadIdx.x;
     double* const base = pers_slots(a, k);
     const int ng = ngroups_of(a);
-    double* const sp = base + which * kPersW * a.nslices;
-    double* const gp = base + 2 * kPersW * a.nslices + which * ng;
+    double* const sp = base + which * a.nslices;
+    double* const gp = base + 2 * a.nslices + which * ng;
     const int g = s0 / kGroup;
     const int i = g * kGroup + lane;
-    if constexpr (kPersW == 1)
-        if (lane < cnt && !(which == kPAP && s0 + lane == a.dbg_withhold - 1)) st_sc1(sp + s0 + lane, bs);
+    if (lane < cnt && !(which == kPAP && s0 + lane == a.dbg_withhold - 1)) st_sc1(sp + s0 + lane, bs);
     if (!(role & 1)) return;
     double v;
     unsigned t0 = 0, polls = 0;
     for (;;) {
-        if constexpr (kPersW == 1) {
-            v = i < a.nslices ? ld_sc1(sp + i) : 0.0;
-            if (__all(i >= a.nslices || slot_full(v))) break;
-        } else {
-            double w[kPersW];
-            bool full = true;
-#pragma unroll
-            for (int j = 0; j < kPersW; j++) {
-                w[j] = i < a.nslices ? ld_sc1(sp + i * kPersW + j) : 0.0;
-                full = full && (i >= a.nslices || slot_full(w[j]));
-            }
-            if (__all(full)) {
-                v = 0.0;  // (the block sum's order: ws2[.][0..3] from 0.0)
-#pragma unroll
-                for (int j = 0; j < kPersW; j++) v += w[j];
-                if (i >= a.nslices) v = 0.0;
-                break;
-            }
-        }
+        v = i < a.nslices ? ld_sc1(sp + i) : 0.0;
+        if (__all(i >= a.nslices || slot_full(v))) break;
         if ((++polls & 15) == 0 && wait_expired(a, t0)) {
             if (lane == 0) abort_solve(a, kErrGroupWait, g, k, which);
             return;
@@ -1964,17 +1936,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
         }
         {
             const double w0 = wave_sum(d0), w1 = wave_sum(d1);
-            if constexpr (kPersW > 1) {
-                if (lane == 0) pers_pub(a, s0, nsl, w0, w1, kPAP, k, wv);
-            } else if (lane == 0) {
+            if (lane == 0) {
                 ws2[0][threadIdx.x / kWave] = w0;
                 ws2[1][threadIdx.x / kWave] = w1;
             }
         }
-        if constexpr (kPersW == 1) bar();
+        bar();
         if (threadIdx.x < kWave) {
             double bsj = 0.0;
-            if (kPersW == 1 && lane < 2) {
+            if (lane < 2) {
 #pragma unroll
                 for (int i = 0; i < kBlock / kWave; i++) bsj += ws2[lane][i];
             }
@@ -2021,17 +1991,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
             // this wave's p_k and r_k have landed before the block's r.r partial
             // (the next iteration's readers are ordered after the r.r total)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if constexpr (kPersW > 1) {
-                if (lane == 0) pers_pub(a, s0, nsl, w0, w1, kRR, k, wv);
-            } else if (lane == 0) {
+            if (lane == 0) {
                 ws2[0][threadIdx.x / kWave] = w0;
                 ws2[1][threadIdx.x / kWave] = w1;
             }
         }
-        if constexpr (kPersW == 1) bar();
+        bar();
         if (threadIdx.x < kWave) {
             double bsj = 0.0;
-            if (kPersW == 1 && lane < 2) {
+            if (lane < 2) {
 #pragma unroll
                 for (int i = 0; i < kBlock / kWave; i++) bsj += ws2[lane][i];
             }
@@ -2058,8 +2026,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
             vm_wait(0);
             return;
         }
-        // (tot_s is written again only once the next p.Ap total exists, which
-        // needs every wave's next partial, published after this read)
+        // (tot_s is written again only after the next p.Ap barrier -- and only
+        // once the next p.Ap total exists, which needs every wave's next partial)
         rr2 = rr1;
         rr1 = tot_s;
     }
