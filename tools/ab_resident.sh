@@ -1,11 +1,9 @@
-# Round-robin A/B of the resident launches at 100^3 (option resident_update
-# 0 = the unit + update-block launch; k_spmv_ar 1 = 3 early slots and steps of
-# 2, 2 = 3/3, 3 = 3/4, 4 = 7/4, 5 = 7/2; the persistent k_cg_persist 6 = 2
-# early register slots + steps of 1, 7 = 1/2, 8 = 3 LDS-ring slots + steps of
-# 2 (auto), 9 = 3 ring/1, 10 = 4 ring/1), fresh process per line.
+# Round-robin A/B of the launch forms at 100^3 (option resident_update 0 = the
+# unit + update-block launch, 1 = the per-iteration resident k_spmv_ar, -1 =
+# auto: the persistent k_cg_persist), fresh process per line.
 export TMPDIR=/tmp; mkdir -p gpurun_out/abr; : > gpurun_out/abr/summary.log
 for rep in $(seq ${REPS:-2}); do
-  for v in ${SHAPES:-0 1 2 3 4 5}; do
+  for v in ${SHAPES:-0 1 -1}; do
     timeout -k 10 200 python bench.py --n ${N:-100} --no-cpu-baseline --no-trace-check --no-secondary --steps ${STEPS:-10} \
         --set resident_update=$v > gpurun_out/abr/one.json 2>> gpurun_out/abr/err.log || exit 1
     python3 -c "

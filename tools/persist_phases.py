@@ -13,7 +13,7 @@ from bench import load_pkg  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=100)
-ap.add_argument("--shapes", default="1,8")
+ap.add_argument("--shapes", default="1,-1", help="resident_update values (1 k_spmv_ar, -1 the persistent launch)")
 args = ap.parse_args()
 import torch  # noqa: E402
 hp = load_pkg()
