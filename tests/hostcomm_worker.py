@@ -230,6 +230,40 @@ def main():
         return out
 
     case("persist40", lambda: persist_case((40, 36, 30), 3))
+
+    # the persistent launch across processes over two launch windows (1100
+    # iterations: kPersistWindow = 512 per launch; the second launch resumes
+    # from the ghost rows and mailbox parities the first left), with a
+    # tolerance exit inside the second window and from a nonzero x0: bitwise
+    # the per-iteration launches
+    def persist_windows():
+        M = hp.Matrix.generate(40, 36, 30)
+        b, _, _ = M.vectors()
+        n = M.info()["nrow"]
+        g = torch.arange(n, dtype=torch.float64, device=f"cuda:{dev}") + rank * n
+        x0 = 0.125 * (torch.remainder(g, 5.0) - 2.0)
+
+        def run(max_iter, tol=0.0):
+            x = x0.clone()
+            _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=max_iter, tolerance=tol, device=True)
+            return it, nr, M.last_trace().tobytes(), x.cpu().numpy().tobytes()
+
+        out = {"used": M.get_option("resident_update")}
+        M.set_option("resident_update", 0)
+        ref = run(1100)
+        tr = np.frombuffer(ref[2])
+        tol = float(tr[700])
+        ref_tol = run(1100, tol)
+        M.set_option("resident_update", -1)
+        got, got_tol = run(1100), run(1100, tol)
+        out["same"] = got == ref
+        out["same_tol"] = got_tol == ref_tol
+        out["niters"], out["niters_tol"] = ref[0], ref_tol[0]
+        out["retries"] = M.get_option("resident_retries")
+        M.close()
+        return out
+
+    case("persist_windows", persist_windows)
     case("persist80", lambda: persist_case((80, 80, 80), 5))
 
     # 8: rank 1's persistent-launch self-test fails (HPCCG_DBG_FAIL_PERSIST):

@@ -162,6 +162,16 @@ def test_hostcomm_persistent_across_processes(hostcomm, name):
     print(name, {k: round(cs[0][k], 2) for k in ("us_per_iter_persistent", "us_per_iter_launches")})
 
 
+def test_hostcomm_persistent_windows(hostcomm):
+    """The persistent launch across processes over two launch windows (1100
+    iterations) and with a tolerance exit inside the second, from a nonzero
+    x0: bitwise the per-iteration launches on both ranks."""
+    _, res = hostcomm
+    for c in _case(res, "persist_windows"):
+        assert c["used"] == 8 and c["same"] and c["same_tol"] and c["retries"] == 0, c
+        assert c["niters"] > 700 and 512 < c["niters_tol"] < 1099, c
+
+
 def test_hostcomm_persistent_fallback_verdict(hostcomm):
     """Rank 1's persistent-launch self-test fails (HPCCG_DBG_FAIL_PERSIST):
     both ranks keep the in-kernel transport and run the per-iteration
