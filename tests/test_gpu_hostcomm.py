@@ -216,9 +216,11 @@ def test_hostcomm_eight_processes_golden(tmp_path, gpu):
     """Eight processes on one GPU -- the world size of the driver's 8-GPU run --
     through the default transport: every rank maps the seven other mailboxes
     (the in-kernel all-reduce sums eight contributions in rank order) and pulls
-    its ghost planes from its z-neighbours' memory; all creation-time
-    self-tests pass on every rank and the solve meets the reference's 8-rank
-    golden (27pt_16x16x16_x8ranks: 16x16x128 global) at RTRANS_RTOL_MULTI.
+    its ghost planes from its z-neighbours' memory, inside one persistent
+    launch per solve; all creation-time self-tests pass on every rank and the
+    solve meets the reference's 8-rank golden (27pt_16x16x16_x8ranks: 16x16x128
+    global) at RTRANS_RTOL_MULTI; the per-iteration launches (k_pull, eager)
+    give the same bits.
     Same caveats as above: no xGMI here."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     port = 29300 + os.getpid() % 250
@@ -236,6 +238,8 @@ def test_hostcomm_eight_processes_golden(tmp_path, gpu):
         t = c["transport"]
         assert t["peer_allreduce"] == 1 and t["halo_pull"] == 2 and t["rhalo"] == 1, t
         assert t["peer_auto_ok"] == 1 and t["pull_auto_ok"] == 1 and t["proto_auto_ok"] == 1, t
+        # the persistent launch across the eight processes (interior ranks pull from both sides)
+        assert t["persist_auto_ok"] == 1 and t["resident_update"] == 8, t
         assert c["checked"] >= 5 and c["x_err"] <= 1e-12
         assert c["kpull_same"] and c["eager_same"]
     # every rank reports the same global solve
