@@ -1,7 +1,7 @@
 """Nothing carries from one solve into the next.
 
 HPCCG.cpp:342-356 starts every solve from r = b - A x; the device-resident
-solver keeps iteration state, dot slots, ready slots, tickets, scalars and
+solver keeps iteration state, dot slots, ready slots, scalars and
 rings between solves, and re-arms them at every solve start (k_rearm). Each
 test solves one matrix with b1, then with b2 (a different right-hand side),
 possibly after a disturbance -- the placement probe's timed solves and buffer
