@@ -284,6 +284,55 @@ def main():
         return out
 
     case("persist_fallback", persist_fallback)
+
+    # 9: degenerate starts across the processes (tests/test_gpu_edge.py's
+    # cases): the persistent launch and the per-iteration launches give the
+    # same outcome -- no iteration from a zero or NaN residual, the 0/0 path
+    # to niters 2 under a negative tolerance or an infinite b entry -- with the
+    # non-finite entry on rank 1's first plane (the rows rank 0 pulls); the
+    # NaN partials pass the dot slots and mailboxes without a wait expiring
+    def degenerate():
+        dims = (40, 36, 30)
+        M = hp.Matrix.generate(*dims)
+        n = M.info()["nrow"]
+        d = f"cuda:{dev}"
+        ones = torch.ones(n, dtype=torch.float64, device=d)
+        y = torch.zeros(n, dtype=torch.float64, device=d)
+        hp.HPC_sparsemv(M, ones, y)  # this rank's b (KAT-1: A 1 = b bitwise)
+        i = 7 if rank == 1 else 0
+        runs = {}
+
+        def put(v, val):
+            w = y.clone() if v is None else v.clone()
+            if rank == 1:
+                w[i] = val
+            return w
+
+        todo = {"exact": (y, ones, 30, 0.0), "zero_rhs": (torch.zeros_like(y), torch.zeros_like(y), 30, 0.0),
+                "exact_negtol": (y, ones, 30, -1.0), "nan_b": (put(None, float("nan")), torch.zeros_like(y), 30, 0.0),
+                "nan_x0": (y, put(torch.zeros_like(y), float("nan")), 30, 0.0),
+                "inf_x0": (y, put(torch.zeros_like(y), float("inf")), 30, 0.0),
+                "inf_b": (put(None, float("-inf")), torch.zeros_like(y), 30, 0.0)}
+        out = {"used": M.get_option("resident_update")}
+        for form in (-1, 0):
+            M.set_option("resident_update", form)
+            for name, (bb, x0, mi, tol) in todo.items():
+                x = x0.clone()
+                _, it, nr, _ = hp.HPCCG(M, bb, x, max_iter=mi, tolerance=tol, device=True)
+                xh = x.cpu().numpy()
+                rec = (it, nr.hex(), xh.tobytes())
+                if form == -1:
+                    runs[name] = rec
+                    out[name] = {"niters": it, "normr": nr.hex(), "x_nan": int(np.isnan(xh).sum()),
+                                 "x_is_x0": bool(np.array_equal(xh, x0.cpu().numpy(), equal_nan=True))}
+                else:
+                    out[name]["launches_same"] = rec == runs[name]
+        out["retries"] = M.get_option("resident_retries")
+        out["n"] = n
+        M.close()
+        return out
+
+    case("degenerate", degenerate)
     finish(res, out_dir, rank, hp, dist)
 
 

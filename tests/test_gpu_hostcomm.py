@@ -186,6 +186,49 @@ def test_hostcomm_persistent_fallback_verdict(hostcomm):
         assert (c["niters"], c["normr"]) == (ref[0]["niters"], ref[0]["normr"])
 
 
+def test_hostcomm_degenerate_starts(hostcomm):
+    """tests/test_gpu_edge.py's degenerate starts across the processes, the
+    non-finite entry on rank 1's first plane (rows rank 0 pulls): the
+    persistent launch and the per-iteration launches give the same bits, and
+    both ranks the oracle's outcome on the global 40x36x60 problem -- niters,
+    normr (0 or NaN, exact), x untouched where no iteration ran, all NaN after
+    the 0/0 path -- with no wait expired."""
+    import math
+    import oracle
+    _, res = hostcomm
+    cs = _case(res, "degenerate")
+    A = oracle.generate(40, 36, 60)
+    n = cs[0]["n"]
+    N = A.nrow
+    row = n + 7  # rank 1's row 7, global
+    ones = np.ones(N)
+    zeros = np.zeros(N)
+
+    def at(v, val):
+        w = v.copy()
+        w[row] = val
+        return w
+
+    todo = {"exact": (A.b, ones, 0.0), "zero_rhs": (zeros, zeros, 0.0), "exact_negtol": (A.b, ones, -1.0),
+            "nan_b": (at(A.b, np.nan), zeros, 0.0), "nan_x0": (A.b, at(zeros, np.nan), 0.0),
+            "inf_x0": (A.b, at(zeros, np.inf), 0.0), "inf_b": (at(A.b, -np.inf), zeros, 0.0)}
+    for name, (b, x0, tol) in todo.items():
+        ref = oracle.hpccg(A, b=b, x=x0, max_iter=30, tolerance=tol)
+        rnan = math.isnan(ref["normr"])
+        for c in cs:
+            d = c[name]
+            assert d["launches_same"], (name, d)
+            assert d["niters"] == ref["niters"], (name, d, ref["niters"])
+            nr = float.fromhex(d["normr"])
+            assert (rnan and math.isnan(nr)) or nr == ref["normr"], (name, d)
+            if ref["niters"] == 0:
+                assert d["x_is_x0"], (name, d)
+            else:
+                assert d["x_nan"] == n and np.isnan(ref["x"]).all(), (name, d)
+    for c in cs:
+        assert c["used"] == 8 and c["retries"] == 0, c
+
+
 def test_hostcomm_kernel_level(hostcomm):
     """HPC_sparsemv with the host-staged halo: A 1 = b bitwise on both ranks
     (KAT-1 across the slab boundary); ddot all-reduced over the callback:

@@ -194,3 +194,44 @@ def test_reference_build_not_interposed_by_our_library(hp, golden):
     M.close()
     assert res["niters"] == c["runs"]["150"]["niters"]
     assert res["normr"] == unhex(c["runs"]["150"]["normr"])
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="reference build only in the dev container")
+def test_degenerate_starts_match_reference():
+    """Pins the oracle on the degenerate starts tests/test_gpu_edge.py checks
+    the GPU against (HPCCG.cpp:347-386): a zero initial residual (no
+    iteration), the 0/0 path under a negative tolerance (niters 2, NaN), NaN
+    in b or x0 (no iteration), an infinite x0 entry on an interior row and on
+    a face row (no iteration either: p = x + 0.0 x, HPCCG.cpp:347 through
+    waxpby.cpp:77, is NaN there), and an infinite b entry (r0 = b - A x0 holds
+    inf, r0.r0 = inf > 0: k = 1 forms p = r + 0.0 r, NaN, and the NaN path
+    ends at niters 2). Same niters, normr bitwise or both NaN, x bitwise with
+    NaN in the same places."""
+    import math
+    nx, ny, nz = 9, 11, 7
+    M, _, b, _ = oracle.ref_generate(nx, ny, nz)
+    A = oracle.generate(nx, ny, nz)
+    n = A.nrow
+    interior = (nz // 2) * nx * ny + (ny // 2) * nx + nx // 2
+    face = (nz // 2) * nx * ny + (ny // 2) * nx + nx - 1  # the x = nx-1 face
+    bn = b.copy()
+    bn[n // 3] = np.nan
+    xn = np.zeros(n)
+    xn[n // 2 + 7] = np.nan
+    xi = np.zeros(n)
+    xi[interior] = np.inf
+    xf = np.zeros(n)
+    xf[face] = np.inf
+    bi = b.copy()
+    bi[face] = -np.inf
+    todo = [("exact", b, np.ones(n), 30, 0.0, 0), ("zero_rhs", np.zeros(n), np.zeros(n), 30, 0.0, 0),
+            ("exact_negtol", b, np.ones(n), 30, -1.0, 2), ("nan_b", bn, np.zeros(n), 30, 0.0, 0),
+            ("nan_x0", b, xn, 30, 0.0, 0), ("inf_interior", b, xi, 30, 0.0, 0), ("inf_face", b, xf, 30, 0.0, 0),
+            ("inf_b", bi, np.zeros(n), 30, 0.0, 2)]
+    for name, bb, x0, mi, tol, want in todo:
+        ref = oracle.ref_hpccg(M, bb, max_iter=mi, tolerance=tol, x=x0)
+        got = oracle.hpccg(A, b=bb, x=x0, max_iter=mi, tolerance=tol)
+        assert ref["niters"] == got["niters"] == want, name
+        assert (math.isnan(ref["normr"]) and math.isnan(got["normr"])) or ref["normr"] == got["normr"], name
+        assert np.array_equal(ref["x"], got["x"], equal_nan=True), name
+    M.close()
