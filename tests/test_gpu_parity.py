@@ -441,9 +441,12 @@ def _oracle_trace(dims, s7, iters):
 @pytest.mark.parametrize("dims,s7,trace_iters", [((100, 100, 100), False, 90),
                                                   ((200, 200, 200), False, 60),
                                                   ((256, 256, 256), True, 60),
-                                                  ((320, 320, 320), False, 0)])
+                                                  ((320, 320, 320), False, 0),
+                                                  ((432, 432, 432), False, 0)])
 def test_full_size(hp, gpu, dims, s7, trace_iters, record_property):
-    """BASELINE sizes (and 320^3: 32.8 M rows, 0.88 G nonzeros) on the default
+    """BASELINE sizes (and 320^3: 32.8 M rows, 0.88 G nonzeros; 432^3: 80.6 M
+    rows, 2.167 G nonzeros and 2.18 G A-image slots, past 2^31 -- every slot and
+    nonzero count and offset 64-bit) on the default
     kernel: the first iterations' rtrans against the oracle on the same matrix
     (1e-8) -- the unmodified reference build (oracle/_ref) at sampled
     iterations where it is present, and the C restatement's full trace --,
