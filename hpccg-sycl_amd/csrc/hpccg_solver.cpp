@@ -2666,6 +2666,20 @@ int persist_autotest(hpccg_hip_matrix* M, int* local_ok)
     return 0;
 }
 
+// The reference's residual lines (HPCCG.cpp:342-344, 356, 372-373) from the
+// solve's trace, rank 0 only.
+void print_trace(const hpccg_hip_matrix* M, int niters, int max_iter)
+{
+    if (M->rank != 0) return;
+    int pf = max_iter / 10;
+    if (pf > 50) pf = 50;
+    if (pf < 1) pf = 1;
+    std::cout << "Initial Residual = " << M->trace[0] << std::endl;
+    for (int k = 1; k <= niters; k++)
+        if (k % pf == 0 || k + 1 == max_iter)
+            std::cout << "Iteration = " << k << "   Residual = " << M->trace[k] << std::endl;
+}
+
 // After a failed solve: every dot slot empty again, the
 // error record cleared, so the next solve starts from the allocation state.
 int reset_dot_state(hpccg_hip_matrix* M)
@@ -3020,15 +3034,7 @@ int solve_ranks(hpccg_hip_matrix* const* Ms, int P, const double* const* b_dev, 
         M->ktimes[2] = up;
         M->ktimes[3] = niters + 1;
     }
-    if (print && M->rank == 0) {
-        int pf = max_iter / 10;
-        if (pf > 50) pf = 50;
-        if (pf < 1) pf = 1;
-        std::cout << "Initial Residual = " << M->trace[0] << std::endl;
-        for (int k = 1; k <= niters; k++)
-            if (k % pf == 0 || k + 1 == max_iter)
-                std::cout << "Iteration = " << k << "   Residual = " << M->trace[k] << std::endl;
-    }
+    if (print) print_trace(M, niters, max_iter);
     if (times) {
         const std::vector<unsigned long long> st(stamps, stamps + nstamps);
         stamps_to_times(st, max_iter, times);
@@ -4020,27 +4026,53 @@ int hpccg_hip_solve_device(hpccg_hip_matrix* M, const double* b_dev, double* x_d
     return wait_matrix(M);
 }
 
-int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tolerance, int* niters,
-                    double* normr, double* times, int print)
+namespace {
+
+// The caller's b and x into d_b / d_x: pageable copies straight from the
+// caller's memory (the runtime moves them at ~56 GB/s on the box; a pinned
+// stage filled by host threads measured 1-3 % slower per solve at 100^3 and
+// 200^3, its extra host copy costing more than it saved).
+int upload_host(hpccg_hip_matrix* M, const double* b, const double* x, bool with_b)
 {
-    if (!M || !b || !x || !niters || !normr) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
-    HIP_TRY(hipSetDevice(M->device));
-    const auto t0 = std::chrono::steady_clock::now();
-    HIP_TRY(hipMemcpyAsync(M->d_b, b, sizeof(double) * M->nrow, hipMemcpyHostToDevice, M->stream));
+    if (with_b) HIP_TRY(hipMemcpyAsync(M->d_b, b, sizeof(double) * M->nrow, hipMemcpyHostToDevice, M->stream));
     HIP_TRY(hipMemcpyAsync(M->d_x, x, sizeof(double) * M->nrow, hipMemcpyHostToDevice, M->stream));
     HIP_TRY(hipStreamSynchronize(M->stream));
+    return 0;
+}
+
+int download_x(hpccg_hip_matrix* M, double* x)
+{
+    HIP_TRY(hipMemcpy(x, M->d_x, sizeof(double) * M->nrow, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// hpccg_hip_solve up to (not including) the copy of x back to the caller
+int solve_host(hpccg_hip_matrix* M, const double* b, const double* x, int max_iter, double tolerance, int* niters,
+               double* normr, double* times, int print)
+{
+    HIP_TRY(hipSetDevice(M->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    TRY(upload_host(M, b, x, true));
     const double setup = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     int rc = solve_impl(M, M->d_b, M->d_x, max_iter, tolerance, niters, normr, times, print);
     if (resident_retry(M, rc)) {  // from the caller's x again
-        HIP_TRY(hipMemcpyAsync(M->d_x, x, sizeof(double) * M->nrow, hipMemcpyHostToDevice, M->stream));
-        HIP_TRY(hipStreamSynchronize(M->stream));
+        TRY(upload_host(M, b, x, false));
         rc = solve_impl(M, M->d_b, M->d_x, max_iter, tolerance, niters, normr, times, print);
         resident_rearm(M);
     }
     TRY(rc);
-    HIP_TRY(hipMemcpy(x, M->d_x, sizeof(double) * M->nrow, hipMemcpyDeviceToHost));
     if (times) times[6] = setup;
     return 0;
+}
+
+}  // namespace
+
+int hpccg_hip_solve(hpccg_hip_matrix* M, const double* b, double* x, int max_iter, double tolerance, int* niters,
+                    double* normr, double* times, int print)
+{
+    if (!M || !b || !x || !niters || !normr) return set_err(HPCCG_HIP_EINVAL, "NULL argument");
+    TRY(solve_host(M, b, x, max_iter, tolerance, niters, normr, times, print));
+    return download_x(M, x);
 }
 
 int hpccg_hip_diag_spmv(hpccg_hip_matrix* M, int kernel, int reps, double* avg_us)
@@ -4452,7 +4484,33 @@ int hpccg_hip_HPCCG(HPC_Sparse_Matrix* A, double* b, double* x, int max_iter, do
                        "A has local_ncol %d != local_nrow %d: it has been through make_local_matrix (local column "
                        "indices); pass the matrix with global column indices",
                        A->local_ncol, A->local_nrow);
+    // A cached image is solved on at once, while host threads fingerprint A
+    // (~23 ms at 200^3, 12 % of the solve); x is written back only if the
+    // fingerprint still matches -- otherwise A changed since it was cached, and
+    // the image is rebuilt and the solve run again from the caller's x.
     hpccg_hip_matrix* M = nullptr;
+    unsigned long long cached_fp = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_dropin_mu);
+        auto it = g_dropin_cache.find(A);
+        // (the sizes first: the speculative solve reads nrow values of b and x)
+        if (it != g_dropin_cache.end() && it->second.M->nrow == A->local_nrow &&
+            it->second.M->start_row == A->start_row && it->second.M->total_nrow == A->total_nrow)
+            M = it->second.M, cached_fp = it->second.fp;
+    }
+    if (M) {
+        unsigned long long fp = 0;
+        std::thread fth([&] { fp = fingerprint(A); });
+        const int rc = solve_host(M, b, x, max_iter, tolerance, niters, normr, times, 0);
+        fth.join();
+        if (fp == cached_fp) {
+            TRY(rc);
+            print_trace(M, *niters, max_iter);
+            return download_x(M, x);
+        }
+        (void)hipGetLastError();
+        g_err.clear();
+    }
     double setup = 0.0;
     {
         std::lock_guard<std::mutex> lk(g_dropin_mu);

@@ -75,3 +75,32 @@ def test_dropin_new_matrix_same_address(hp, gpu):
         A = prob.A
         prob.close()  # hpccg_free_problem -> destroyMatrix -> hpccg_hip_dropin_release
         assert hp.lib().hpccg_hip_dropin_cached(A) == 0  # hpccg_free_problem -> destroyMatrix -> hpccg_hip_dropin_release
+
+
+def test_dropin_prints_one_solve(hp, gpu, capfd):
+    """A repeated call solves on the cached image while host threads
+    fingerprint A (the fingerprint hidden under the solve); x and the
+    reference's residual lines come out only once the fingerprint matched. An
+    in-place edit found that way re-solves on a fresh image: the caller still
+    sees ONE set of residual lines (HPCCG.cpp:356, 372-373), the edited
+    matrix's."""
+    prob = hp.generate_matrix(10, 9, 8)
+    x = prob.x
+    hp.dropin_HPCCG(prob, x, max_iter=50)  # builds and caches the image
+    capfd.readouterr()
+    x2 = prob.x
+    _, it, nr, _ = hp.dropin_HPCCG(prob, x2, max_iter=50)  # cached: the speculative path
+    out = capfd.readouterr().out
+    assert out.count("Initial Residual") == 1 and out.count("Iteration = 49 ") == 1
+    assert np.array_equal(x, x2)
+    A = prob.A.contents
+    nnz = int(sum(A.nnz_in_row[i] for i in range(A.local_nrow)))
+    vals = np.ctypeslib.as_array(A.list_of_vals, (nnz,))
+    vals *= 4.0
+    x3 = prob.x
+    _, it3, nr3, _ = hp.dropin_HPCCG(prob, x3, max_iter=50)
+    out = capfd.readouterr().out
+    assert out.count("Initial Residual") == 1, out
+    assert np.max(np.abs(x3 - 0.25)) <= 1e-12  # the edited matrix's solution, not the stale image's
+    vals /= 4.0
+    hp.lib().hpccg_hip_dropin_release(prob.A)
