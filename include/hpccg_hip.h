@@ -359,6 +359,9 @@ int hpccg_hip_waxpby(int n, double alpha, const double* x_dev, double beta, cons
  * matrix (cached per A: keyed by the address AND a fingerprint of the sizes,
  * row lengths, column indices and values, so a matrix re-created at the same
  * address or edited in place is converted again), then runs hpccg_hip_solve.
+ * On a cached image the solve starts at once and the fingerprint is taken
+ * beside it; x and the residual lines are written only once it matched (else
+ * the image is rebuilt and the solve re-run from the caller's x).
  * A localised matrix (local_ncol > local_nrow) is refused (HPCCG_HIP_EPLAN). */
 int hpccg_hip_HPCCG(struct HPC_Sparse_Matrix_STRUCT* A, double* b, double* x, int max_iter,
                     double tolerance, int* niters, double* normr, double* times);
