@@ -729,8 +729,51 @@ def secondary_config(hp, torch, n, stencil, dev, args, world=1, dist=None, rank=
         M.close()
 
 
+def host_boundary(hp, n, stencil, max_iter, solves=3):
+    """The rate a caller of the reference's own interface sees (DESIGN.md 8,
+    "The host boundary, measured"): HPCCG() through the C drop-in
+    hpccg_hip_HPCCG (HPCCG.hpp:61-63) on a host HPC_Sparse_Matrix with host b
+    and x -- device image cached by the first call, so each timed call is the
+    PCIe copies of b and x plus the solve. Informational, never `value`. The
+    drop-in prints the reference's residual lines (HPCCG.cpp:356, 372-373):
+    stdout is pointed at stderr meanwhile, so the bench line stays the only
+    stdout line."""
+    import ctypes as C
+    import numpy as np
+    prob = hp.generate_matrix(n, n, n, use_7pt=stencil == 7)
+    L = hp.lib()
+    b = np.ascontiguousarray(prob.b)
+    ni, nrm = C.c_int(0), C.c_double(0.0)
+    times = np.zeros(7)
+    walls, x = [], None
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        for i in range(solves + 1):
+            x = prob.x
+            t0 = time.perf_counter()
+            rc = L.hpccg_hip_HPCCG(prob.A, b.ctypes.data, x.ctypes.data, max_iter, 0.0, C.byref(ni), C.byref(nrm),
+                                   times.ctypes.data_as(C.POINTER(C.c_double)))
+            hp._check(rc, "hpccg_hip_HPCCG")
+            walls.append(time.perf_counter() - t0)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+    err = float(np.max(np.abs(x - 1.0)))
+    prob.close()
+    w = float(np.median(walls[1:]))
+    return {"value": round(ni.value / w, 1), "unit": "CG iterations/s",
+            "interface": "hpccg_hip_HPCCG (the reference's HPCCG() signature) on a host HPC_Sparse_Matrix, host b and x",
+            "solves": solves, "median_wall_ms": round(w * 1e3, 3), "first_call_ms": round(walls[0] * 1e3, 1),
+            "niters": ni.value, "x_minus_xexact_inf": err,
+            "note": "PCIe copies of b and x included (device image cached by the first call, whose time includes "
+                    "building it); informational, never value"}
+
+
 def build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt, ranks, cpu, secondary,
-               probe_report, trace_check=None):
+               probe_report, trace_check=None, host_rate=None):
     """The one JSON line (pure: the CPU suite checks its schema for N > 1)."""
     it_per_s = meas["niters_total"] / meas["elapsed"]  # per rank: every rank runs the same iterations
     value = it_per_s * world
@@ -798,6 +841,8 @@ def build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt
     }
     if trace_check is not None:
         out["check"]["trace_vs_oracle"] = trace_check
+    if host_rate is not None:
+        out["host_boundary"] = host_rate
     if world > 1:
         out["multirank"] = multirank_summary(ranks, roof["bytes_per_launch"])
     if secondary is not None:
@@ -814,6 +859,8 @@ def main():
     ap.add_argument("--stencil", type=int, default=27, choices=[27, 7])
     ap.add_argument("--max-iter", type=int, default=500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-boundary", action="store_true",
+                    help="N = 1: skip the host-interface rate (hpccg_hip_HPCCG with host b and x)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the other configs (N = 1: 27-pt 100^3, 7-pt 256^3; N > 1: 27-pt 100^3 per GPU)")
     ap.add_argument("--no-trace-check", action="store_true",
@@ -924,6 +971,15 @@ def main():
         rt["distinct_devices"] = 1
     M.close()
 
+    host_rate = None
+    if world == 1 and not args.no_host_boundary:
+        try:
+            stage("host_boundary_run")
+            host_rate = host_boundary(hp, n, args.stencil, args.max_iter)
+            stage("host_boundary", value=host_rate["value"])
+        except Exception as e:  # reported, never silently dropped
+            host_rate = {"error": repr(e)}
+
     secondary, sec_traces = None, {}
     if not args.no_secondary:
         secondary = []
@@ -989,7 +1045,7 @@ def main():
             if not args.no_trace_check:
                 secondary[i]["check"]["trace_vs_oracle"] = trace_record(f"secondary{i}", tr2, n2, n2 * world, st2)
         out = build_line(args, world, n, meas, roof, kernel, kfmt, fused, info, M_opts, rt, ranks, cpu, secondary,
-                         placement_report(args.placement, probe_us, pick), tchk)
+                         placement_report(args.placement, probe_us, pick), tchk, host_rate)
         retries = [meas["chk"][2]] + [s_["check"]["resident_retries_max_over_ranks"] for s_ in (secondary or [])
                                        if "check" in s_]
         if not ok_all:

@@ -11,7 +11,7 @@ for cfg in "${cfgs[@]}"; do
   for rep in $(seq ${REPS:-3}); do
     for which in new ${LIBS:-base}; do
       if [ $which = new ]; then unset HPCCG_HIP_LIB; else export HPCCG_HIP_LIB=$PWD/lib_$which/libhpccg_hip.so; fi
-      timeout -k 10 200 python bench.py $cfg --no-cpu-baseline --no-trace-check --steps ${STEPS:-10} $EXTRA > gpurun_out/abl/one.json \
+      timeout -k 10 200 python bench.py $cfg --no-cpu-baseline --no-trace-check --no-host-boundary --steps ${STEPS:-10} $EXTRA > gpurun_out/abl/one.json \
           2>> gpurun_out/abl/err.log || { tail -20 gpurun_out/abl/err.log; exit 1; }
       python3 -c "
 import json; d = json.load(open('gpurun_out/abl/one.json'))

@@ -5,7 +5,7 @@ export TMPDIR=/tmp; mkdir -p gpurun_out/abo; : > gpurun_out/abo/bench.log
 IFS=';' read -ra CASES <<< "$AB_CASES"
 for rep in 1 2; do
   for c in "${CASES[@]}"; do
-    timeout -k 10 200 python bench.py $c --no-cpu-baseline --no-trace-check --steps ${STEPS:-10} > gpurun_out/abo/one.json 2>> gpurun_out/abo/bench.err || exit 1
+    timeout -k 10 200 python bench.py $c --no-cpu-baseline --no-trace-check --no-host-boundary --steps ${STEPS:-10} > gpurun_out/abo/one.json 2>> gpurun_out/abo/bench.err || exit 1
     python3 - "$c" <<'PY' >> gpurun_out/abo/bench.log
 import json, sys
 d = json.load(open("gpurun_out/abo/one.json"))

@@ -4,7 +4,7 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out/abr; : > gpurun_out/abr/summary.log
 for rep in $(seq ${REPS:-2}); do
   for v in ${SHAPES:-0 1 -1}; do
-    timeout -k 10 200 python bench.py --n ${N:-100} --no-cpu-baseline --no-trace-check --no-secondary --steps ${STEPS:-10} \
+    timeout -k 10 200 python bench.py --n ${N:-100} --no-cpu-baseline --no-trace-check --no-host-boundary --no-secondary --steps ${STEPS:-10} \
         --set resident_update=$v > gpurun_out/abr/one.json 2>> gpurun_out/abr/err.log || exit 1
     python3 -c "
 import json; d = json.load(open('gpurun_out/abr/one.json'))

@@ -9,7 +9,7 @@ export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out/pmr
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 \
     --master-port 29711 tests/hostcomm_worker.py gpurun_out/pmr > gpurun_out/pmr/worker.log 2>&1 || exit 1
-timeout -k 10 300 python bench.py --n 80 --steps 10 --no-secondary --no-cpu-baseline --no-trace-check \
+timeout -k 10 300 python bench.py --n 80 --steps 10 --no-secondary --no-cpu-baseline --no-trace-check --no-host-boundary \
     > gpurun_out/pmr/single80.json 2> gpurun_out/pmr/single80.err || exit 1
 python3 - <<'PY'
 import json
