@@ -513,6 +513,10 @@ def measure(hp, torch, M, dev, max_iter, steps, warmup, event_steps, world, dist
             dist.barrier()
 
     cold_s = None
+    # the ranks start their first solve together: its in-kernel waits for the
+    # other ranks' contributions are bounded (spin_budget_us), so setup skew
+    # between ranks must not eat into them
+    barrier()
     for i in range(warmup):
         t0 = time.perf_counter()
         step(i == 0)
