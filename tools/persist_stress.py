@@ -8,6 +8,7 @@ resident retry). Every rank solves each size `--solves` times and compares
 
     python -m torch.distributed.run --nproc-per-node 2 tools/persist_stress.py OUT [--solves 200]
     python -m torch.distributed.run --nproc-per-node 8 tools/persist_stress.py OUT --dims 16,16,16
+    python tools/persist_stress.py OUT --dims 100,100,100 --solves 1000     (one rank)
 
 Writes OUT/stress_rank<r>.json; rank 0 prints a one-line summary."""
 import argparse
@@ -32,13 +33,20 @@ def main():
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
-    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
     hp = load_pkg()
     dev = 0
     torch.cuda.set_device(dev)
     hp.set_device(dev)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    hp.comm_init_host(world, rank)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        hp.comm_init_host(world, rank)
+    else:  # one process (python tools/persist_stress.py OUT): the single-rank launches
+        class _One:
+            @staticmethod
+            def barrier():
+                pass
+        dist = _One
     res = {"rank": rank, "world": world, "cases": {}}
     for spec in args.dims.split(";"):
         dims = tuple(int(v) for v in spec.split(","))
@@ -81,8 +89,9 @@ def main():
                           "resident_update": cs[0]["resident_update"], "us_per_iter": round(cs[0]["us_per_iter"], 2),
                           "x_err_max": max(c["x_err"] for c in cs)}
         print(json.dumps(summ), flush=True)
-    hp.comm_destroy()
-    dist.destroy_process_group()
+    if world > 1:
+        hp.comm_destroy()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
