@@ -14,6 +14,13 @@ namespace hpccg {
 constexpr int kSliceRows = 512;
 constexpr int kNumXcd = 8;  // MI355X: 8 XCDs, blocks dealt round-robin
 constexpr int kReadyStride = 16;  // doubles between the fused update's p.Ap ready slots (128 B)
+// The persistent launch's broadcast copies of each dot total (blocks poll copy
+// blockIdx % kPersBcast): 64 copies measured +0.1-0.2 % over one per XCD at
+// 100^3, 12 alternating runs (profiles/r06_ab/persist_bcast_copies_ab100.log)
+#ifndef HPCCG_BCAST
+#define HPCCG_BCAST 64
+#endif
+constexpr int kPersBcast = HPCCG_BCAST;
 
 // Indices into the device scalar block (g = scal[0..], loc = scal[2..]).
 // kRRPar: with the fused update (a.fupd) r.r is also kept in two slots by the
@@ -249,14 +256,14 @@ int resident_capacity(bool nt);
 // capacity, the launch, and the slot fill (kSlotEmpty) that precedes it
 constexpr int kResidentPersist = 6;
 constexpr int kResidentAuto = 8;  // resident_update -1: the persistent launch with the 3-slot LDS ring
-constexpr int kPersistWindow = 512;  // iterations per persistent launch (its slots: 17 MB at 100^3)
+constexpr int kPersistWindow = 512;  // iterations per persistent launch (its slots: 24 MB at 100^3)
 int persist_capacity(bool nt);
 void launch_cg_persist(const CgArgs& a, hipStream_t s);
 void launch_fill_empty(double* p, long long n, hipStream_t s);
 // slots per iteration of the persistent launch
 inline long long persist_slot_stride(int nslices)
 {
-    return 2LL * nslices + 2LL * ((nslices + 63) / 64) + 2LL * kNumXcd * kReadyStride;
+    return 2LL * nslices + 2LL * ((nslices + 63) / 64) + 2LL * kPersBcast * kReadyStride;
 }
 void launch_cg_update(const CgArgs& a, bool prologue, hipStream_t s);
 void launch_cg_stamp(const CgArgs& a, int slot, bool prologue, hipStream_t s);

@@ -1548,7 +1548,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 // block keeps its rows' x, r_{k-1} and p_{k-1} in registers (x += alpha p_k
 // there: no deferred-x side blocks, x stored once at the end), and the two
 // dots of every iteration complete through slots of their own (a.pslots:
-// iteration k's slice partials, group sums and kNumXcd broadcast copies of the
+// iteration k's slice partials, group sums and kPersBcast broadcast copies of the
 // total, all emptied before the launch), so no slot is reused within the
 // launch. Neighbour values of r_{k-1} and p_{k-1} are read with sc1 buffer
 // loads (L1 bypassed: another CU rewrote them during this launch) after the
@@ -1596,7 +1596,7 @@ __device__ __forceinline__ void st_rs(__amdgpu_buffer_rsrc_t rs, int byte, int r
 }
 
 // Iteration k's slots: [which][nslices] partials, [which][ngroups] group sums,
-// [which][kNumXcd x kReadyStride] broadcast copies of the total.
+// [which][kPersBcast x kReadyStride] broadcast copies of the total.
 __device__ __forceinline__ double* pers_slots(const CgArgs& a, int k)
 {
     return a.pslots + (size_t)(k - a.pk0) * a.pslot_stride;  // (the launch's window starts at pk0)
@@ -1604,7 +1604,7 @@ __device__ __forceinline__ double* pers_slots(const CgArgs& a, int k)
 __device__ __forceinline__ double* pers_bcast(const CgArgs& a, int k, int which)
 {
     const int ng = ngroups_of(a);
-    return pers_slots(a, k) + 2 * a.nslices + 2 * ng + which * kNumXcd * kReadyStride;
+    return pers_slots(a, k) + 2 * a.nslices + 2 * ng + which * kPersBcast * kReadyStride;
 }
 
 // complete_dot_lanes' slot protocol on iteration k's own slots (no resets):
@@ -1672,7 +1672,7 @@ __device__ __forceinline__ void pers_dot(const CgArgs& a, int role, int s0, int 
         if (__shfl(bad, 0, kWave)) return;  // (the solve was given up: the waiters see the error record)
     }
     tot = __shfl(tot, 0, kWave);
-    if (lane < kNumXcd) st_sc1(pers_bcast(a, k, which) + kReadyStride * lane, tot);  // the 8 copies at once
+    if (lane < kPersBcast) st_sc1(pers_bcast(a, k, which) + kReadyStride * lane, tot);  // the copies at once
     if (lane == 0) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
 }
 
@@ -1680,12 +1680,12 @@ __device__ __forceinline__ void pers_dot(const CgArgs& a, int role, int s0, int 
 // Returns false when the solve was abandoned.
 __device__ __forceinline__ bool pers_wait(const CgArgs& a, int k, int which, double& out, bool stall)
 {
-    const double* slot = pers_bcast(a, k, which) + kReadyStride * (blockIdx.x % kNumXcd);
+    const double* slot = pers_bcast(a, k, which) + kReadyStride * (blockIdx.x % kPersBcast);
     unsigned t0 = 0, polls = 0;
     double v;
     while (!slot_full(v = ld_sc1(slot)) || stall) {
         if ((++polls & 15) == 0 && wait_expired(a, t0)) {
-            abort_solve(a, kErrReadyWait, blockIdx.x % kNumXcd, k, which);
+            abort_solve(a, kErrReadyWait, blockIdx.x % kPersBcast, k, which);
             return false;
         }
         __builtin_amdgcn_s_sleep(1);
