@@ -21,6 +21,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <system_error>
 #include <unordered_map>
 #include <vector>
 
@@ -4500,9 +4501,14 @@ int hpccg_hip_HPCCG(HPC_Sparse_Matrix* A, double* b, double* x, int max_iter, do
     }
     if (M) {
         unsigned long long fp = 0;
-        std::thread fth([&] { fp = fingerprint(A); });
+        std::thread fth;
+        try {
+            fth = std::thread([&] { fp = fingerprint(A); });
+        } catch (const std::system_error&) {  // no thread to spare: fingerprint first
+            fp = fingerprint(A);
+        }
         const int rc = solve_host(M, b, x, max_iter, tolerance, niters, normr, times, 0);
-        fth.join();
+        if (fth.joinable()) fth.join();
         if (fp == cached_fp) {
             TRY(rc);
             print_trace(M, *niters, max_iter);
