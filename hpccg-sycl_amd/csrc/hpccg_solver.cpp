@@ -20,8 +20,8 @@
 #include <map>
 #include <mutex>
 #include <string>
-#include <thread>
 #include <system_error>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
