@@ -26,6 +26,42 @@ sys.path.insert(0, HERE)
 from conftest import RTRANS_RTOL_MULTI, check_final, check_trace, kat2_rr0, load_pkg, solve_case, unhex  # noqa: E402
 
 
+FUZZ_SEED = 2606
+FUZZ_CASES = 16
+
+
+def fuzz_cases(seed=FUZZ_SEED, count=FUZZ_CASES):
+    """(i, (nx, ny, nz per rank), 7-pt?, max_iter) for the 2-process fuzz:
+    thin and odd slabs, 1- and 2-wide axes, both stencils, short and long
+    solves, sizes from one slice up to ones whose two ranks' pair blocks
+    no longer fit the GPU together (the per-iteration launches then)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        s7 = bool(rng.integers(2))
+        nx, ny = (int(v) for v in rng.integers(1, 41, size=2))
+        nz = int(rng.integers(1, 25))
+        if i % 5 == 1:
+            nx = 1
+        elif i % 5 == 2:
+            ny = 2
+        out.append((i, (nx, ny, nz), s7, int(rng.integers(1, 151))))
+    # and three larger slabs: 2 x 240 pair blocks (persistent across the
+    # processes), 2 x 563 (more than the GPU holds at once: the per-iteration
+    # launches), 7-pt 2 x 74^3
+    for j, (dims, s7, it) in enumerate((((64, 64, 60), False, 120), ((80, 80, 90), False, 60),
+                                        ((74, 74, 74), True, 90))):
+        out.append((count + j, dims, s7, it))
+    return out
+
+
+def fuzz_x0(n, rank):
+    """A nonzero x0 of this rank's rows, a function of the global row: the
+    in-process group builds the same vectors."""
+    g = np.arange(n, dtype=np.float64) + rank * n
+    return 0.125 * (np.remainder(g * 7.0, 11.0) - 5.0)
+
+
 def main():
     import torch
     import torch.distributed as dist
@@ -95,6 +131,23 @@ def main():
 
     if len(sys.argv) > 2 and sys.argv[2] == "eight":
         case("golden27x8", lambda: golden_case("27pt_16x16x16_x8ranks"))
+        return finish(res, out_dir, rank, hp, dist)
+    if len(sys.argv) > 2 and sys.argv[2] == "fuzz":
+        # seeded random 2-process cases (tests/test_gpu_hostcomm.py::test_hostcomm_fuzz
+        # solves each with the in-process group and the oracle)
+        for i, dims, s7, max_iter in fuzz_cases():
+            def one(dims=dims, s7=s7, max_iter=max_iter, i=i):
+                M = hp.Matrix.generate(*dims, use_7pt=s7)
+                b, _, _ = M.vectors()
+                n = M.info()["nrow"]
+                x = torch.from_numpy(fuzz_x0(n, rank)).to(f"cuda:{dev}")
+                _, it, nr, _ = hp.HPCCG(M, b, x, max_iter=max_iter, device=True)
+                np.savez(os.path.join(out_dir, f"fuzz_c{i}_rank{rank}.npz"), trace=M.last_trace().copy(),
+                         x=x.cpu().numpy())
+                out = {"transport": transport(M), "niters": it, "normr": nr.hex()}
+                M.close()
+                return out
+            case(f"fuzz{i}", one)
         return finish(res, out_dir, rank, hp, dist)
     case("golden27", lambda: golden_case("27pt_8x8x8_x2ranks"))
     case("golden7", lambda: golden_case("7pt_12x10x8_x2ranks"))

@@ -255,6 +255,68 @@ def test_hostcomm_collective_fallback_verdict(hostcomm):
     assert "failed on purpose" in cs[1]["refused"]
 
 
+@pytest.fixture(scope="module")
+def hostcomm_fuzz(tmp_path_factory, gpu):
+    """One 2-process launch runs every fuzz case (hostcomm_worker.py fuzz)."""
+    out = tmp_path_factory.mktemp("hostcomm_fuzz")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    port = 29300 + os.getpid() % 250
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), WORKER, str(out), "fuzz"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-4000:]
+    res = []
+    for q in range(2):
+        with open(out / f"rank{q}.json") as f:
+            res.append(json.load(f))
+    return out, res
+
+
+def _fuzz_ids():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from hostcomm_worker import fuzz_cases
+    return fuzz_cases()
+
+
+@pytest.mark.parametrize("case", _fuzz_ids(), ids=lambda c: f"c{c[0]}")
+def test_hostcomm_fuzz(hostcomm_fuzz, hp, gpu, case):
+    """Seeded random cases across two processes (thin and odd slabs, 1-wide
+    axes, both stencils, 1-150 iterations, a nonzero x0; sizes up to ones
+    whose two ranks no longer fit the GPU together): the default transport --
+    the persistent launch across the processes where it was kept, else the
+    per-iteration launches -- bitwise the in-process group's solve (same
+    kernels' sums in rank order) and, through it, the oracle's serial solve of
+    the z-stacked global problem (niters, rtrans within RTRANS_RTOL_MULTI)."""
+    import torch
+    import oracle
+    from conftest import RTRANS_RTOL_MULTI, check_trace
+    from hostcomm_worker import fuzz_x0
+    out, res = hostcomm_fuzz
+    i, (nx, ny, nz), s7, max_iter = case
+    cs = _case(res, f"fuzz{i}")
+    assert cs[0]["niters"] == cs[1]["niters"] and cs[0]["normr"] == cs[1]["normr"]
+    if (nx, ny, nz, s7) == (64, 64, 60, False):  # 2 x 240 pair blocks: the persistent launch across them
+        assert all(c["transport"]["resident_update"] == 8 for c in cs), cs[0]["transport"]
+    if (nx, ny, nz, s7) == (80, 80, 90, False):  # 2 x 563: more than the GPU holds at once
+        assert all(c["transport"]["resident_update"] == 0 for c in cs), cs[0]["transport"]
+    n = nx * ny * nz
+    Ms = hp.group_generate(nx, ny, nz, 2, use_7pt=s7)
+    xs = [torch.from_numpy(fuzz_x0(n, r)).to(gpu) for r in range(2)]
+    _, it, nr, _ = hp.group_HPCCG(Ms, [M.vectors()[0] for M in Ms], xs, max_iter=max_iter)
+    tr = Ms[0].last_trace()
+    for M in Ms:
+        M.close()
+    assert cs[0]["niters"] == it and float.fromhex(cs[0]["normr"]) == nr, (cs[0]["transport"], it, nr)
+    for q in range(2):
+        d = np.load(out / f"fuzz_c{i}_rank{q}.npz")
+        assert d["trace"].tobytes() == tr.tobytes(), (q, cs[q]["transport"])
+        assert d["x"].tobytes() == xs[q].cpu().numpy().tobytes(), (q, cs[q]["transport"])
+    A = oracle.generate(nx, ny, 2 * nz, use_7pt=s7)
+    ref = oracle.hpccg(A, x=np.concatenate([fuzz_x0(n, 0), fuzz_x0(n, 1)]), max_iter=max_iter)
+    assert it == ref["niters"]
+    check_trace(tr, ref["trace"], RTRANS_RTOL_MULTI)
+
+
 def test_hostcomm_eight_processes_golden(tmp_path, gpu):
     """Eight processes on one GPU -- the world size of the driver's 8-GPU run --
     through the default transport: every rank maps the seven other mailboxes
