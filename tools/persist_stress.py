@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--solves", type=int, default=200)
     ap.add_argument("--dims", default="40,36,30;80,80,80", help="';'-separated nx,ny,nz per rank")
     ap.add_argument("--max-iter", type=int, default=500)
+    ap.add_argument("--stencil", type=int, default=27)
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -50,7 +51,7 @@ def main():
     res = {"rank": rank, "world": world, "cases": {}}
     for spec in args.dims.split(";"):
         dims = tuple(int(v) for v in spec.split(","))
-        M = hp.Matrix.generate(*dims)
+        M = hp.Matrix.generate(*dims, use_7pt=args.stencil == 7)
         b, _, _ = M.vectors()
         n = M.info()["nrow"]
         x = torch.zeros(n, dtype=torch.float64, device=f"cuda:{dev}")
