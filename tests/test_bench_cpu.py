@@ -58,8 +58,8 @@ def _worker(rank, world, port, q):
                     "traffic": 2.04e9, "bytes_per_launch": 2.05e9, "avg_launch_us": 340.0}
             cpu = {"value": 12.0, "unit": "CG iterations/s (global-problem iterations x 2 slabs)", "cores": 16,
                    "kind": "reference", "sample": "synthetic"}
-            opts = dict(transport, device_bytes=4.2e9, fuse_p=1, fold=1, x_defer=2, x_ring=32, rev_update=1,
-                        overlap=0, graph_chunk=32, nt=1, a2_ring=3, nt_store=0)
+            opts = dict(transport, device_bytes=4.2e9, fuse_p=1, fold=1, x_defer=2, x_ring=32, graph_chunk=32, nt=1,
+                        a2_ring=3, nt_store=0)
             tchk = bench.rtrans_check([1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125], [1.0, 0.5, 0.25, 0.125, 0.0625,
                                                                                    0.03125], bench.RTRANS_RTOL_MULTI)
             sec = [{"workload": "HPCCG solve, 27-pt 100x100x100 per GPU, z-stacked", "value": 44000.0,
