@@ -57,6 +57,10 @@ secondary: the other configs of BASELINE.json measured in the same run the
   weak-scaled like the headline (north_star's second size at 1/2/4/8 GPUs):
   value, launch time, compulsory-byte fraction, committed PMC traffic ratio,
   its own trace check; no CPU leg.
+host_boundary (N = 1): the rate a caller of the reference's own HPCCG()
+  interface sees -- the C drop-in hpccg_hip_HPCCG on a host HPC_Sparse_Matrix
+  with host b and x (PCIe copies included; the device image cached by a first,
+  untimed call); informational, never value.
 
 Multi-GPU runs describe themselves: every rank logs its stages on stderr
 (comm init, setup, first solve, timed steps), the line carries what RCCL
