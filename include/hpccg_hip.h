@@ -245,8 +245,8 @@ int hpccg_hip_last_trace(const hpccg_hip_matrix* M, double* out, int cap);
  * get only: "has_sell", "has_a", "has_pairs", "a_width", "lds_doubles", "nt",
  * "nt_store", "halo_mode", "num_external", "group_fold" (the last in-process
  * group solve summed its dots in its members' kernels), "resident_retries",
- * "peer_auto_ok", "pull_auto_ok", "proto_auto_ok" (the creation-time
- * self-tests' verdicts), "placement_pick", "device_bytes" (device memory M
+ * "peer_auto_ok", "pull_auto_ok", "proto_auto_ok", "persist_auto_ok" (the
+ * creation-time self-tests' verdicts), "placement_pick", "device_bytes" (device memory M
  * holds). None of the options changes a computed value: every kernel, fusion
  * and fold setting gives the same bits. Variants that measured even or slower
  * than these defaults were removed. */
