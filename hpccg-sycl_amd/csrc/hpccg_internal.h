@@ -15,10 +15,11 @@ constexpr int kSliceRows = 512;
 constexpr int kNumXcd = 8;  // MI355X: 8 XCDs, blocks dealt round-robin
 constexpr int kReadyStride = 16;  // doubles between the fused update's p.Ap ready slots (128 B)
 // The persistent launch's broadcast copies of each dot total (blocks poll copy
-// blockIdx % kPersBcast): 64 copies measured +0.1-0.2 % over one per XCD at
-// 100^3, 12 alternating runs (profiles/r06_ab/persist_bcast_copies_ab100.log)
+// blockIdx % kPersBcast): at 100^3, 64 copies measured +0.1-0.2 % over one per
+// XCD (12 alternating runs), 128 another +0.25 % over 64 (13 runs, two
+// sessions), 256 -0.25 % (profiles/r06_ab/persist_bcast_copies_ab100.log)
 #ifndef HPCCG_BCAST
-#define HPCCG_BCAST 64
+#define HPCCG_BCAST 128
 #endif
 constexpr int kPersBcast = HPCCG_BCAST;
 
@@ -256,7 +257,7 @@ int resident_capacity(bool nt);
 // capacity, the launch, and the slot fill (kSlotEmpty) that precedes it
 constexpr int kResidentPersist = 6;
 constexpr int kResidentAuto = 8;  // resident_update -1: the persistent launch with the 3-slot LDS ring
-constexpr int kPersistWindow = 512;  // iterations per persistent launch (its slots: 24 MB at 100^3)
+constexpr int kPersistWindow = 512;  // iterations per persistent launch (its slots: 32 MB at 100^3)
 int persist_capacity(bool nt);
 void launch_cg_persist(const CgArgs& a, hipStream_t s);
 void launch_fill_empty(double* p, long long n, hipStream_t s);

@@ -1672,7 +1672,7 @@ __device__ __forceinline__ void pers_dot(const CgArgs& a, int role, int s0, int 
         if (__shfl(bad, 0, kWave)) return;  // (the solve was given up: the waiters see the error record)
     }
     tot = __shfl(tot, 0, kWave);
-    if (lane < kPersBcast) st_sc1(pers_bcast(a, k, which) + kReadyStride * lane, tot);  // the copies at once
+    for (int c = lane; c < kPersBcast; c += kWave) st_sc1(pers_bcast(a, k, which) + kReadyStride * c, tot);
     if (lane == 0) stamp(a, k, which == kRR ? kStampFinRR : kStampFinPAP);
 }
 
